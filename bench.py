@@ -1,0 +1,180 @@
+"""Benchmark: Raft group-steps/sec (BASELINE.json metric) on MI355X.
+
+One step = one tick of every group: client append of E
+entries to the leader (main.go:327-329), one leader replication round to all
+R-1 peers through their AppendEntries handlers (main.go:334-379, 121-156),
+the commit rule (main.go:381-391) and the election timers — one fused kernel
+launch per tick, state read from and written back to HBM every tick.
+
+Workload at N=1: SURVEY config C2 — 2^20 independent 5-replica groups,
+steady-state AppendEntries + commitIndex, one client entry per tick, seeded
+synthetic trace. For N>1 each rank owns 2^20 groups (weak scaling; groups
+shard by id, no data-path collective); the per-tick statistics are summed
+across GPUs with RCCL inside the engine.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raft-sample_amd"))
+
+R_DEFAULT = 5
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(R, E):
+    """minimal SoA bytes per group-step, REF steady state:
+    B(R,E) = 25 + 37(R-1) + 12 E R (233 B at R=5, E=1)."""
+    return 25 + 37 * (R - 1) + 12 * E * R
+
+
+def cpu_baseline(args, R, E):
+    """The oracle (C restatement of main.go's handlers, oracle/) timed on the
+    host cores on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    G, T = args.cpu_groups, args.cpu_ticks
+    o = oracle.Oracle(replicas=R, groups=G, ring_depth=32, client_period=1, entries_per_tick=E,
+                      seed=0x5EED0002)
+    o.init_steady(0, 0)
+    t0 = time.perf_counter()
+    o.tick(1, T, threads=threads)
+    dt = time.perf_counter() - t0
+    o.close()
+    return {"value": G * T / dt, "unit": "group-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{G} groups x {T} ticks, R={R}, E={E}, steady state from init_steady, "
+                      f"{threads} pthreads over contiguous group ranges ({dt:.2f} s)"}
+
+
+def load_pmc(workload):
+    """HBM traffic per launch from a committed rocprofv3 --pmc summary for
+    this workload (tools/pmc_summary.py), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--groups-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--replicas", type=int, default=R_DEFAULT)
+    ap.add_argument("--entries", type=int, default=1)
+    ap.add_argument("--ring-depth", type=int, default=32)
+    ap.add_argument("--leader", type=int, default=0, help="steady-state leader replica (-1: hashed per group)")
+    ap.add_argument("--cpu-groups", type=int, default=131072)
+    ap.add_argument("--cpu-ticks", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from raftstep import Engine, STAT_NAMES
+
+    R, E, G = args.replicas, args.entries, args.groups_per_gpu
+    eng = Engine(replicas=R, groups=G, group_base=rank * G, ring_depth=args.ring_depth,
+                 entries_per_tick=E, client_period=1, seed=0x5EED0002, device=local)
+    if dist is not None:
+        uid = [Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(world, rank, uid[0])
+    eng.init_steady(args.leader, 0)
+
+    tick = 1
+    if args.warmup:
+        eng.tick(tick, args.warmup, stats=True)
+        tick += args.warmup
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    eng.profile(True)
+    barrier()
+    t0 = time.perf_counter()
+    stats = eng.tick(tick, args.steps, stats=True)   # K fused tick launches + per-tick stats (+RCCL sum)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms, launches = eng.profile_read()
+    eng.profile(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_steps = G * world * args.steps
+    value = total_steps / elapsed
+    # correctness guard on the timed run: the steady state commits exactly one
+    # entry per group per tick and never faults
+    expect_commit = G * world * args.steps * E
+    ok = stats[STAT_NAMES.index("committed")] == expect_commit and stats[STAT_NAMES.index("faults")] == 0
+
+    B = algorithmic_bytes(R, E)
+    avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)
+    achieved = B * G / avg_kernel_s / 1e9
+    workload = f"C2: {G} x {R}-replica groups per GPU, steady-state AppendEntries+commit, E={E}"
+    traffic = load_pmc(workload)
+    result = {
+        "metric": "Raft group-steps/sec at 1M 5-replica groups, 1-8 GPUs; % of HBM peak",
+        "value": value,
+        "unit": "group-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (seeded splitmix64 trace; post-election steady state, SURVEY.md §8(d) C2)",
+        "config": {"workload": workload, "groups_per_gpu": G, "groups_total": G * world, "replicas": R,
+                   "entries_per_tick": E, "ring_depth": args.ring_depth, "leader": args.leader,
+                   "semantics": "REF (main.go)", "parallelism": f"group-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "bytes_per_group_step": B, "avg_kernel_us": avg_kernel_s * 1e6, "launches": launches},
+        "stats": dict(zip(STAT_NAMES, [int(x) for x in stats])),
+        "stats_check": bool(ok),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, R, E)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    if not ok:
+        raise SystemExit("bench: steady-state statistics check failed")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,242 @@
+/*
+ * raftstep.h — C-ABI of the MI355X-native batched Raft step engine.
+ *
+ * This is the drop-in boundary for the hot path of eastwd/raft-sample:
+ * the RequestVote / AppendEntries handlers and the leader commit logic of
+ * main.go (FollowerRun main.go:111-180, CandidateRun main.go:193-287,
+ * LeaderRun main.go:304-397). The reference has no exported API: its
+ * handlers are inline `select` cases over `*Node` (main.go:14-39) and the
+ * message structs (main.go:42-49, 182-191, 289-302). Each entry point below
+ * names the reference code it replaces; INTEGRATION.md shows the cgo stub a
+ * maintainer adds to main.go's package to call it.
+ *
+ * Rules of the ABI:
+ *  - plain C types only; no torch / HIP types in any signature;
+ *  - every function returns 0 on success or a negative errno-style code
+ *    (RAFT_E*); the message is available from raft_last_error();
+ *  - caller-owned host buffers are only borrowed for the duration of a call
+ *    (cgo pointer rules: nothing is retained after return);
+ *  - one engine = one GPU = one host thread at a time (not re-entrant).
+ *
+ * Semantics are the reference's ("REF") bit for bit,
+ * including its quirks; where the reference would panic or deadlock the
+ * group is frozen with a per-group fault code instead of killing the process.
+ */
+#ifndef RAFTSTEP_H
+#define RAFTSTEP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RAFT_ABI_VERSION 1u
+#define RAFT_MAX_REPLICAS 8u
+
+/* Node.State (main.go:51-57). */
+enum raft_role { RAFT_FOLLOWER = 0, RAFT_CANDIDATE = 1, RAFT_LEADER = 2 };
+
+/* Per-group fault codes. The reference panics or blocks forever instead;
+ * the engine freezes the group from that point on (no further state change). */
+enum raft_fault {
+  RAFT_F_NONE = 0,
+  RAFT_F_PANIC_GETLOG = 1,        /* GetLog(i) out of range: main.go:142 -> 403-405 */
+  RAFT_F_DEADLOCK_VRES = 2,       /* candidate answers a VoteRequest into its own VRes: main.go:242 */
+  RAFT_F_DEADLOCK_LEADER_VREQ = 3,/* leader has no VReq case: main.go:308-332 */
+  RAFT_F_RING_EVICTED = 4,        /* EXT: entry older than the ring depth K was needed */
+  RAFT_F_OVERFLOW = 5             /* EXT: a term/index would leave int32 (Go int is 64-bit) */
+};
+
+enum raft_semantics { RAFT_SEM_REF = 0 };
+
+/* Error codes (negative returns). */
+#define RAFT_OK 0
+#define RAFT_EINVAL (-22)
+#define RAFT_ENOMEM (-12)
+#define RAFT_ERANGE (-34)
+#define RAFT_ENODEV (-19)
+#define RAFT_EHIP (-1000)
+#define RAFT_ERCCL (-2000)
+
+/* Statistics of one or more ticks (summed over groups, and over GPUs once a
+ * communicator is attached). Index names: */
+enum raft_stat {
+  RAFT_STAT_COMMITTED = 0,      /* sum of leader CommitIndex advances (main.go:389) */
+  RAFT_STAT_ELECTIONS_WON = 1,  /* candidate -> leader (main.go:273-282) */
+  RAFT_STAT_TERM_BUMPS = 2,     /* election timeouts, Term++ (main.go:176, 250) */
+  RAFT_STAT_AE_OK = 3,          /* AppendEntries answered Success:true */
+  RAFT_STAT_AE_FAIL = 4,        /* AppendEntries answered false (or dropped, EXT) */
+  RAFT_STAT_VOTES_GRANTED = 5,  /* VoteResponse vote:true */
+  RAFT_STAT_FAULTS = 6,         /* groups that faulted during the tick(s) */
+  RAFT_STAT_LEADER_GROUPS = 7,  /* groups with >=1 leader at the end of each tick (summed over ticks) */
+  RAFT_NSTATS = 8
+};
+typedef struct raft_tick_stats { int64_t v[RAFT_NSTATS]; } raft_tick_stats;
+
+/* Engine configuration. Zero-initialise, then set fields; see
+ * raft_config_default(). Virtual time: one tick = tick_seconds virtual
+ * seconds (the leader heartbeat period, main.go:394). */
+typedef struct raft_config {
+  uint32_t abi_version;        /* = RAFT_ABI_VERSION */
+  uint32_t replicas;           /* R = len(Nodes), 1..8 (main.go:81 uses 3) */
+  uint64_t groups;             /* independent Raft groups on this engine */
+  uint64_t group_base;         /* global id of local group 0 (sharding across GPUs) */
+  uint32_t ring_depth;         /* K: log entries kept per replica, power of two */
+  uint32_t entries_per_tick;   /* E: client entries appended per client event (main.go:92) */
+  uint32_t client_period;      /* ticks between client events; 0 = no client */
+  uint32_t semantics;          /* RAFT_SEM_REF */
+  uint64_t seed;               /* trace seed (splitmix64 counter RNG) */
+  int32_t tick_seconds;        /* 2 (main.go:394) */
+  int32_t follower_timeout_min;   /* 10 s  (main.go:114: rand.Intn(20)+10) */
+  int32_t follower_timeout_span;  /* 20    */
+  int32_t candidate_timeout_min;  /* 10 s  (main.go:194: rand.Intn(4)+10) */
+  int32_t candidate_timeout_span; /* 4     */
+  uint32_t isolate_per_65536;  /* EXT: probability (x/65536) per 32-tick epoch that one replica is isolated */
+  uint32_t isolate_min_ticks;  /* EXT: isolation length range, 1..32 */
+  uint32_t isolate_max_ticks;
+  int32_t device;              /* HIP device ordinal */
+  uint32_t reserved[8];
+} raft_config;
+
+/* Canonical host view of engine state, group-major:
+ *   per-replica arrays are indexed [g*R + r], match is [(g*R + leader)*R + peer],
+ *   log arrays are [(g*R + r)*K + slot] where log index i (1-based) lives at
+ *   slot (i-1) mod K and only i in (max(0,last-K), last] is meaningful (other
+ *   slots read back as 0). match rows of replicas that are not leaders read
+ *   back as 0. Any pointer may be NULL on store (field skipped). */
+typedef struct raft_state_view {
+  uint8_t* role;      /* Node.State (main.go:16) */
+  uint8_t* voted;     /* Node.Voted (main.go:20) */
+  int32_t* term;      /* Node.Term (main.go:19) */
+  int32_t* last;      /* Node.LastApplied == len(Node.Log) (main.go:25, 148-149, 328-329) */
+  int32_t* commit;    /* Node.CommitIndex (main.go:24) */
+  int32_t* deadline;  /* election timer deadline, virtual seconds */
+  int32_t* timeout;   /* current timer duration d, seconds (main.go:114, 194) */
+  int32_t* match;     /* Node.MatchIndex (main.go:29); NextIndex == MatchIndex+1 (main.go:280-281, 376-377) */
+  uint8_t* fault;     /* per group, enum raft_fault */
+  int32_t* log_term;  /* Log.Term (main.go:47) */
+  int64_t* log_value; /* Log.Value (main.go:48) */
+} raft_state_view;
+
+typedef struct raft_engine raft_engine;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+void raft_config_default(raft_config* cfg);
+int raft_engine_create(const raft_config* cfg, raft_engine** out);
+int raft_engine_destroy(raft_engine* e);
+const char* raft_last_error(void);              /* thread-local message of the last failure */
+int raft_engine_info(const raft_engine* e, raft_config* cfg_out, uint64_t* device_bytes);
+
+/* NewNode x R for every group (main.go:59-76) followed by FollowerRun entry
+ * (timer drawn, main.go:113-115) at virtual tick `tick0`. */
+int raft_init_new_nodes(raft_engine* e, int64_t tick0);
+/* Post-election state (KAT-1 generalised): replica `leader` (or a per-group
+ * hashed replica when leader < 0) is Leader with Term 1, the others are
+ * Followers with Term 1 and Voted, MatchIndex 0 / NextIndex 1, empty logs. */
+int raft_init_steady(raft_engine* e, int32_t leader, int64_t tick0);
+
+int raft_load_state(raft_engine* e, const raft_state_view* v);
+int raft_store_state(raft_engine* e, raft_state_view* v);
+
+/* ---- the fused tick (the metric path) -----------------------------------
+ * Advances every group by `nticks` ticks starting at virtual tick
+ * `first_tick`. One tick per kernel launch; per tick and group, in order:
+ *   1. client append to leaders (main.go:87-93 -> 327-329),
+ *   2. replicas in ascending id: leader replication round + commit
+ *      (main.go:332-391) / candidate vote round (main.go:253-284), every
+ *      message delivered through the receiver's handler,
+ *   3. election timers that expired, in (deadline, id) order, each followed
+ *      at once by the new candidate's vote round (main.go:171-177, 248-251).
+ * `out` (may be NULL) receives the stats summed over the ticks. */
+int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_stats* out);
+int raft_sync(raft_engine* e);
+
+/* ---- message-level handlers (drop-in for the select cases) --------------
+ * Batched: element i is applied to group reqs[i].group; all groups of one
+ * batch must be distinct (RAFT_EINVAL otherwise). `now_tick` is the virtual
+ * time used for timer resets / redraws. */
+typedef struct raft_log_entry { int64_t term; int64_t value; } raft_log_entry; /* Log (main.go:46-49) */
+
+typedef struct raft_ae_req {     /* AppendEntriesRequest (main.go:289-296) */
+  uint64_t group;
+  uint32_t to;                   /* receiving replica */
+  uint32_t leader_id;            /* LeaderId (routing only) */
+  int64_t term;                  /* Term */
+  int64_t prev_log_index;        /* PrevLogIndex */
+  int64_t prev_log_term;         /* PrevLogTerm */
+  int64_t leader_commit;         /* LeaderCommit */
+  uint64_t entries_offset;       /* Logs = entries[entries_offset .. +n_entries) */
+  uint64_t n_entries;
+} raft_ae_req;
+typedef struct raft_ae_resp {    /* AppendEntriesResponse (main.go:298-302) */
+  int64_t term;
+  int64_t match_index;
+  int32_t success;
+  int32_t fault;                 /* enum raft_fault raised while handling (0 = none) */
+} raft_ae_resp;
+/* FollowerRun case AEReq (main.go:121-156), CandidateRun case AEReq
+ * (main.go:200-223), LeaderRun case AEReq (main.go:309-326), dispatched on
+ * the receiver's State like Run (main.go:98-109). */
+int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_req* reqs, size_t n,
+                              const raft_log_entry* entries, size_t n_entries_total, raft_ae_resp* out);
+
+typedef struct raft_vote_req {   /* VoteRequest (main.go:182-187) */
+  uint64_t group;
+  uint32_t to;
+  uint32_t candidate_id;         /* CandidateId (routing only) */
+  int64_t term;
+  int64_t last_log_index;        /* never read by the reference (main.go:185-186, 264) */
+  int64_t last_log_term;
+} raft_vote_req;
+typedef struct raft_vote_resp {  /* VoteResponse (main.go:188-191) */
+  int64_t term;
+  int32_t vote_granted;
+  int32_t fault;
+} raft_vote_resp;
+/* FollowerRun case VReq (main.go:157-170), CandidateRun case VReq
+ * (main.go:224-246); a leader has no VReq case (main.go:308) -> fault. */
+int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_req* reqs, size_t n,
+                            raft_vote_resp* out);
+
+/* Whole-node steps, batched over distinct groups. */
+enum raft_op_kind {
+  RAFT_OP_CLIENT_APPEND = 1,   /* LeaderRun case LogReq (main.go:327-329); arg = Value */
+  RAFT_OP_LEADER_ROUND = 2,    /* LeaderRun default: AE to each peer + commit (main.go:332-391) */
+  RAFT_OP_CANDIDATE_ROUND = 3, /* CandidateRun default: vote round + tally (main.go:253-284) */
+  RAFT_OP_TIMEOUT = 4,         /* timer.C: follower -> candidate / candidate Term++ (main.go:171-177, 248-251) */
+  RAFT_OP_LEADER_COMMIT = 5    /* commit rule alone (main.go:381-391) */
+};
+typedef struct raft_group_op {
+  uint64_t group;
+  uint32_t replica;
+  uint32_t kind;
+  int64_t arg;
+} raft_group_op;
+typedef struct raft_op_result {
+  int32_t status;   /* 0 applied; RAFT_EINVAL if the replica's State does not run this step */
+  int32_t fault;    /* group fault code after the op */
+  int64_t value;    /* CommitIndex after LEADER_ROUND/LEADER_COMMIT; 1 if elected by CANDIDATE_ROUND */
+} raft_op_result;
+int raft_group_ops_batch(raft_engine* e, int64_t now_tick, const raft_group_op* ops, size_t n,
+                         raft_op_result* out);
+
+/* ---- multi-GPU statistics (RCCL over xGMI) -------------------------------
+ * Groups shard by id (config.group_base); the only collective is the sum of
+ * tick statistics. Rank 0 creates the id and distributes it out of band. */
+int raft_comm_unique_id(uint8_t id_out[128]);
+int raft_comm_init(raft_engine* e, int nranks, int rank, const uint8_t id[128]);
+/* All-reduce `stats` (in/out) over the communicator (sum); no-op without one. */
+int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats);
+
+/* ---- instrumentation -----------------------------------------------------
+ * When enabled, every tick launch is bracketed by HIP events on the engine
+ * stream; raft_profile_read() syncs and returns the summed kernel time. */
+int raft_profile_enable(raft_engine* e, int enable);
+int raft_profile_read(raft_engine* e, double* total_ms, uint64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAFTSTEP_H */

@@ -1,0 +1,162 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes handle over liboracle.so, the CPU
+restatement of main.go (see raft_oracle.h). Imported only by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker.
+
+Mirrors raftstep.Engine's methods so parity tests can drive both the same way.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.normpath(os.path.join(_HERE, "..", "raft-sample_amd")))
+from raftstep import abi  # noqa: E402  (record layouts of the boundary only)
+
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+P = C.c_void_p
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def load(path=None):
+    global _lib
+    if _lib is None or path:
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            build()
+        lib = C.CDLL(p)
+        sig = {
+            "oracle_create": (P, [P]),
+            "oracle_destroy": (None, [P]),
+            "oracle_init_new_nodes": (None, [P, C.c_int64]),
+            "oracle_init_steady": (None, [P, C.c_int32, C.c_int64]),
+            "oracle_load_state": (C.c_int, [P, P]),
+            "oracle_store_state": (None, [P, P]),
+            "oracle_tick": (None, [P, C.c_int64, C.c_uint32, C.c_int, P]),
+            "oracle_append_entries": (C.c_int, [P, C.c_int64, P, C.c_size_t, P, P]),
+            "oracle_request_vote": (C.c_int, [P, C.c_int64, P, C.c_size_t, P]),
+            "oracle_group_ops": (C.c_int, [P, C.c_int64, P, C.c_size_t, P]),
+            "oracle_rng": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64]),
+            "oracle_client_value": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]),
+            "oracle_timer_draw": (C.c_int32, [P, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64]),
+            "oracle_isolated": (C.c_int, [P, C.c_uint64, C.c_uint32, C.c_int64]),
+            "oracle_steady_leader": (C.c_uint32, [P, C.c_uint64, C.c_int32]),
+            "oracle_nodelog": (C.c_int, [P, C.c_uint64, C.c_char_p, C.c_size_t]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data if a is not None and a.size else None
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc != 0:
+        raise OracleError(f"oracle error {rc}")
+
+
+class Oracle:
+    def __init__(self, cfg=None, **kw):
+        self.lib = load()
+        self.cfg = cfg if cfg is not None else abi.default_config(**kw)
+        self.h = self.lib.oracle_create(C.byref(self.cfg))
+        if not self.h:
+            raise OracleError("oracle_create failed")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.oracle_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def init_new_nodes(self, tick0=0):
+        self.lib.oracle_init_new_nodes(self.h, tick0)
+
+    def init_steady(self, leader=0, tick0=0):
+        self.lib.oracle_init_steady(self.h, leader, tick0)
+
+    def store_state(self, logs=True):
+        st = abi.empty_state(self.cfg.groups, self.cfg.replicas, self.cfg.ring_depth)
+        if not logs:
+            st.pop("log_term")
+            st.pop("log_value")
+        v = abi.make_view(st)
+        self.lib.oracle_store_state(self.h, C.byref(v))
+        return st
+
+    def load_state(self, st):
+        st = {k: np.ascontiguousarray(st[k]) for k in abi.STATE_FIELDS}
+        v = abi.make_view(st)
+        _check(self.lib.oracle_load_state(self.h, C.byref(v)))
+
+    def tick(self, first_tick, nticks=1, stats=True, threads=1):
+        s = abi.TickStats()
+        self.lib.oracle_tick(self.h, first_tick, nticks, threads, C.byref(s))
+        return np.array(s.v, dtype=np.int64) if stats else None
+
+    def append_entries(self, now_tick, reqs, entries=None):
+        reqs = np.ascontiguousarray(reqs, dtype=abi.AE_REQ)
+        ents = np.ascontiguousarray(entries if entries is not None else np.zeros(0, abi.LOG_ENTRY),
+                                    dtype=abi.LOG_ENTRY)
+        out = np.zeros(len(reqs), abi.AE_RESP)
+        _check(self.lib.oracle_append_entries(self.h, now_tick, _ptr(reqs), len(reqs), _ptr(ents), _ptr(out)))
+        return out
+
+    def request_vote(self, now_tick, reqs):
+        reqs = np.ascontiguousarray(reqs, dtype=abi.VOTE_REQ)
+        out = np.zeros(len(reqs), abi.VOTE_RESP)
+        _check(self.lib.oracle_request_vote(self.h, now_tick, _ptr(reqs), len(reqs), _ptr(out)))
+        return out
+
+    def group_ops(self, now_tick, ops):
+        ops = np.ascontiguousarray(ops, dtype=abi.GROUP_OP)
+        out = np.zeros(len(ops), abi.OP_RESULT)
+        _check(self.lib.oracle_group_ops(self.h, now_tick, _ptr(ops), len(ops), _ptr(out)))
+        return out
+
+    def nodelog(self, group):
+        buf = C.create_string_buffer(4096)
+        n = self.lib.oracle_nodelog(self.h, group, buf, 4096)
+        return buf.value[:max(n, 0)].decode()
+
+    # trace definition helpers
+    def rng(self, gid, replica, stream, tick):
+        return self.lib.oracle_rng(self.cfg.seed, gid, replica, stream, tick)
+
+    def client_value(self, gid, replica, tick, e):
+        return self.lib.oracle_client_value(self.cfg.seed, gid, replica, tick, e)
+
+    def timer_draw(self, gid, replica, role, tick):
+        return self.lib.oracle_timer_draw(C.byref(self.cfg), gid, replica, role, tick)
+
+    def isolated(self, gid, replica, tick):
+        return bool(self.lib.oracle_isolated(C.byref(self.cfg), gid, replica, tick))
+
+    def steady_leader(self, gid, leader):
+        return self.lib.oracle_steady_leader(C.byref(self.cfg), gid, leader)

@@ -1,0 +1,671 @@
+/*
+ * raft_oracle.c — TEST INFRASTRUCTURE ONLY (see raft_oracle.h).
+ *
+ * Plain-C restatement of eastwd/raft-sample main.go, one group at a time,
+ * array-of-structs, Go-slice logs. Every handler cites the main.go lines it
+ * restates. The only additions are the ones the tick model needs and the
+ * engine shares by definition:
+ *   - a virtual clock (1 tick = cfg.tick_seconds, main.go:394) replacing
+ *     time.Timer / time.Sleep;
+ *   - a counter RNG keyed by (seed, group, replica, stream, tick) replacing
+ *     math/rand (main.go:92, 114, 194);
+ *   - fault codes where Go would panic (main.go:142 -> 404) or block forever
+ *     (main.go:242, 265, 308), freezing the group;
+ *   - EXT: ring-depth visibility (RAFT_F_RING_EVICTED), int32 range
+ *     (RAFT_F_OVERFLOW), seeded isolation windows (dropped messages).
+ */
+#include "raft_oracle.h"
+
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define I32MAX 2147483647LL
+
+enum { ST_VALUE = 1, ST_TIMER_F = 2, ST_TIMER_C = 3, ST_ISOLATE = 4 };
+
+/* ---------------------------------------------------------------- RNG ---- */
+static uint64_t sm64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+uint64_t oracle_rng(uint64_t seed, uint64_t gid, uint32_t replica, uint32_t stream, uint64_t tick) {
+  uint64_t k = sm64(seed ^ sm64(gid));
+  uint64_t h = sm64(k ^ (((uint64_t)stream << 32) | replica));
+  return sm64(h ^ tick);
+}
+/* rand.Int() (main.go:92): uniform in [0, 2^63). */
+uint64_t oracle_client_value(uint64_t seed, uint64_t gid, uint32_t replica, uint64_t tick, uint32_t e) {
+  return sm64(oracle_rng(seed, gid, replica, ST_VALUE, tick) ^ (uint64_t)e) >> 1;
+}
+/* rand.Intn(20)+10 (main.go:114) / rand.Intn(4)+10 (main.go:194). */
+int32_t oracle_timer_draw(const raft_config* c, uint64_t gid, uint32_t replica, int role, uint64_t tick) {
+  int cand = role == RAFT_CANDIDATE;
+  uint64_t h = oracle_rng(c->seed, gid, replica, cand ? ST_TIMER_C : ST_TIMER_F, tick);
+  uint32_t span = (uint32_t)(cand ? c->candidate_timeout_span : c->follower_timeout_span);
+  int32_t mn = cand ? c->candidate_timeout_min : c->follower_timeout_min;
+  return mn + (int32_t)((uint32_t)(h >> 32) % span);
+}
+/* EXT isolation windows: per 32-tick epoch, with probability p/65536 one
+ * replica is cut off for [start, start+len) ticks (len <= 32). */
+int oracle_isolated(const raft_config* c, uint64_t gid, uint32_t replica, int64_t tick) {
+  if (c->isolate_per_65536 == 0 || tick < 0) return 0;
+  int64_t ep = tick >> 5;
+  for (int64_t e = ep; e >= ep - 1 && e >= 0; --e) {
+    uint64_t h = oracle_rng(c->seed, gid, 0, ST_ISOLATE, (uint64_t)e);
+    if ((h & 0xFFFF) >= c->isolate_per_65536) continue;
+    uint32_t victim = (uint32_t)((h >> 16) & 0xFF) % c->replicas;
+    int64_t start = e * 32 + (int64_t)((h >> 24) & 31);
+    uint32_t span = c->isolate_max_ticks - c->isolate_min_ticks + 1;
+    int64_t len = c->isolate_min_ticks + (int64_t)((uint32_t)(h >> 32) % span);
+    if (victim == replica && tick >= start && tick < start + len) return 1;
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------ state ---- */
+typedef struct { int64_t term, value; } o_ent;   /* Log (main.go:46-49) */
+
+typedef struct {                                 /* Node (main.go:14-39) */
+  int role;                                      /* State */
+  int voted;                                     /* Voted */
+  int64_t term;                                  /* Term */
+  int64_t last;                                  /* LastApplied == len(Log) */
+  int64_t commit;                                /* CommitIndex */
+  int64_t deadline, timeout;                     /* timer (virtual seconds) */
+  int64_t match[RAFT_MAX_REPLICAS];              /* MatchIndex; NextIndex = match+1 */
+  o_ent* log;
+  int64_t cap;
+} o_node;
+
+typedef struct {
+  o_node n[RAFT_MAX_REPLICAS];
+  int fault;
+} o_group;
+
+struct oracle {
+  raft_config cfg;
+  o_group* g;
+};
+
+typedef struct {                                 /* one handler invocation's context */
+  const raft_config* cfg;
+  uint64_t gid;
+  int64_t tick, now;
+  int64_t st[RAFT_NSTATS];
+  int drops;                                     /* EXT isolation active */
+} o_ctx;
+
+typedef struct {                                 /* AppendEntriesRequest (main.go:289-296) */
+  int64_t term, prev_idx, prev_term, lc;
+  const o_ent* ents;
+  int64_t n;
+} o_ae;
+typedef struct { int64_t term, match; int ok; } o_aer;  /* AppendEntriesResponse (main.go:298-302) */
+
+static void set_fault(o_group* G, int f) {
+  if (!G->fault) G->fault = f;
+}
+
+/* append(n.Log, ...) (main.go:148, 328): Go slices grow by doubling. */
+static void log_append(o_node* n, const o_ent* src, int64_t cnt) {
+  if (cnt <= 0) return;
+  if (n->last + cnt > n->cap) {
+    int64_t nc = n->cap ? n->cap : 8;
+    while (nc < n->last + cnt) nc *= 2;
+    n->log = (o_ent*)realloc(n->log, (size_t)nc * sizeof(o_ent));
+    n->cap = nc;
+  }
+  memmove(n->log + n->last, src, (size_t)cnt * sizeof(o_ent));
+  n->last += cnt;
+}
+
+/* GetLog(i) = Log[i-1] (main.go:403-405): panics outside [1, len]; the
+ * EXT ring-depth rule makes entries at or below last-K unreadable. */
+static int get_log_term(const o_ctx* c, o_group* G, const o_node* n, int64_t i, int64_t* out) {
+  if (i < 1 || i > n->last) { set_fault(G, RAFT_F_PANIC_GETLOG); return 0; }
+  if (i <= n->last - (int64_t)c->cfg->ring_depth) { set_fault(G, RAFT_F_RING_EVICTED); return 0; }
+  *out = n->log[i - 1].term;
+  return 1;
+}
+
+/* FollowerRun entry (main.go:111-115): draw d, start the timer. */
+static void enter_follower(const o_ctx* c, o_node* n, int x) {
+  n->role = RAFT_FOLLOWER;
+  n->timeout = oracle_timer_draw(c->cfg, c->gid, (uint32_t)x, RAFT_FOLLOWER, (uint64_t)c->tick);
+  n->deadline = c->now + n->timeout;
+}
+/* CandidateRun entry (main.go:193-195). */
+static void enter_candidate(const o_ctx* c, o_node* n, int x) {
+  n->role = RAFT_CANDIDATE;
+  n->timeout = oracle_timer_draw(c->cfg, c->gid, (uint32_t)x, RAFT_CANDIDATE, (uint64_t)c->tick);
+  n->deadline = c->now + n->timeout;
+}
+
+/* ------------------------------------------------ AppendEntries handlers */
+/* FollowerRun case r := <-n.AEReq (main.go:121-156). */
+static o_aer follower_ae(const o_ctx* c, o_group* G, int x, const o_ae* r) {
+  o_node* n = &G->n[x];
+  o_aer res = {n->term, n->last, 0};
+  n->deadline = c->now + n->timeout;                     /* 124-127: timer.Reset(d) */
+  if (r->term < n->term) return res;                     /* 129-133 */
+  if (n->last > 0) {                                     /* 135 */
+    if (n->last + r->n < r->prev_idx) return res;        /* 137-140 */
+    int64_t t;
+    if (!get_log_term(c, G, n, r->prev_idx, &t)) return res; /* 142: GetLog may panic */
+    if (t != r->prev_term) return res;                   /* 142-145 */
+  }
+  if (n->last + r->n > I32MAX) { set_fault(G, RAFT_F_OVERFLOW); return res; }
+  log_append(n, r->ents, r->n);                          /* 148-149 */
+  if (r->lc > n->commit)                                 /* 151-152: min(LC, len(Log)+1) */
+    n->commit = r->lc < n->last + 1 ? r->lc : n->last + 1;
+  n->term = r->term;                                     /* 155 */
+  res.term = n->term; res.match = n->last; res.ok = 1;   /* 156 */
+  return res;
+}
+/* CandidateRun case r := <-n.AEReq (main.go:200-223). */
+static o_aer candidate_ae(const o_ctx* c, o_group* G, int x, const o_ae* r) {
+  o_node* n = &G->n[x];
+  o_aer res = {n->term, n->last, 0};
+  if (r->term >= n->term) {                              /* 204 */
+    res.ok = 1;                                          /* 205-209: MatchIndex = LastApplied, nothing appended */
+    n->voted = 1;                                        /* 211 */
+    n->term = r->term;                                   /* 212 */
+    enter_follower(c, n, x);                             /* 210, 213-216 -> Run -> FollowerRun */
+  }
+  return res;                                            /* 219-223 */
+}
+/* LeaderRun case r := <-n.AEReq (main.go:309-326). */
+static o_aer leader_ae(const o_ctx* c, o_group* G, int x, const o_ae* r) {
+  o_node* n = &G->n[x];
+  o_aer res = {n->term, 0, 0};                           /* MatchIndex unset -> 0 */
+  if (r->term > n->term) {                               /* 312 */
+    res.ok = 1;                                          /* 313-316 */
+    n->voted = 0;                                        /* 318 */
+    n->term = r->term;                                   /* 319 */
+    enter_follower(c, n, x);                             /* 317, 320 */
+    memset(n->match, 0, sizeof n->match);
+  }
+  return res;
+}
+/* Run (main.go:98-109) dispatches the message to the receiver's role loop. */
+static o_aer deliver_ae(const o_ctx* c, o_group* G, int x, const o_ae* r) {
+  switch (G->n[x].role) {
+    case RAFT_FOLLOWER: return follower_ae(c, G, x, r);
+    case RAFT_CANDIDATE: return candidate_ae(c, G, x, r);
+    default: return leader_ae(c, G, x, r);
+  }
+}
+
+/* -------------------------------------------------- RequestVote handlers */
+/* Returns 1 if granted; sets a fault where the requester would block. */
+static int deliver_vr(const o_ctx* c, o_group* G, int x, int64_t rterm, int64_t* resp_term) {
+  o_node* n = &G->n[x];
+  *resp_term = n->term;
+  switch (n->role) {
+    case RAFT_FOLLOWER:                                  /* main.go:157-170 */
+      if (rterm < n->term || n->voted) return 0;         /* 160-162 (no timer reset) */
+      n->deadline = c->now + n->timeout;                 /* 164-167 */
+      n->term = rterm;                                   /* 168 */
+      n->voted = 1;                                      /* 169 */
+      *resp_term = n->term;
+      return 1;                                          /* 170 */
+    case RAFT_CANDIDATE:                                 /* main.go:224-246 */
+      if (rterm > n->term) {                             /* 227-238 */
+        n->voted = 1;
+        n->term = rterm;
+        enter_follower(c, n, x);
+        return 1;
+      }
+      /* 242: the rejection goes into the candidate's OWN VRes, the requester
+       * blocks at main.go:265 forever; 243-246 reset this candidate's timer. */
+      n->deadline = c->now + n->timeout;
+      set_fault(G, RAFT_F_DEADLOCK_VRES);
+      return 0;
+    default:                                             /* LeaderRun has no VReq case (main.go:308) */
+      set_fault(G, RAFT_F_DEADLOCK_LEADER_VREQ);
+      return 0;
+  }
+}
+
+/* ------------------------------------------------------- node steps ----- */
+static int dropped(const o_ctx* c, int a, int b) {
+  if (!c->drops) return 0;
+  return oracle_isolated(c->cfg, c->gid, (uint32_t)a, c->tick) ||
+         oracle_isolated(c->cfg, c->gid, (uint32_t)b, c->tick);
+}
+
+/* CandidateRun default branch (main.go:253-284). Returns 1 if elected. */
+static int candidate_round(o_ctx* c, o_group* G, int cand) {
+  const int R = (int)c->cfg->replicas;
+  o_node* n = &G->n[cand];
+  int count = 1;                                         /* 255 */
+  n->voted = 1;                                          /* 256 */
+  for (int p = 0; p < R; ++p) {                          /* 259-269 */
+    if (p == cand) continue;
+    if (dropped(c, cand, p)) continue;                   /* EXT */
+    int64_t rt;
+    int grant = deliver_vr(c, G, p, n->term, &rt);       /* 264-265 */
+    if (G->fault) return 0;
+    if (grant) { count++; c->st[RAFT_STAT_VOTES_GRANTED]++; } /* 266-268 */
+  }
+  if (2 * count > R) {                                   /* 273: float64(count) > float64(N)/2 */
+    n->role = RAFT_LEADER;                               /* 274 */
+    memset(n->match, 0, sizeof n->match);                /* 275-282: MatchIndex 0, NextIndex 1 */
+    c->st[RAFT_STAT_ELECTIONS_WON]++;
+    return 1;
+  }
+  return 0;
+}
+
+/* Commit rule (main.go:381-391): exact-value histogram of the peers'
+ * MatchIndex, leader excluded, no current-term rule. */
+static void leader_commit(o_ctx* c, o_group* G, int L) {
+  const int R = (int)c->cfg->replicas;
+  o_node* n = &G->n[L];
+  for (int p = 0; p < R; ++p) {                          /* 386: at most one value can qualify */
+    if (p == L) continue;
+    int cnt = 0;
+    for (int q = 0; q < R; ++q)                          /* 382-385 */
+      if (q != L && n->match[q] == n->match[p]) cnt++;
+    if (2 * cnt > R && n->match[p] > n->commit) {        /* 387 */
+      c->st[RAFT_STAT_COMMITTED] += n->match[p] - n->commit;
+      n->commit = n->match[p];                           /* 389 */
+    }
+  }
+}
+
+/* LeaderRun default branch (main.go:332-391). */
+static void leader_round(o_ctx* c, o_group* G, int L) {
+  const int R = (int)c->cfg->replicas;
+  o_node* n = &G->n[L];
+  for (int p = 0; p < R; ++p) {                          /* 334-379 */
+    if (p == L) continue;
+    if (dropped(c, L, p)) { c->st[RAFT_STAT_AE_FAIL]++; continue; }  /* EXT */
+    o_ae r;
+    r.term = n->term; r.lc = n->commit;
+    int64_t nxt = n->match[p] + 1;                       /* NextIndex == MatchIndex + 1 */
+    if (nxt <= n->last) {                                /* 341 */
+      if (nxt == 1) {                                    /* 343-351: whole log, PrevLogIndex 0 */
+        r.ents = n->log; r.n = n->last;
+        r.prev_term = n->term; r.prev_idx = 0;
+      } else {                                           /* 353-360 */
+        if (nxt < 1) { set_fault(G, RAFT_F_PANIC_GETLOG); return; }  /* GetLogsFrom(<1) panics */
+        int64_t pt;
+        if (!get_log_term(c, G, n, n->match[p], &pt)) return;       /* GetLog(MatchIndex) */
+        r.ents = n->log + (nxt - 1); r.n = n->last - nxt + 1;
+        r.prev_term = pt; r.prev_idx = n->match[p];
+      }
+    } else {                                             /* 364-371: heartbeat, PrevLogTerm = Term */
+      r.ents = NULL; r.n = 0;
+      r.prev_term = n->term; r.prev_idx = n->match[p];
+    }
+    o_aer res = deliver_ae(c, G, p, &r);                 /* 344/353/364 -> 373 */
+    if (G->fault) return;
+    if (res.ok) {                                        /* 375-378; response Term ignored */
+      n->match[p] = res.match;
+      c->st[RAFT_STAT_AE_OK]++;
+    } else {
+      c->st[RAFT_STAT_AE_FAIL]++;
+    }
+  }
+  leader_commit(c, G, L);
+}
+
+/* timer.C fires (main.go:171-177 follower, 248-251 candidate). */
+static void timeout_fire(o_ctx* c, o_group* G, int x) {
+  o_node* n = &G->n[x];
+  if (n->term >= I32MAX) { set_fault(G, RAFT_F_OVERFLOW); return; }
+  n->term++;                                             /* 176 / 250 */
+  c->st[RAFT_STAT_TERM_BUMPS]++;
+  enter_candidate(c, n, x);                              /* 175 / 251 -> CandidateRun */
+}
+
+/* LeaderRun case LogReq (main.go:327-329). */
+static void client_append(const o_ctx* c, o_group* G, int L, int64_t value) {
+  o_node* n = &G->n[L];
+  if (n->last >= I32MAX) { set_fault(G, RAFT_F_OVERFLOW); return; }
+  o_ent e = {n->term, value};
+  log_append(n, &e, 1);
+}
+
+/* One tick of one group. */
+static void tick_group(o_ctx* c, o_group* G) {
+  const int R = (int)c->cfg->replicas;
+  if (G->fault) return;
+  /* 1. client (main.go:87-93): every replica whose State is Leader */
+  if (c->cfg->client_period && c->tick % c->cfg->client_period == 0) {
+    for (int r = 0; r < R && !G->fault; ++r) {
+      if (G->n[r].role != RAFT_LEADER) continue;
+      for (uint32_t e = 0; e < c->cfg->entries_per_tick && !G->fault; ++e)
+        client_append(c, G, r, (int64_t)oracle_client_value(c->cfg->seed, c->gid, (uint32_t)r, (uint64_t)c->tick, e));
+    }
+  }
+  /* 2. rounds, ascending replica id */
+  for (int r = 0; r < R && !G->fault; ++r) {
+    if (G->n[r].role == RAFT_LEADER) leader_round(c, G, r);
+    else if (G->n[r].role == RAFT_CANDIDATE) candidate_round(c, G, r);
+  }
+  /* 3. expired timers in (deadline, id) order; a new candidate runs its
+   *    vote round at once (CandidateRun's default branch). */
+  for (int it = 0; it < R && !G->fault; ++it) {
+    int best = -1;
+    for (int r = 0; r < R; ++r) {
+      const o_node* n = &G->n[r];
+      if (n->role == RAFT_LEADER || n->deadline > c->now) continue;
+      if (best < 0 || n->deadline < G->n[best].deadline) best = r;
+    }
+    if (best < 0) break;
+    timeout_fire(c, G, best);
+    if (G->fault) break;
+    candidate_round(c, G, best);
+  }
+  if (G->fault) { c->st[RAFT_STAT_FAULTS]++; return; }
+  for (int r = 0; r < R; ++r)
+    if (G->n[r].role == RAFT_LEADER) { c->st[RAFT_STAT_LEADER_GROUPS]++; break; }
+}
+
+/* ------------------------------------------------------------- API ----- */
+oracle* oracle_create(const raft_config* cfg) {
+  if (!cfg || cfg->replicas < 1 || cfg->replicas > RAFT_MAX_REPLICAS) return NULL;
+  oracle* o = (oracle*)calloc(1, sizeof *o);
+  o->cfg = *cfg;
+  o->g = (o_group*)calloc(cfg->groups ? cfg->groups : 1, sizeof(o_group));
+  return o;
+}
+
+static void free_logs(oracle* o) {
+  for (uint64_t g = 0; g < o->cfg.groups; ++g)
+    for (uint32_t r = 0; r < o->cfg.replicas; ++r) {
+      free(o->g[g].n[r].log);
+      o->g[g].n[r].log = NULL; o->g[g].n[r].cap = 0;
+    }
+}
+
+void oracle_destroy(oracle* o) {
+  if (!o) return;
+  free_logs(o);
+  free(o->g);
+  free(o);
+}
+
+static o_ctx make_ctx(const oracle* o, uint64_t g, int64_t tick) {
+  o_ctx c;
+  memset(&c, 0, sizeof c);
+  c.cfg = &o->cfg;
+  c.gid = o->cfg.group_base + g;
+  c.tick = tick;
+  c.now = tick * o->cfg.tick_seconds;
+  c.drops = o->cfg.isolate_per_65536 != 0;
+  return c;
+}
+
+/* NewNode (main.go:59-76) + FollowerRun entry (main.go:113-115). */
+void oracle_init_new_nodes(oracle* o, int64_t tick0) {
+  free_logs(o);
+  for (uint64_t g = 0; g < o->cfg.groups; ++g) {
+    o_ctx c = make_ctx(o, g, tick0);
+    memset(&o->g[g], 0, sizeof(o_group));
+    for (uint32_t r = 0; r < o->cfg.replicas; ++r) enter_follower(&c, &o->g[g].n[r], (int)r);
+  }
+}
+
+uint32_t oracle_steady_leader(const raft_config* cfg, uint64_t gid, int32_t leader) {
+  if (leader >= 0) return (uint32_t)leader % cfg->replicas;
+  return (uint32_t)(sm64(cfg->seed ^ 0x1EADE5ULL ^ sm64(gid)) >> 33) % cfg->replicas;
+}
+
+/* KAT-1 generalised: the state right after the first election. */
+void oracle_init_steady(oracle* o, int32_t leader, int64_t tick0) {
+  free_logs(o);
+  for (uint64_t g = 0; g < o->cfg.groups; ++g) {
+    o_ctx c = make_ctx(o, g, tick0);
+    o_group* G = &o->g[g];
+    memset(G, 0, sizeof(o_group));
+    uint32_t L = oracle_steady_leader(&o->cfg, c.gid, leader);
+    for (uint32_t r = 0; r < o->cfg.replicas; ++r) {
+      o_node* n = &G->n[r];
+      n->term = 1; n->voted = 1;
+      if (r == L) { enter_candidate(&c, n, (int)r); n->role = RAFT_LEADER; }
+      else enter_follower(&c, n, (int)r);
+    }
+  }
+}
+
+int oracle_load_state(oracle* o, const raft_state_view* v) {
+  const uint32_t R = o->cfg.replicas, K = o->cfg.ring_depth;
+  free_logs(o);
+  for (uint64_t g = 0; g < o->cfg.groups; ++g) {
+    o_group* G = &o->g[g];
+    memset(G, 0, sizeof(o_group));
+    G->fault = v->fault[g];
+    for (uint32_t r = 0; r < R; ++r) {
+      uint64_t i = g * R + r;
+      o_node* n = &G->n[r];
+      n->role = v->role[i]; n->voted = v->voted[i];
+      n->term = v->term[i]; n->commit = v->commit[i];
+      n->deadline = v->deadline[i]; n->timeout = v->timeout[i];
+      for (uint32_t p = 0; p < R; ++p) n->match[p] = v->match[i * R + p];
+      int64_t last = v->last[i];
+      if (last < 0) return RAFT_EINVAL;
+      n->last = 0;
+      if (last > 0) {
+        o_ent* tmp = (o_ent*)calloc((size_t)last, sizeof(o_ent));
+        for (int64_t idx = last > K ? last - K + 1 : 1; idx <= last; ++idx) {
+          uint64_t s = i * K + (uint64_t)((idx - 1) & (K - 1));
+          tmp[idx - 1].term = v->log_term[s];
+          tmp[idx - 1].value = v->log_value[s];
+        }
+        log_append(n, tmp, last);
+        free(tmp);
+      }
+    }
+  }
+  return RAFT_OK;
+}
+
+void oracle_store_state(const oracle* o, raft_state_view* v) {
+  const uint32_t R = o->cfg.replicas, K = o->cfg.ring_depth;
+  for (uint64_t g = 0; g < o->cfg.groups; ++g) {
+    const o_group* G = &o->g[g];
+    if (v->fault) v->fault[g] = (uint8_t)G->fault;
+    for (uint32_t r = 0; r < R; ++r) {
+      uint64_t i = g * R + r;
+      const o_node* n = &G->n[r];
+      if (v->role) v->role[i] = (uint8_t)n->role;
+      if (v->voted) v->voted[i] = (uint8_t)n->voted;
+      if (v->term) v->term[i] = (int32_t)n->term;
+      if (v->last) v->last[i] = (int32_t)n->last;
+      if (v->commit) v->commit[i] = (int32_t)n->commit;
+      if (v->deadline) v->deadline[i] = (int32_t)n->deadline;
+      if (v->timeout) v->timeout[i] = (int32_t)n->timeout;
+      if (v->match)
+        for (uint32_t p = 0; p < R; ++p)
+          v->match[i * R + p] = (n->role == RAFT_LEADER && p != r) ? (int32_t)n->match[p] : 0;
+      for (uint32_t s = 0; s < K; ++s) {
+        if (v->log_term) v->log_term[i * K + s] = 0;
+        if (v->log_value) v->log_value[i * K + s] = 0;
+      }
+      int64_t lo = n->last > K ? n->last - K + 1 : 1;
+      for (int64_t idx = lo; idx <= n->last; ++idx) {
+        uint64_t s = i * K + (uint64_t)((idx - 1) & (K - 1));
+        if (v->log_term) v->log_term[s] = (int32_t)n->log[idx - 1].term;
+        if (v->log_value) v->log_value[s] = n->log[idx - 1].value;
+      }
+    }
+  }
+}
+
+typedef struct {
+  oracle* o;
+  uint64_t g0, g1;
+  int64_t first;
+  uint32_t nticks;
+  int64_t st[RAFT_NSTATS];
+} o_job;
+
+static void* run_job(void* arg) {
+  o_job* j = (o_job*)arg;
+  for (uint64_t g = j->g0; g < j->g1; ++g) {
+    for (uint32_t t = 0; t < j->nticks; ++t) {
+      o_ctx c = make_ctx(j->o, g, j->first + (int64_t)t);
+      tick_group(&c, &j->o->g[g]);
+      for (int s = 0; s < RAFT_NSTATS; ++s) j->st[s] += c.st[s];
+    }
+  }
+  return NULL;
+}
+
+void oracle_tick(oracle* o, int64_t first_tick, uint32_t nticks, int nthreads, raft_tick_stats* out) {
+  if (nthreads < 1) nthreads = 1;
+  if ((uint64_t)nthreads > o->cfg.groups) nthreads = o->cfg.groups ? (int)o->cfg.groups : 1;
+  o_job* jobs = (o_job*)calloc((size_t)nthreads, sizeof(o_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int i = 0; i < nthreads; ++i) {
+    jobs[i].o = o;
+    jobs[i].g0 = o->cfg.groups * (uint64_t)i / (uint64_t)nthreads;
+    jobs[i].g1 = o->cfg.groups * (uint64_t)(i + 1) / (uint64_t)nthreads;
+    jobs[i].first = first_tick;
+    jobs[i].nticks = nticks;
+    if (nthreads > 1) pthread_create(&th[i], NULL, run_job, &jobs[i]);
+  }
+  if (nthreads == 1) run_job(&jobs[0]);
+  else for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+  if (out) {
+    memset(out, 0, sizeof *out);
+    for (int i = 0; i < nthreads; ++i)
+      for (int s = 0; s < RAFT_NSTATS; ++s) out->v[s] += jobs[i].st[s];
+  }
+  free(jobs);
+  free(th);
+}
+
+static int check_distinct(const oracle* o, const uint64_t* gs, size_t stride, size_t n) {
+  unsigned char* seen = (unsigned char*)calloc(o->cfg.groups ? o->cfg.groups : 1, 1);
+  int rc = RAFT_OK;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t g = *(const uint64_t*)((const char*)gs + i * stride);
+    if (g >= o->cfg.groups || seen[g]) { rc = RAFT_EINVAL; break; }
+    seen[g] = 1;
+  }
+  free(seen);
+  return rc;
+}
+
+static int fits32(int64_t v) { return v >= -I32MAX - 1 && v <= I32MAX; }
+
+int oracle_append_entries(oracle* o, int64_t now_tick, const raft_ae_req* reqs, size_t n,
+                          const raft_log_entry* entries, raft_ae_resp* out) {
+  int rc = check_distinct(o, &reqs[0].group, sizeof(raft_ae_req), n);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; ++i) {
+    const raft_ae_req* q = &reqs[i];
+    if (q->to >= o->cfg.replicas || !fits32(q->term) || !fits32(q->prev_log_index) ||
+        !fits32(q->prev_log_term) || !fits32(q->leader_commit))
+      return RAFT_EINVAL;
+    for (uint64_t k = 0; k < q->n_entries; ++k)
+      if (!fits32(entries[q->entries_offset + k].term)) return RAFT_EINVAL;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const raft_ae_req* q = &reqs[i];
+    o_group* G = &o->g[q->group];
+    o_ctx c = make_ctx(o, q->group, now_tick);
+    raft_ae_resp* rs = &out[i];
+    memset(rs, 0, sizeof *rs);
+    if (G->fault) { rs->fault = G->fault; continue; }
+    o_ae r;
+    r.term = q->term; r.prev_idx = q->prev_log_index; r.prev_term = q->prev_log_term;
+    r.lc = q->leader_commit; r.n = (int64_t)q->n_entries;
+    r.ents = (const o_ent*)(entries + q->entries_offset);
+    o_aer a = deliver_ae(&c, G, (int)q->to, &r);
+    rs->term = a.term; rs->match_index = a.match; rs->success = G->fault ? 0 : a.ok;
+    rs->fault = G->fault;
+  }
+  return RAFT_OK;
+}
+
+int oracle_request_vote(oracle* o, int64_t now_tick, const raft_vote_req* reqs, size_t n,
+                        raft_vote_resp* out) {
+  int rc = check_distinct(o, &reqs[0].group, sizeof(raft_vote_req), n);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; ++i)
+    if (reqs[i].to >= o->cfg.replicas || !fits32(reqs[i].term)) return RAFT_EINVAL;
+  for (size_t i = 0; i < n; ++i) {
+    const raft_vote_req* q = &reqs[i];
+    o_group* G = &o->g[q->group];
+    o_ctx c = make_ctx(o, q->group, now_tick);
+    raft_vote_resp* rs = &out[i];
+    memset(rs, 0, sizeof *rs);
+    if (G->fault) { rs->fault = G->fault; continue; }
+    int64_t rt;
+    int grant = deliver_vr(&c, G, (int)q->to, q->term, &rt);
+    rs->term = rt; rs->vote_granted = grant; rs->fault = G->fault;
+  }
+  return RAFT_OK;
+}
+
+int oracle_group_ops(oracle* o, int64_t now_tick, const raft_group_op* ops, size_t n,
+                     raft_op_result* out) {
+  int rc = check_distinct(o, &ops[0].group, sizeof(raft_group_op), n);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; ++i)
+    if (ops[i].replica >= o->cfg.replicas || ops[i].kind < RAFT_OP_CLIENT_APPEND ||
+        ops[i].kind > RAFT_OP_LEADER_COMMIT)
+      return RAFT_EINVAL;
+  for (size_t i = 0; i < n; ++i) {
+    const raft_group_op* q = &ops[i];
+    o_group* G = &o->g[q->group];
+    o_ctx c = make_ctx(o, q->group, now_tick);
+    raft_op_result* rs = &out[i];
+    memset(rs, 0, sizeof *rs);
+    int x = (int)q->replica;
+    o_node* nd = &G->n[x];
+    if (G->fault) { rs->fault = G->fault; continue; }
+    switch (q->kind) {
+      case RAFT_OP_CLIENT_APPEND:
+        if (nd->role != RAFT_LEADER) { rs->status = RAFT_EINVAL; break; }
+        client_append(&c, G, x, q->arg);
+        rs->value = nd->last;
+        break;
+      case RAFT_OP_LEADER_ROUND:
+        if (nd->role != RAFT_LEADER) { rs->status = RAFT_EINVAL; break; }
+        leader_round(&c, G, x);
+        rs->value = nd->commit;
+        break;
+      case RAFT_OP_CANDIDATE_ROUND:
+        if (nd->role != RAFT_CANDIDATE) { rs->status = RAFT_EINVAL; break; }
+        rs->value = candidate_round(&c, G, x);
+        break;
+      case RAFT_OP_TIMEOUT:
+        if (nd->role == RAFT_LEADER) { rs->status = RAFT_EINVAL; break; }
+        timeout_fire(&c, G, x);
+        rs->value = nd->term;
+        break;
+      case RAFT_OP_LEADER_COMMIT:
+        if (nd->role != RAFT_LEADER) { rs->status = RAFT_EINVAL; break; }
+        leader_commit(&c, G, x);
+        rs->value = nd->commit;
+        break;
+    }
+    rs->fault = G->fault;
+  }
+  return RAFT_OK;
+}
+
+/* nodelog (main.go:399-401): "[Id:Term:CommitIndex:LastApplied][State]". */
+int oracle_nodelog(const oracle* o, uint64_t group, char* buf, size_t cap) {
+  static const char* names[] = {"follower", "candidate", "leader"};
+  size_t off = 0;
+  if (group >= o->cfg.groups) return RAFT_EINVAL;
+  for (uint32_t r = 0; r < o->cfg.replicas; ++r) {
+    const o_node* n = &o->g[group].n[r];
+    int w = snprintf(buf + off, cap > off ? cap - off : 0, "[Server%u:%lld:%lld:%lld][%s]\n", r,
+                     (long long)n->term, (long long)n->commit, (long long)n->last, names[n->role]);
+    if (w < 0) return RAFT_EINVAL;
+    off += (size_t)w;
+  }
+  return (int)off;
+}

@@ -1,0 +1,678 @@
+// engine.cpp — host side of the C-ABI (include/raftstep.h).
+//
+// Owns the device planes of one GPU, validates every call, converts the
+// canonical group-major host view to/from the replica-major device layout,
+// launches the kernels on the engine's own HIP stream and, when attached,
+// sums tick statistics across GPUs with RCCL. Nothing here computes Raft
+// state: that is all on the device (kernels.hip).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/raftstep.h"
+#include "kernels.h"
+
+using namespace raftstep;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) return fail(RAFT_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+#define RCCLCHK(expr)                                                                         \
+  do {                                                                                        \
+    ncclResult_t _r = (expr);                                                                 \
+    if (_r != ncclSuccess) return fail(RAFT_ERCCL, "%s: %s", #expr, ncclGetErrorString(_r)); \
+  } while (0)
+
+constexpr int I32 = 2147483647;
+
+bool fits32(int64_t v) { return v >= -int64_t(I32) - 1 && v <= int64_t(I32); }
+
+}  // namespace
+
+struct raft_engine {
+  raft_config cfg{};
+  int R = 0;
+  uint64_t Gp = 0;
+  hipStream_t stream = nullptr;
+  DevPlanes P{};
+  std::vector<void*> allocs;
+  uint64_t device_bytes = 0;
+  // per-tick statistics: [cap][STAT_SLOTS][NSTAT] u64
+  unsigned long long* hist = nullptr;
+  uint32_t hist_cap = 0;
+  // handler-batch staging
+  void* stage = nullptr;
+  size_t stage_cap = 0;
+  // profiling
+  bool prof = false;
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
+  double prof_ms = 0.0;
+  uint64_t prof_n = 0;
+  // RCCL
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace {
+
+int dev_alloc(raft_engine* e, void** p, size_t bytes) {
+  hipError_t rc = hipMalloc(p, bytes ? bytes : 16);
+  if (rc != hipSuccess) return fail(RAFT_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(rc));
+  e->allocs.push_back(*p);
+  e->device_bytes += bytes;
+  return RAFT_OK;
+}
+
+Trace make_trace(const raft_engine* e, int64_t tick) {
+  Trace T{};
+  T.seed = e->cfg.seed;
+  T.tick = tick;
+  T.now = int32_t(tick * e->cfg.tick_seconds);
+  T.f_min = e->cfg.follower_timeout_min;
+  T.f_span = e->cfg.follower_timeout_span;
+  T.c_min = e->cfg.candidate_timeout_min;
+  T.c_span = e->cfg.candidate_timeout_span;
+  T.iso_p = e->cfg.isolate_per_65536;
+  T.iso_min = e->cfg.isolate_min_ticks;
+  T.iso_span = e->cfg.isolate_max_ticks - e->cfg.isolate_min_ticks + 1;
+  return T;
+}
+
+// virtual seconds must stay inside int32 (deadline = now + d)
+int check_ticks(const raft_engine* e, int64_t first, uint64_t n) {
+  const int64_t maxd = std::max(e->cfg.follower_timeout_min + e->cfg.follower_timeout_span,
+                                e->cfg.candidate_timeout_min + e->cfg.candidate_timeout_span);
+  if (first < 0) return fail(RAFT_ERANGE, "tick must be >= 0");
+  const long double last_now = (long double)(first + int64_t(n)) * e->cfg.tick_seconds + maxd;
+  if (last_now >= (long double)I32) return fail(RAFT_ERANGE, "virtual time leaves int32 seconds");
+  return RAFT_OK;
+}
+
+int ensure_stage(raft_engine* e, size_t bytes) {
+  if (bytes <= e->stage_cap) return RAFT_OK;
+  if (e->stage) {
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipFree(e->stage));
+    e->stage = nullptr;
+  }
+  size_t cap = std::max<size_t>(bytes, 1 << 20);
+  HIPCHK(hipMalloc(&e->stage, cap));
+  e->stage_cap = cap;
+  return RAFT_OK;
+}
+
+int ensure_hist(raft_engine* e, uint32_t n) {
+  if (n <= e->hist_cap) return RAFT_OK;
+  if (e->hist) {
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipFree(e->hist));
+    e->hist = nullptr;
+  }
+  uint32_t cap = std::max<uint32_t>(n, 64);
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->hist), size_t(cap) * STAT_SLOTS * NSTAT * 8));
+  e->hist_cap = cap;
+  return RAFT_OK;
+}
+
+hipEvent_t next_event(raft_engine* e) {
+  if (e->ev_used == e->ev.size()) {
+    hipEvent_t x;
+    if (hipEventCreate(&x) != hipSuccess) return nullptr;
+    e->ev.push_back(x);
+  }
+  return e->ev[e->ev_used++];
+}
+
+int check_distinct(const raft_engine* e, const uint64_t* first, size_t stride, size_t n) {
+  std::vector<uint64_t> gs(n);
+  for (size_t i = 0; i < n; ++i) {
+    gs[i] = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(first) + i * stride);
+    if (gs[i] >= e->cfg.groups) return fail(RAFT_EINVAL, "batch element %zu: group %llu out of range", i,
+                                           (unsigned long long)gs[i]);
+  }
+  std::sort(gs.begin(), gs.end());
+  for (size_t i = 1; i < n; ++i)
+    if (gs[i] == gs[i - 1])
+      return fail(RAFT_EINVAL, "batch targets group %llu twice; batches need distinct groups",
+                  (unsigned long long)gs[i]);
+  return RAFT_OK;
+}
+
+// Runs a prepared DevOp batch (+ entries) through ops_kernel and returns the results.
+int run_ops(raft_engine* e, int64_t now_tick, const std::vector<DevOp>& ops, const std::vector<int32_t>& et,
+            const std::vector<int64_t>& ev, std::vector<DevRes>& res) {
+  const size_t n = ops.size();
+  res.assign(n, DevRes{});
+  if (!n) return RAFT_OK;
+  if (int rc = check_ticks(e, now_tick, 1)) return rc;
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t b_ops = al(n * sizeof(DevOp)), b_res = al(n * sizeof(DevRes));
+  const size_t b_et = al(et.size() * 4 + 4), b_ev = al(ev.size() * 8 + 8);
+  if (int rc = ensure_stage(e, b_ops + b_res + b_et + b_ev)) return rc;
+  char* base = static_cast<char*>(e->stage);
+  DevOp* d_ops = reinterpret_cast<DevOp*>(base);
+  DevRes* d_res = reinterpret_cast<DevRes*>(base + b_ops);
+  int32_t* d_et = reinterpret_cast<int32_t*>(base + b_ops + b_res);
+  int64_t* d_ev = reinterpret_cast<int64_t*>(base + b_ops + b_res + b_et);
+  HIPCHK(hipMemcpyAsync(d_ops, ops.data(), n * sizeof(DevOp), hipMemcpyHostToDevice, e->stream));
+  if (!et.empty()) {
+    HIPCHK(hipMemcpyAsync(d_et, et.data(), et.size() * 4, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(d_ev, ev.data(), ev.size() * 8, hipMemcpyHostToDevice, e->stream));
+  }
+  const Trace T = make_trace(e, now_tick);
+  HIPCHK(launch_ops(e->R, e->P, T, d_ops, uint32_t(n), d_et, d_ev, d_res, e->stream));
+  HIPCHK(hipMemcpyAsync(res.data(), d_res, n * sizeof(DevRes), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RAFT_OK;
+}
+
+template <typename T>
+int d2h(raft_engine* e, std::vector<T>& h, const T* d, size_t n) {
+  h.resize(n);
+  HIPCHK(hipMemcpyAsync(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, e->stream));
+  return RAFT_OK;
+}
+template <typename T>
+int h2d(raft_engine* e, T* d, const std::vector<T>& h) {
+  HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, e->stream));
+  return RAFT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void raft_config_default(raft_config* c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof *c);
+  c->abi_version = RAFT_ABI_VERSION;
+  c->replicas = 3;                 // main.go:81
+  c->groups = 1;
+  c->ring_depth = 32;
+  c->entries_per_tick = 1;
+  c->client_period = 5;            // one client write per 10 s (main.go:89) at 2 s per tick
+  c->semantics = RAFT_SEM_REF;
+  c->seed = 0x5EED0001ULL;
+  c->tick_seconds = 2;             // main.go:394
+  c->follower_timeout_min = 10;    // main.go:114
+  c->follower_timeout_span = 20;
+  c->candidate_timeout_min = 10;   // main.go:194
+  c->candidate_timeout_span = 4;
+  c->isolate_min_ticks = 8;
+  c->isolate_max_ticks = 32;
+  c->device = 0;
+}
+
+const char* raft_last_error(void) { return g_err.c_str(); }
+
+int raft_engine_create(const raft_config* cfg, raft_engine** out) {
+  if (!cfg || !out) return fail(RAFT_EINVAL, "null argument");
+  *out = nullptr;
+  const raft_config& c = *cfg;
+  if (c.abi_version != RAFT_ABI_VERSION) return fail(RAFT_EINVAL, "abi_version %u != %u", c.abi_version, RAFT_ABI_VERSION);
+  if (c.replicas < 1 || c.replicas > RAFT_MAX_REPLICAS) return fail(RAFT_EINVAL, "replicas must be 1..8");
+  if (c.groups < 1) return fail(RAFT_EINVAL, "groups must be >= 1");
+  if (c.ring_depth < 2 || c.ring_depth > 4096 || (c.ring_depth & (c.ring_depth - 1)))
+    return fail(RAFT_EINVAL, "ring_depth must be a power of two in [2, 4096]");
+  if (c.semantics != RAFT_SEM_REF) return fail(RAFT_EINVAL, "only RAFT_SEM_REF is implemented");
+  if (c.tick_seconds < 1) return fail(RAFT_EINVAL, "tick_seconds must be >= 1");
+  if (c.follower_timeout_min < 1 || c.follower_timeout_span < 1 || c.candidate_timeout_min < 1 ||
+      c.candidate_timeout_span < 1 || c.follower_timeout_min + c.follower_timeout_span > 8192 ||
+      c.candidate_timeout_min + c.candidate_timeout_span > 8192)
+    return fail(RAFT_EINVAL, "timer ranges must be >= 1 and below 8192 s");
+  if (c.isolate_per_65536 > 65536) return fail(RAFT_EINVAL, "isolate_per_65536 must be <= 65536");
+  if (c.isolate_per_65536 &&
+      (c.isolate_min_ticks < 1 || c.isolate_max_ticks > 32 || c.isolate_min_ticks > c.isolate_max_ticks))
+    return fail(RAFT_EINVAL, "isolation length must satisfy 1 <= min <= max <= 32");
+  const uint64_t Gp = (c.groups + 255) & ~uint64_t(255);
+  if (Gp * c.replicas * c.ring_depth >= (uint64_t(1) << 40)) return fail(RAFT_EINVAL, "state too large");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RAFT_ENODEV, "no HIP device");
+  if (c.device < 0 || c.device >= ndev) return fail(RAFT_ENODEV, "device %d out of range", c.device);
+  HIPCHK(hipSetDevice(c.device));
+
+  raft_engine* e = new raft_engine();
+  e->cfg = c;
+  e->R = int(c.replicas);
+  e->Gp = Gp;
+  int rc = RAFT_OK;
+  auto A = [&](void** p, size_t bytes) {
+    if (rc == RAFT_OK) rc = dev_alloc(e, p, bytes);
+  };
+  const uint64_t R = c.replicas, K = c.ring_depth;
+  A(reinterpret_cast<void**>(&e->P.term), R * Gp * 4);
+  A(reinterpret_cast<void**>(&e->P.last), R * Gp * 4);
+  A(reinterpret_cast<void**>(&e->P.commit), R * Gp * 4);
+  A(reinterpret_cast<void**>(&e->P.deadline), R * Gp * 4);
+  A(reinterpret_cast<void**>(&e->P.rs), R * Gp * 2);
+  A(reinterpret_cast<void**>(&e->P.lmatch), R * Gp * 4);
+  A(reinterpret_cast<void**>(&e->P.xmatch), R * R * Gp * 4);
+  A(reinterpret_cast<void**>(&e->P.gmeta), Gp);
+  A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
+  A(reinterpret_cast<void**>(&e->P.log_value), R * K * Gp * 8);
+  if (rc == RAFT_OK) {
+    hipError_t h = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (h != hipSuccess) rc = fail(RAFT_EHIP, "hipStreamCreate: %s", hipGetErrorString(h));
+  }
+  if (rc != RAFT_OK) {
+    std::string keep = g_err;
+    raft_engine_destroy(e);
+    g_err = keep;
+    return rc;
+  }
+  e->P.Gp = Gp;
+  e->P.G = c.groups;
+  e->P.gbase = c.group_base;
+  e->P.K = c.ring_depth;
+  e->P.kmask = c.ring_depth - 1;
+  // zero everything once so that padding / unused rows are deterministic
+  for (void* p : e->allocs) (void)p;
+  hipError_t z = hipSuccess;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.term, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.last, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.commit, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.deadline, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.rs, 0, R * Gp * 2, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.lmatch, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.xmatch, 0, R * R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.gmeta, NO_PRIMARY, Gp, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.log_value, 0, R * K * Gp * 8, e->stream) : z;
+  z = z == hipSuccess ? hipStreamSynchronize(e->stream) : z;
+  if (z != hipSuccess) {
+    raft_engine_destroy(e);
+    return fail(RAFT_EHIP, "initial memset: %s", hipGetErrorString(z));
+  }
+  *out = e;
+  return RAFT_OK;
+}
+
+int raft_engine_destroy(raft_engine* e) {
+  if (!e) return RAFT_OK;
+  (void)hipSetDevice(e->cfg.device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->comm) (void)ncclCommDestroy(e->comm);
+  for (hipEvent_t x : e->ev) (void)hipEventDestroy(x);
+  for (void* p : e->allocs) (void)hipFree(p);
+  if (e->hist) (void)hipFree(e->hist);
+  if (e->stage) (void)hipFree(e->stage);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return RAFT_OK;
+}
+
+int raft_engine_info(const raft_engine* e, raft_config* cfg_out, uint64_t* device_bytes) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  if (cfg_out) *cfg_out = e->cfg;
+  if (device_bytes) *device_bytes = e->device_bytes;
+  return RAFT_OK;
+}
+
+int raft_init_new_nodes(raft_engine* e, int64_t tick0) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  if (int rc = check_ticks(e, tick0, 1)) return rc;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  const uint64_t R = e->cfg.replicas, Gp = e->Gp;
+  HIPCHK(hipMemsetAsync(e->P.lmatch, 0, R * Gp * 4, e->stream));
+  HIPCHK(launch_init_new(e->R, e->P, make_trace(e, tick0), e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RAFT_OK;
+}
+
+int raft_init_steady(raft_engine* e, int32_t leader, int64_t tick0) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  if (int rc = check_ticks(e, tick0, 1)) return rc;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  HIPCHK(launch_init_steady(e->R, e->P, make_trace(e, tick0), leader, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RAFT_OK;
+}
+
+int raft_store_state(raft_engine* e, raft_state_view* v) {
+  if (!e || !v) return fail(RAFT_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(e->cfg.device));
+  const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
+  std::vector<int32_t> term, last, commit, dl, lm, xm, lt;
+  std::vector<uint16_t> rs;
+  std::vector<uint8_t> meta;
+  std::vector<int64_t> lv;
+  int rc = RAFT_OK;
+  if (!rc) rc = d2h(e, term, e->P.term, R * Gp);
+  if (!rc) rc = d2h(e, last, e->P.last, R * Gp);
+  if (!rc) rc = d2h(e, commit, e->P.commit, R * Gp);
+  if (!rc) rc = d2h(e, dl, e->P.deadline, R * Gp);
+  if (!rc) rc = d2h(e, rs, e->P.rs, R * Gp);
+  if (!rc) rc = d2h(e, lm, e->P.lmatch, R * Gp);
+  if (!rc) rc = d2h(e, xm, e->P.xmatch, R * R * Gp);
+  if (!rc) rc = d2h(e, meta, e->P.gmeta, Gp);
+  const bool logs = v->log_term || v->log_value;
+  if (!rc && logs) rc = d2h(e, lt, e->P.log_term, R * K * Gp);
+  if (!rc && logs) rc = d2h(e, lv, e->P.log_value, R * K * Gp);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  for (uint64_t g = 0; g < G; ++g) {
+    const int primary = meta[g] & 0xF;
+    if (v->fault) v->fault[g] = uint8_t(meta[g] >> 4);
+    for (uint64_t r = 0; r < R; ++r) {
+      const uint64_t d = r * Gp + g, c = g * R + r;
+      const int role = rs[d] & 3;
+      if (v->role) v->role[c] = uint8_t(role);
+      if (v->voted) v->voted[c] = uint8_t((rs[d] >> 2) & 1);
+      if (v->term) v->term[c] = term[d];
+      if (v->last) v->last[c] = last[d];
+      if (v->commit) v->commit[c] = commit[d];
+      if (v->deadline) v->deadline[c] = dl[d];
+      if (v->timeout) v->timeout[c] = int32_t(rs[d] >> 3);
+      if (v->match)
+        for (uint64_t p = 0; p < R; ++p) {
+          int32_t m = 0;
+          if (role == ROLE_L && p != r)
+            m = (int(r) == primary) ? lm[p * Gp + g] : xm[(r * R + p) * Gp + g];
+          v->match[c * R + p] = m;
+        }
+      if (logs) {
+        const int64_t l = last[d];
+        for (uint64_t s = 0; s < K; ++s) {
+          // slot s holds the largest index i <= l with (i-1) mod K == s
+          int64_t idx = l >= 1 ? l - ((l - 1 - int64_t(s)) & int64_t(K - 1)) : 0;
+          const bool live = idx >= 1 && idx <= l && idx > l - int64_t(K);
+          const uint64_t o = (r * K + s) * Gp + g;
+          if (v->log_term) v->log_term[c * K + s] = live ? lt[o] : 0;
+          if (v->log_value) v->log_value[c * K + s] = live ? lv[o] : 0;
+        }
+      }
+    }
+  }
+  return RAFT_OK;
+}
+
+int raft_load_state(raft_engine* e, const raft_state_view* v) {
+  if (!e || !v) return fail(RAFT_EINVAL, "null argument");
+  if (!v->role || !v->voted || !v->term || !v->last || !v->commit || !v->deadline || !v->timeout ||
+      !v->match || !v->fault || !v->log_term || !v->log_value)
+    return fail(RAFT_EINVAL, "raft_load_state needs every field of the view");
+  HIPCHK(hipSetDevice(e->cfg.device));
+  const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
+  std::vector<int32_t> term(R * Gp, 0), last(R * Gp, 0), commit(R * Gp, 0), dl(R * Gp, 0), lm(R * Gp, 0),
+      xm(R * R * Gp, 0), lt(R * K * Gp, 0);
+  std::vector<uint16_t> rs(R * Gp, 0);
+  std::vector<uint8_t> meta(Gp, uint8_t(NO_PRIMARY));
+  std::vector<int64_t> lv(R * K * Gp, 0);
+  for (uint64_t g = 0; g < G; ++g) {
+    if (v->fault[g] > RAFT_F_OVERFLOW) return fail(RAFT_EINVAL, "group %llu: bad fault code", (unsigned long long)g);
+    int primary = NO_PRIMARY;
+    for (uint64_t r = 0; r < R; ++r) {
+      const uint64_t c = g * R + r;
+      if (v->role[c] > RAFT_LEADER || v->voted[c] > 1 || v->last[c] < 0 || v->timeout[c] < 0 || v->timeout[c] > 8191)
+        return fail(RAFT_EINVAL, "group %llu replica %llu: field out of range", (unsigned long long)g,
+                    (unsigned long long)r);
+      if (v->role[c] == RAFT_LEADER && primary == NO_PRIMARY) primary = int(r);
+    }
+    meta[g] = uint8_t(primary | (v->fault[g] << 4));
+    for (uint64_t r = 0; r < R; ++r) {
+      const uint64_t d = r * Gp + g, c = g * R + r;
+      term[d] = v->term[c];
+      last[d] = v->last[c];
+      commit[d] = v->commit[c];
+      dl[d] = v->deadline[c];
+      rs[d] = uint16_t(v->role[c] | (v->voted[c] << 2) | (uint32_t(v->timeout[c]) << 3));
+      if (v->role[c] == RAFT_LEADER)
+        for (uint64_t p = 0; p < R; ++p) {
+          if (p == r) continue;
+          if (int(r) == primary) lm[p * Gp + g] = v->match[c * R + p];
+          else xm[(r * R + p) * Gp + g] = v->match[c * R + p];
+        }
+      for (uint64_t s = 0; s < K; ++s) {
+        lt[(r * K + s) * Gp + g] = v->log_term[c * K + s];
+        lv[(r * K + s) * Gp + g] = v->log_value[c * K + s];
+      }
+    }
+  }
+  int rc = RAFT_OK;
+  if (!rc) rc = h2d(e, e->P.term, term);
+  if (!rc) rc = h2d(e, e->P.last, last);
+  if (!rc) rc = h2d(e, e->P.commit, commit);
+  if (!rc) rc = h2d(e, e->P.deadline, dl);
+  if (!rc) rc = h2d(e, e->P.rs, rs);
+  if (!rc) rc = h2d(e, e->P.lmatch, lm);
+  if (!rc) rc = h2d(e, e->P.xmatch, xm);
+  if (!rc) rc = h2d(e, e->P.gmeta, meta);
+  if (!rc) rc = h2d(e, e->P.log_term, lt);
+  if (!rc) rc = h2d(e, e->P.log_value, lv);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RAFT_OK;
+}
+
+static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool stats) {
+  if (int rc = check_ticks(e, first_tick, nticks)) return rc;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  if (stats) {
+    if (int rc = ensure_hist(e, nticks)) return rc;
+    HIPCHK(hipMemsetAsync(e->hist, 0, size_t(nticks) * STAT_SLOTS * NSTAT * 8, e->stream));
+  }
+  for (uint32_t i = 0; i < nticks; ++i) {
+    const int64_t t = first_tick + int64_t(i);
+    const Trace T = make_trace(e, t);
+    const uint32_t period = e->cfg.client_period;
+    const uint32_t E = (period && (t % int64_t(period)) == 0) ? e->cfg.entries_per_tick : 0;
+    hipEvent_t a = nullptr, b = nullptr;
+    if (e->prof) {
+      a = next_event(e);
+      b = next_event(e);
+      if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
+      HIPCHK(hipEventRecord(a, e->stream));
+    }
+    HIPCHK(launch_tick(e->R, e->P, T, E, stats ? e->hist + size_t(i) * STAT_SLOTS * NSTAT : nullptr, e->stream));
+    if (e->prof) HIPCHK(hipEventRecord(b, e->stream));
+  }
+  if (stats && e->comm)
+    RCCLCHK(ncclAllReduce(e->hist, e->hist, size_t(nticks) * STAT_SLOTS * NSTAT, ncclUint64, ncclSum, e->comm,
+                          e->stream));
+  return RAFT_OK;
+}
+
+static int read_hist(raft_engine* e, uint32_t nticks, std::vector<unsigned long long>& h) {
+  h.resize(size_t(nticks) * STAT_SLOTS * NSTAT);
+  HIPCHK(hipMemcpyAsync(h.data(), e->hist, h.size() * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RAFT_OK;
+}
+
+int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_stats* out) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  if (int rc = tick_impl(e, first_tick, nticks, out != nullptr)) return rc;
+  if (out) {
+    std::vector<unsigned long long> h;
+    if (int rc = read_hist(e, nticks, h)) return rc;
+    std::memset(out, 0, sizeof *out);
+    for (size_t i = 0; i < h.size(); ++i) out->v[i % NSTAT] += int64_t(h[i]);
+  }
+  return RAFT_OK;
+}
+
+int raft_sync(raft_engine* e) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  HIPCHK(hipSetDevice(e->cfg.device));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RAFT_OK;
+}
+
+int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_req* reqs, size_t n,
+                              const raft_log_entry* entries, size_t n_entries_total, raft_ae_resp* out) {
+  if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
+  if (n == 0) return RAFT_OK;
+  if (int rc = check_distinct(e, &reqs[0].group, sizeof(raft_ae_req), n)) return rc;
+  std::vector<DevOp> ops(n);
+  std::vector<int32_t> et;
+  std::vector<int64_t> ev;
+  for (size_t i = 0; i < n; ++i) {
+    const raft_ae_req& q = reqs[i];
+    if (q.to >= e->cfg.replicas) return fail(RAFT_EINVAL, "req %zu: receiver out of range", i);
+    if (!fits32(q.term) || !fits32(q.prev_log_index) || !fits32(q.prev_log_term) || !fits32(q.leader_commit))
+      return fail(RAFT_EINVAL, "req %zu: term/index outside the int32 range of the engine", i);
+    if (q.n_entries > uint64_t(I32) || q.entries_offset + q.n_entries > n_entries_total || (q.n_entries && !entries))
+      return fail(RAFT_EINVAL, "req %zu: entries out of range", i);
+    DevOp& o = ops[i];
+    std::memset(&o, 0, sizeof o);
+    o.group = q.group; o.replica = q.to; o.kind = OP_AE;
+    o.term = int32_t(q.term); o.prev_idx = int32_t(q.prev_log_index);
+    o.prev_term = int32_t(q.prev_log_term); o.lc = int32_t(q.leader_commit);
+    o.n = uint32_t(q.n_entries);
+    o.off = et.size();
+    // only the last K entries of a request can land in the ring
+    const uint64_t K = e->cfg.ring_depth;
+    const uint64_t j0 = q.n_entries > K ? q.n_entries - K : 0;
+    for (uint64_t j = 0; j < q.n_entries; ++j) {
+      const raft_log_entry& le = entries[q.entries_offset + j];
+      if (!fits32(le.term)) return fail(RAFT_EINVAL, "req %zu: entry term outside int32", i);
+      if (j < j0) { et.push_back(0); ev.push_back(0); continue; }
+      et.push_back(int32_t(le.term));
+      ev.push_back(le.value);
+    }
+  }
+  std::vector<DevRes> res;
+  if (int rc = run_ops(e, now_tick, ops, et, ev, res)) return rc;
+  for (size_t i = 0; i < n; ++i) {
+    out[i].term = res[i].term;
+    out[i].match_index = res[i].value;
+    out[i].success = res[i].ok;
+    out[i].fault = res[i].fault;
+  }
+  return RAFT_OK;
+}
+
+int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_req* reqs, size_t n,
+                            raft_vote_resp* out) {
+  if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
+  if (n == 0) return RAFT_OK;
+  if (int rc = check_distinct(e, &reqs[0].group, sizeof(raft_vote_req), n)) return rc;
+  std::vector<DevOp> ops(n);
+  for (size_t i = 0; i < n; ++i) {
+    const raft_vote_req& q = reqs[i];
+    if (q.to >= e->cfg.replicas) return fail(RAFT_EINVAL, "req %zu: receiver out of range", i);
+    if (!fits32(q.term)) return fail(RAFT_EINVAL, "req %zu: term outside int32", i);
+    std::memset(&ops[i], 0, sizeof(DevOp));
+    ops[i].group = q.group; ops[i].replica = q.to; ops[i].kind = OP_VR; ops[i].term = int32_t(q.term);
+  }
+  std::vector<DevRes> res;
+  if (int rc = run_ops(e, now_tick, ops, {}, {}, res)) return rc;
+  for (size_t i = 0; i < n; ++i) {
+    out[i].term = res[i].term;
+    out[i].vote_granted = res[i].ok;
+    out[i].fault = res[i].fault;
+  }
+  return RAFT_OK;
+}
+
+int raft_group_ops_batch(raft_engine* e, int64_t now_tick, const raft_group_op* ops_in, size_t n,
+                         raft_op_result* out) {
+  if (!e || (n && (!ops_in || !out))) return fail(RAFT_EINVAL, "null argument");
+  if (n == 0) return RAFT_OK;
+  if (int rc = check_distinct(e, &ops_in[0].group, sizeof(raft_group_op), n)) return rc;
+  std::vector<DevOp> ops(n);
+  for (size_t i = 0; i < n; ++i) {
+    const raft_group_op& q = ops_in[i];
+    if (q.replica >= e->cfg.replicas) return fail(RAFT_EINVAL, "op %zu: replica out of range", i);
+    if (q.kind < RAFT_OP_CLIENT_APPEND || q.kind > RAFT_OP_LEADER_COMMIT)
+      return fail(RAFT_EINVAL, "op %zu: unknown kind %u", i, q.kind);
+    std::memset(&ops[i], 0, sizeof(DevOp));
+    ops[i].group = q.group; ops[i].replica = q.replica; ops[i].kind = q.kind; ops[i].arg = q.arg;
+  }
+  std::vector<DevRes> res;
+  if (int rc = run_ops(e, now_tick, ops, {}, {}, res)) return rc;
+  for (size_t i = 0; i < n; ++i) {
+    out[i].status = res[i].status;
+    out[i].fault = res[i].fault;
+    out[i].value = res[i].value;
+  }
+  return RAFT_OK;
+}
+
+int raft_comm_unique_id(uint8_t id_out[128]) {
+  if (!id_out) return fail(RAFT_EINVAL, "null argument");
+  ncclUniqueId id;
+  RCCLCHK(ncclGetUniqueId(&id));
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  std::memcpy(id_out, &id, 128);
+  return RAFT_OK;
+}
+
+int raft_comm_init(raft_engine* e, int nranks, int rank, const uint8_t id[128]) {
+  if (!e || !id) return fail(RAFT_EINVAL, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(RAFT_EINVAL, "bad rank/nranks");
+  if (e->comm) return fail(RAFT_EINVAL, "communicator already attached");
+  HIPCHK(hipSetDevice(e->cfg.device));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, 128);
+  RCCLCHK(ncclCommInitRank(&e->comm, nranks, uid, rank));
+  e->nranks = nranks;
+  e->rank = rank;
+  return RAFT_OK;
+}
+
+int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats) {
+  if (!e || !stats) return fail(RAFT_EINVAL, "null argument");
+  if (!e->comm) return RAFT_OK;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  if (int rc = ensure_hist(e, 1)) return rc;
+  std::vector<unsigned long long> h(NSTAT);
+  for (int s = 0; s < NSTAT; ++s) h[s] = (unsigned long long)stats->v[s];
+  HIPCHK(hipMemcpyAsync(e->hist, h.data(), NSTAT * 8, hipMemcpyHostToDevice, e->stream));
+  RCCLCHK(ncclAllReduce(e->hist, e->hist, NSTAT, ncclUint64, ncclSum, e->comm, e->stream));
+  HIPCHK(hipMemcpyAsync(h.data(), e->hist, NSTAT * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  for (int s = 0; s < NSTAT; ++s) stats->v[s] = int64_t(h[s]);
+  return RAFT_OK;
+}
+
+int raft_profile_enable(raft_engine* e, int enable) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  e->prof = enable != 0;
+  e->ev_used = 0;
+  e->prof_ms = 0.0;
+  e->prof_n = 0;
+  return RAFT_OK;
+}
+
+int raft_profile_read(raft_engine* e, double* total_ms, uint64_t* launches) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  HIPCHK(hipSetDevice(e->cfg.device));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  for (size_t i = 0; i + 1 < e->ev_used; i += 2) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev[i], e->ev[i + 1]));
+    e->prof_ms += ms;
+    e->prof_n += 1;
+  }
+  e->ev_used = 0;
+  if (total_ms) *total_ms = e->prof_ms;
+  if (launches) *launches = e->prof_n;
+  return RAFT_OK;
+}
+
+}  // extern "C"

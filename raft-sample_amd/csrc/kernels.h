@@ -1,0 +1,38 @@
+// kernels.h — host-side launchers and device argument records of the engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "raft_device.hpp"
+
+namespace raftstep {
+
+enum : uint32_t {
+  OP_CLIENT_APPEND = 1, OP_LEADER_ROUND = 2, OP_CANDIDATE_ROUND = 3, OP_TIMEOUT = 4,
+  OP_LEADER_COMMIT = 5, OP_AE = 100, OP_VR = 101
+};
+
+// One handler-batch element after host-side range checks (int64 -> int32).
+struct DevOp {
+  uint64_t group;
+  uint32_t replica;   // receiving / acting replica
+  uint32_t kind;
+  int64_t arg;        // CLIENT_APPEND value
+  int32_t term, prev_idx, prev_term, lc;  // AE / VR request fields
+  uint32_t n;         // AE: len(Logs)
+  uint32_t pad;
+  uint64_t off;       // AE: offset into the entry arrays
+};
+struct DevRes {
+  int32_t status, fault, ok, term;
+  int64_t value;      // AE: MatchIndex; VR: granted; ops: see raft_op_result
+};
+
+hipError_t launch_tick(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
+                       hipStream_t s);
+hipError_t launch_ops(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
+                      const int32_t* et, const int64_t* ev, DevRes* out, hipStream_t s);
+hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_t s);
+hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s);
+
+}  // namespace raftstep

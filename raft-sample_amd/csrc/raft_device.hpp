@@ -1,0 +1,500 @@
+// raft_device.hpp — CDNA4 device code of the batched Raft step engine.
+//
+// One lane owns one Raft group for the duration of a launch. The group's R
+// replicas are loaded from struct-of-arrays planes ([R][Gp], one 256-B
+// coalesced wave access per plane) into registers, every message between
+// replicas is a register hand-off inside the lane, and only changed fields
+// are stored back. Handler semantics follow main.go (eastwd/raft-sample)
+// exactly; each function cites the lines it implements. The CPU oracle in
+// oracle/ restates the same lines independently and the parity tests diff
+// the two.
+//
+// Register discipline: arrays indexed by a compile-time replica id stay in
+// VGPRs; arrays indexed by a runtime replica id go through sel()/put()
+// (v_cndmask chains) so nothing spills to scratch. Per-replica roles and
+// flags are bit-packed into one 32-bit register.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+namespace raftstep {
+
+enum : int { ROLE_F = 0, ROLE_C = 1, ROLE_L = 2 };
+enum : int {
+  F_NONE = 0, F_PANIC_GETLOG = 1, F_DEADLOCK_VRES = 2, F_DEADLOCK_LEADER_VREQ = 3,
+  F_RING_EVICTED = 4, F_OVERFLOW = 5
+};
+enum : uint32_t { ST_VALUE = 1, ST_TIMER_F = 2, ST_TIMER_C = 3, ST_ISOLATE = 4 };
+enum : int {
+  S_COMMITTED = 0, S_WON = 1, S_BUMPS = 2, S_AE_OK = 3, S_AE_FAIL = 4, S_VOTES = 5,
+  S_FAULTS = 6, S_LEADER_GROUPS = 7, NSTAT = 8
+};
+constexpr int NO_PRIMARY = 0xF;
+constexpr int I32MAX = 2147483647;
+constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to cut atomic contention
+
+// Device layout. Per-replica scalar planes are [R][Gp]; the per-replica log
+// ring is [R][K][Gp] (slot-major, so a wave of groups in lock-step writes
+// one 256-B term segment and one 512-B value segment per entry).
+struct DevPlanes {
+  int32_t* term;       // Node.Term                 (main.go:19)
+  int32_t* last;       // Node.LastApplied=len(Log) (main.go:25)
+  int32_t* commit;     // Node.CommitIndex          (main.go:24)
+  int32_t* deadline;   // election timer deadline, virtual seconds
+  uint16_t* rs;        // role:2 | voted:1 | timer duration d:13 (main.go:16, 20, 114, 194)
+  int32_t* lmatch;     // [R][Gp] MatchIndex row of the group's primary leader (main.go:29)
+  int32_t* xmatch;     // [R][R][Gp] rows of any further concurrent leaders (EXT only)
+  uint8_t* gmeta;      // primary leader id:4 | fault:4
+  int32_t* log_term;   // Log.Term  ring
+  int64_t* log_value;  // Log.Value ring
+  uint64_t Gp;         // plane pitch (groups, padded)
+  uint64_t G;          // groups on this engine
+  uint64_t gbase;      // global id of local group 0
+  uint32_t K;          // ring depth (power of two)
+  uint32_t kmask;
+};
+
+struct Trace {          // per-launch trace parameters (virtual clock + RNG)
+  uint64_t seed;
+  int64_t tick;
+  int32_t now;          // tick * tick_seconds
+  int32_t f_min, f_span, c_min, c_span;
+  uint32_t iso_p, iso_min, iso_span;
+};
+
+// ------------------------------------------------------------------ RNG --
+__device__ __forceinline__ uint64_t sm64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ uint64_t group_key(uint64_t seed, uint64_t gid) { return sm64(seed ^ sm64(gid)); }
+__device__ __forceinline__ uint64_t rng_k(uint64_t key, uint32_t r, uint32_t stream, uint64_t tick) {
+  return sm64(sm64(key ^ ((uint64_t(stream) << 32) | r)) ^ tick);
+}
+
+// ------------------------------------------------- register-array helpers --
+// Runtime-indexed access to a register array without letting LLVM fold the
+// select chain into a dynamic GEP (which would demote the whole Group to
+// scratch): each element is masked arithmetically and OR-ed (exclusive), and
+// writes are unconditional selects per element.
+template <int R>
+__device__ __forceinline__ int sel(const int (&a)[R], int c) {
+  int v = 0;
+#pragma unroll
+  for (int i = 0; i < R; ++i) v |= a[i] & -int(c == i);
+  return v;
+}
+template <int R>
+__device__ __forceinline__ void put(int (&a)[R], int c, int v) {
+#pragma unroll
+  for (int i = 0; i < R; ++i) a[i] = (c == i) ? v : a[i];
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (N > 0) {
+    static_for<N - 1>(f);
+    f(std::integral_constant<int, N - 1>{});
+  }
+}
+
+struct AEReq {          // AppendEntriesRequest (main.go:289-296), LeaderId implicit
+  int term, prev_idx, prev_term, lc;
+  int n;                // len(Logs)
+};
+struct AEResp { int term, match, ok; };  // AppendEntriesResponse (main.go:298-302)
+
+// Group context: the R replicas of one group, in registers.
+template <int R>
+struct Group {
+  int term[R], last[R], commit[R], dl[R], dur[R];
+  uint32_t roles;       // 2 bits per replica
+  uint32_t voted;       // 1 bit per replica
+  uint32_t known;       // deadline register valid
+  uint32_t d_term, d_last, d_commit, d_dl, d_rs;
+  int primary, fault, meta0;
+  uint32_t iso;         // EXT: replicas isolated during this tick
+  uint64_t g, key;
+  int64_t tick;
+  int32_t now;
+  int st[NSTAT];
+  // fast path for the entries appended by the client in this tick: the
+  // follower copy regenerates them from the trace RNG instead of re-reading
+  int cache_leader, cache_from, cache_term;
+  uint64_t cache_vbase;
+
+  __device__ __forceinline__ int role(int r) const { return int(roles >> (2 * r)) & 3; }
+  __device__ __forceinline__ void set_role(int r, int v) {
+    roles = (roles & ~(3u << (2 * r))) | (uint32_t(v) << (2 * r));
+    d_rs |= 1u << r;
+  }
+  __device__ __forceinline__ bool is_voted(int r) const { return (voted >> r) & 1u; }
+  __device__ __forceinline__ void set_voted(int r, bool v) {
+    voted = v ? (voted | (1u << r)) : (voted & ~(1u << r));
+    d_rs |= 1u << r;
+  }
+  __device__ __forceinline__ void raise(int f) {
+    if (!fault) fault = f;
+  }
+  __device__ __forceinline__ bool alive() const { return fault == 0; }
+  __device__ __forceinline__ bool dropped(int a, int b) const { return ((iso >> a) | (iso >> b)) & 1u; }
+
+  // ---------------------------------------------------------- load/store --
+  __device__ __forceinline__ void begin(const DevPlanes& P, const Trace& T, uint64_t g_) {
+    g = g_;
+    key = group_key(T.seed, P.gbase + g);
+    tick = T.tick;
+    now = T.now;
+    d_term = d_last = d_commit = d_dl = d_rs = 0;
+    known = 0;
+    iso = 0;
+#pragma unroll
+    for (int s = 0; s < NSTAT; ++s) st[s] = 0;
+    cache_leader = -1;
+    cache_from = 0; cache_term = 0; cache_vbase = 0;
+    const int m = P.gmeta[g];
+    meta0 = m;
+    primary = m & 0xF;
+    fault = m >> 4;
+  }
+  __device__ __forceinline__ void load(const DevPlanes& P, bool with_deadlines) {
+    roles = 0; voted = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint64_t i = uint64_t(r) * P.Gp + g;
+      term[r] = P.term[i];
+      last[r] = P.last[i];
+      commit[r] = P.commit[i];
+      const uint32_t x = P.rs[i];
+      roles |= (x & 3u) << (2 * r);
+      voted |= ((x >> 2) & 1u) << r;
+      dur[r] = int(x >> 3);
+      if (with_deadlines) dl[r] = P.deadline[i];
+      else dl[r] = 0;
+    }
+    known = with_deadlines ? (1u << R) - 1u : 0u;
+  }
+  __device__ __forceinline__ void store(const DevPlanes& P) const {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint64_t i = uint64_t(r) * P.Gp + g;
+      if ((d_term >> r) & 1u) P.term[i] = term[r];
+      if ((d_last >> r) & 1u) P.last[i] = last[r];
+      if ((d_commit >> r) & 1u) P.commit[i] = commit[r];
+      if ((d_dl >> r) & 1u) P.deadline[i] = dl[r];
+      if ((d_rs >> r) & 1u)
+        P.rs[i] = uint16_t(((roles >> (2 * r)) & 3u) | (((voted >> r) & 1u) << 2) | (uint32_t(dur[r]) << 3));
+    }
+    const int m = primary | (fault << 4);
+    if (m != meta0) P.gmeta[g] = uint8_t(m);
+  }
+
+  __device__ __forceinline__ uint64_t ring(const DevPlanes& P, int r, int idx) const {
+    return (uint64_t(r) * P.K + uint32_t((idx - 1) & int(P.kmask))) * P.Gp + g;
+  }
+  // Timer of replica r (lazy: only read from HBM when a timeout check needs it).
+  template <int Rp>
+  __device__ __forceinline__ int deadline_of(const DevPlanes& P) {
+    if (!((known >> Rp) & 1u)) {
+      dl[Rp] = P.deadline[uint64_t(Rp) * P.Gp + g];
+      known |= 1u << Rp;
+    }
+    return dl[Rp];
+  }
+
+  // ------------------------------------------------------------ timers --
+  __device__ __forceinline__ int draw(const Trace& T, int r, bool cand) const {
+    const uint64_t h = rng_k(key, uint32_t(r), cand ? ST_TIMER_C : ST_TIMER_F, uint64_t(tick));
+    const uint32_t span = uint32_t(cand ? T.c_span : T.f_span);
+    return (cand ? T.c_min : T.f_min) + int(uint32_t(h >> 32) % span);
+  }
+  // FollowerRun entry: d = rand.Intn(20)+10, timer started (main.go:113-115).
+  template <int Rp>
+  __device__ __forceinline__ void enter_follower(const Trace& T) {
+    set_role(Rp, ROLE_F);
+    dur[Rp] = draw(T, Rp, false);
+    dl[Rp] = now + dur[Rp];
+    known |= 1u << Rp;
+    d_dl |= 1u << Rp;
+  }
+  // CandidateRun entry: d = rand.Intn(4)+10 (main.go:194-195).
+  __device__ __forceinline__ void enter_candidate(const Trace& T, int c) {
+    set_role(c, ROLE_C);
+    const int d = draw(T, c, true);
+    put(dur, c, d);
+    put(dl, c, now + d);
+    known |= 1u << c;
+    d_dl |= 1u << c;
+  }
+  template <int Rp>
+  __device__ __forceinline__ void reset_timer() {   // timer.Reset(d)
+    dl[Rp] = now + dur[Rp];
+    known |= 1u << Rp;
+    d_dl |= 1u << Rp;
+  }
+  template <int Rp>
+  __device__ __forceinline__ void set_term(int t) {
+    if (term[Rp] != t) { term[Rp] = t; d_term |= 1u << Rp; }
+  }
+
+  // -------------------------------------------- AppendEntries receivers --
+  // FollowerRun case AEReq (main.go:121-156). `src.fetch(j, t, v)` yields
+  // Logs[j].
+  template <int Rp, typename Src>
+  __device__ __forceinline__ AEResp follower_ae(const DevPlanes& P, const AEReq& q, const Src& src) {
+    AEResp res{term[Rp], last[Rp], 0};
+    reset_timer<Rp>();                                        // 124-127
+    if (q.term < term[Rp]) return res;                        // 129-133
+    const int l = last[Rp];
+    if (l > 0) {                                              // 135
+      if (int64_t(l) + q.n < q.prev_idx) return res;          // 137-140
+      if (q.prev_idx < 1 || q.prev_idx > l) { raise(F_PANIC_GETLOG); return res; }  // 142 -> 404
+      if (q.prev_idx <= l - int(P.K)) { raise(F_RING_EVICTED); return res; }
+      if (P.log_term[ring(P, Rp, q.prev_idx)] != q.prev_term) return res;          // 142-145
+    }
+    if (int64_t(l) + q.n > I32MAX) { raise(F_OVERFLOW); return res; }
+    // 148-149: append all Logs at the end (no truncation); only the last K
+    // positions are kept in the ring.
+    const int j0 = q.n > int(P.K) ? q.n - int(P.K) : 0;
+    for (int j = j0; j < q.n; ++j) {
+      int t; int64_t v;
+      src.fetch(j, t, v);
+      const uint64_t o = ring(P, Rp, l + 1 + j);
+      P.log_term[o] = t;
+      P.log_value[o] = v;
+    }
+    const int nl = l + q.n;
+    if (q.n) { last[Rp] = nl; d_last |= 1u << Rp; }
+    if (q.lc > commit[Rp]) {                                  // 151-152: min(LC, len(Log)+1)
+      const int64_t cap = int64_t(nl) + 1;
+      const int nc = int64_t(q.lc) < cap ? q.lc : int(cap);
+      if (nc != commit[Rp]) { commit[Rp] = nc; d_commit |= 1u << Rp; }
+    }
+    set_term<Rp>(q.term);                                     // 155
+    res.term = q.term; res.match = nl; res.ok = 1;            // 156
+    return res;
+  }
+  // CandidateRun case AEReq (main.go:200-223).
+  template <int Rp>
+  __device__ __forceinline__ AEResp candidate_ae(const Trace& T, const AEReq& q) {
+    AEResp res{term[Rp], last[Rp], 0};
+    if (q.term >= term[Rp]) {                                 // 204
+      res.ok = 1;                                             // 205-209 (nothing appended)
+      set_voted(Rp, true);                                    // 211
+      set_term<Rp>(q.term);                                   // 212
+      enter_follower<Rp>(T);                                  // 210, 213-216
+    }
+    return res;
+  }
+  // LeaderRun case AEReq (main.go:309-326).
+  template <int Rp>
+  __device__ __forceinline__ AEResp leader_ae(const Trace& T, const AEReq& q) {
+    AEResp res{term[Rp], 0, 0};
+    if (q.term > term[Rp]) {                                  // 312
+      res.ok = 1;                                             // 313-316 (MatchIndex 0)
+      set_voted(Rp, false);                                   // 318
+      set_term<Rp>(q.term);                                   // 319
+      enter_follower<Rp>(T);                                  // 317, 320
+      if (primary == Rp) primary = NO_PRIMARY;
+    }
+    return res;
+  }
+  // Run (main.go:98-109): the message goes to the receiver's current role.
+  template <int Rp, typename Src>
+  __device__ __forceinline__ AEResp deliver_ae(const DevPlanes& P, const Trace& T, const AEReq& q,
+                                               const Src& src) {
+    const int ro = role(Rp);
+    if (ro == ROLE_F) return follower_ae<Rp>(P, q, src);
+    if (ro == ROLE_C) return candidate_ae<Rp>(T, q);
+    return leader_ae<Rp>(T, q);
+  }
+
+  // ---------------------------------------------- RequestVote receivers --
+  template <int Rp>
+  __device__ __forceinline__ int deliver_vr(const Trace& T, int rterm, int* resp_term) {
+    const int ro = role(Rp);
+    *resp_term = term[Rp];
+    if (ro == ROLE_F) {                                       // main.go:157-170
+      if (rterm < term[Rp] || is_voted(Rp)) return 0;         // 160-162
+      reset_timer<Rp>();                                      // 164-167
+      set_term<Rp>(rterm);                                    // 168
+      set_voted(Rp, true);                                    // 169
+      *resp_term = rterm;
+      return 1;                                               // 170
+    }
+    if (ro == ROLE_C) {                                       // main.go:224-246
+      if (rterm > term[Rp]) {                                 // 227-238
+        set_voted(Rp, true);
+        set_term<Rp>(rterm);
+        enter_follower<Rp>(T);
+        return 1;
+      }
+      reset_timer<Rp>();                                      // 243-246
+      raise(F_DEADLOCK_VRES);                                 // 242: reply into its own VRes
+      return 0;
+    }
+    raise(F_DEADLOCK_LEADER_VREQ);                            // main.go:308: no VReq case
+    return 0;
+  }
+
+  // ------------------------------------------------------- node steps ----
+  // CandidateRun default branch (main.go:253-284); c is a runtime id.
+  __device__ __forceinline__ int candidate_round(const DevPlanes& P, const Trace& T, int c) {
+    int count = 1;                                            // 255
+    set_voted(c, true);                                       // 256
+    const int ct = sel(term, c);
+    static_for<R>([&](auto PI) {                              // 259-269
+      constexpr int p = decltype(PI)::value;
+      if (p == c || !alive() || dropped(c, p)) return;
+      int rt;
+      const int gr = deliver_vr<p>(T, ct, &rt);               // 264-265
+      if (alive() && gr) { ++count; ++st[S_VOTES]; }          // 266-268
+    });
+    if (alive() && 2 * count > R) {                           // 273
+      set_role(c, ROLE_L);                                    // 274
+      // 275-282: MatchIndex 0 / NextIndex 1 for every peer
+      int32_t* row;
+      if (primary == NO_PRIMARY) { primary = c; row = P.lmatch; }
+      else row = P.xmatch + uint64_t(c) * R * P.Gp;
+#pragma unroll
+      for (int p = 0; p < R; ++p)
+        if (p != c) row[uint64_t(p) * P.Gp + g] = 0;
+      ++st[S_WON];
+      return 1;
+    }
+    return 0;
+  }
+
+  // Commit rule (main.go:381-391): exact-value histogram over the peers'
+  // MatchIndex (leader excluded); at most one value can hold a majority.
+  __device__ __forceinline__ int commit_rule(const int (&m)[R], int c, int cm) {
+#pragma unroll
+    for (int p = 0; p < R; ++p) {
+      int cnt = 0;
+#pragma unroll
+      for (int q = 0; q < R; ++q) cnt += (q != c && m[q] == m[p]) ? 1 : 0;
+      if (p != c && 2 * cnt > R && m[p] > cm) {               // 387
+        st[S_COMMITTED] += m[p] - cm;
+        cm = m[p];                                            // 389
+      }
+    }
+    return cm;
+  }
+
+  __device__ __forceinline__ int32_t* match_row(const DevPlanes& P, int c) const {
+    return primary == c ? P.lmatch : P.xmatch + uint64_t(c) * R * P.Gp;
+  }
+
+  // LeaderRun default branch (main.go:332-391) for runtime leader id c.
+  // Src builds the entry source for this leader.
+  template <typename SrcF>
+  __device__ __forceinline__ void leader_round(const DevPlanes& P, const Trace& T, int c, const SrcF& make_src) {
+    const int lt = sel(term, c), ll = sel(last, c);
+    int lc = sel(commit, c);
+    int32_t* row = match_row(P, c);
+    int m[R], m0[R];
+#pragma unroll
+    for (int p = 0; p < R; ++p) {
+      m[p] = (p != c) ? row[uint64_t(p) * P.Gp + g] : 0;
+      m0[p] = m[p];
+    }
+    const auto src0 = make_src(c);
+    static_for<R>([&](auto PI) {                              // 334-379
+      constexpr int p = decltype(PI)::value;
+      if (p == c || !alive()) return;
+      if (dropped(c, p)) { ++st[S_AE_FAIL]; return; }
+      AEReq q;
+      q.term = lt; q.lc = lc;
+      const int nxt = m[p] + 1;                               // NextIndex == MatchIndex + 1
+      int from = 1;
+      if (nxt <= ll) {                                        // 341
+        if (nxt == 1) {                                       // 343-351: whole log
+          q.n = ll; q.prev_idx = 0; q.prev_term = lt; from = 1;
+        } else {                                              // 353-360
+          if (nxt < 1 || m[p] > ll) { raise(F_PANIC_GETLOG); return; }
+          if (m[p] <= ll - int(P.K)) { raise(F_RING_EVICTED); return; }
+          q.prev_term = P.log_term[ring(P, c, m[p])];         // GetLog(MatchIndex).Term
+          q.prev_idx = m[p]; q.n = ll - nxt + 1; from = nxt;
+        }
+      } else {                                                // 364-371: heartbeat
+        q.n = 0; q.prev_idx = m[p]; q.prev_term = lt;
+      }
+      auto src = src0;
+      src.from = from;
+      const AEResp a = deliver_ae<p>(P, T, q, src);           // -> 373
+      if (!alive()) return;
+      if (a.ok) { m[p] = a.match; ++st[S_AE_OK]; }            // 375-378
+      else ++st[S_AE_FAIL];
+    });
+    if (alive()) {
+      const int nc = commit_rule(m, c, lc);
+      if (nc != lc) { put(commit, c, nc); d_commit |= 1u << c; }
+    }
+#pragma unroll
+    for (int p = 0; p < R; ++p)
+      if (p != c && m[p] != m0[p]) row[uint64_t(p) * P.Gp + g] = m[p];
+  }
+
+  // Client append to leader c (main.go:327-329): Log += {Term, Value}; LastApplied++.
+  __device__ __forceinline__ void client_append_value(const DevPlanes& P, int c, int64_t v) {
+    const int l = sel(last, c);
+    if (l >= I32MAX) { raise(F_OVERFLOW); return; }
+    const uint64_t o = ring(P, c, l + 1);
+    P.log_term[o] = sel(term, c);
+    P.log_value[o] = v;
+    put(last, c, l + 1);
+    d_last |= 1u << c;
+  }
+
+  // timer.C (main.go:171-177 follower -> candidate, 248-251 candidate Term++).
+  __device__ __forceinline__ void timeout_fire(const Trace& T, int c) {
+    const int t = sel(term, c);
+    if (t >= I32MAX) { raise(F_OVERFLOW); return; }
+    put(term, c, t + 1);
+    d_term |= 1u << c;
+    ++st[S_BUMPS];
+    enter_candidate(T, c);
+  }
+};
+
+// Entry source of a leader round inside the fused tick: entries appended by
+// this tick's client event are regenerated from the trace RNG, older ones
+// are read from the leader's ring. Held by value (no pointer to the
+// register-resident Group, which would force it into scratch).
+struct TickSrc {
+  const int32_t* lt;
+  const int64_t* lv;
+  uint64_t Gp, g;
+  uint32_t K, kmask;
+  int leader, from;
+  int cache_leader, cache_from, cache_term;
+  uint64_t cache_vbase;
+  __device__ __forceinline__ void fetch(int j, int& t, int64_t& v) const {
+    const int idx = from + j;
+    if (leader == cache_leader && idx >= cache_from) {
+      t = cache_term;
+      v = int64_t(sm64(cache_vbase ^ uint64_t(uint32_t(idx - cache_from))) >> 1);
+    } else {
+      const uint64_t o = (uint64_t(leader) * K + uint32_t((idx - 1) & int(kmask))) * Gp + g;
+      t = lt[o];
+      v = lv[o];
+    }
+  }
+};
+
+// Entry source of a host-supplied AppendEntriesRequest (handler batch API).
+struct HostSrc {
+  const int32_t* et;
+  const int64_t* ev;
+  uint64_t off;
+  int from;
+  __device__ __forceinline__ void fetch(int j, int& t, int64_t& v) const {
+    t = et[off + uint64_t(j)];
+    v = ev[off + uint64_t(j)];
+  }
+};
+
+}  // namespace raftstep

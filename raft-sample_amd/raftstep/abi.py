@@ -1,0 +1,160 @@
+"""ctypes mirror of include/raftstep.h (the C-ABI boundary).
+
+Record layouts are declared twice — as ctypes Structures for scalar calls and
+as numpy structured dtypes for batches — and checked against each other at
+import time, so a header change that is not mirrored here fails loudly.
+"""
+import ctypes as C
+
+import numpy as np
+
+RAFT_ABI_VERSION = 1
+RAFT_MAX_REPLICAS = 8
+
+FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
+ROLE_NAMES = {FOLLOWER: "follower", CANDIDATE: "candidate", LEADER: "leader"}  # main.go:51-57
+
+F_NONE, F_PANIC_GETLOG, F_DEADLOCK_VRES, F_DEADLOCK_LEADER_VREQ, F_RING_EVICTED, F_OVERFLOW = range(6)
+
+STAT_NAMES = ("committed", "elections_won", "term_bumps", "ae_ok", "ae_fail",
+              "votes_granted", "faults", "leader_groups")
+NSTATS = len(STAT_NAMES)
+
+OP_CLIENT_APPEND, OP_LEADER_ROUND, OP_CANDIDATE_ROUND, OP_TIMEOUT, OP_LEADER_COMMIT = 1, 2, 3, 4, 5
+
+RAFT_EINVAL, RAFT_ENOMEM, RAFT_ERANGE, RAFT_ENODEV = -22, -12, -34, -19
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_uint32), ("replicas", C.c_uint32),
+        ("groups", C.c_uint64), ("group_base", C.c_uint64),
+        ("ring_depth", C.c_uint32), ("entries_per_tick", C.c_uint32),
+        ("client_period", C.c_uint32), ("semantics", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("tick_seconds", C.c_int32),
+        ("follower_timeout_min", C.c_int32), ("follower_timeout_span", C.c_int32),
+        ("candidate_timeout_min", C.c_int32), ("candidate_timeout_span", C.c_int32),
+        ("isolate_per_65536", C.c_uint32), ("isolate_min_ticks", C.c_uint32),
+        ("isolate_max_ticks", C.c_uint32),
+        ("device", C.c_int32),
+        ("reserved", C.c_uint32 * 8),
+    ]
+
+
+def default_config(**kw):
+    """Defaults of raft_config_default() (main.go's constants), overridden by kw."""
+    c = Config()
+    c.abi_version = RAFT_ABI_VERSION
+    c.replicas = 3            # main.go:81
+    c.groups = 1
+    c.ring_depth = 32
+    c.entries_per_tick = 1
+    c.client_period = 5       # one write per 10 s (main.go:89) at 2 s per tick
+    c.semantics = 0
+    c.seed = 0x5EED0001
+    c.tick_seconds = 2        # main.go:394
+    c.follower_timeout_min, c.follower_timeout_span = 10, 20    # main.go:114
+    c.candidate_timeout_min, c.candidate_timeout_span = 10, 4   # main.go:194
+    c.isolate_per_65536 = 0
+    c.isolate_min_ticks, c.isolate_max_ticks = 8, 32
+    c.device = 0
+    for k, v in kw.items():
+        if not hasattr(c, k):
+            raise TypeError(f"unknown config field {k!r}")
+        setattr(c, k, v)
+    return c
+
+
+class TickStats(C.Structure):
+    _fields_ = [("v", C.c_int64 * NSTATS)]
+
+
+class StateView(C.Structure):
+    _fields_ = [
+        ("role", C.c_void_p), ("voted", C.c_void_p), ("term", C.c_void_p),
+        ("last", C.c_void_p), ("commit", C.c_void_p), ("deadline", C.c_void_p),
+        ("timeout", C.c_void_p), ("match", C.c_void_p), ("fault", C.c_void_p),
+        ("log_term", C.c_void_p), ("log_value", C.c_void_p),
+    ]
+
+
+STATE_FIELDS = ("role", "voted", "term", "last", "commit", "deadline", "timeout",
+                "match", "fault", "log_term", "log_value")
+
+
+def state_shapes(groups, replicas, ring_depth):
+    G, R, K = groups, replicas, ring_depth
+    return {
+        "role": ((G, R), np.uint8), "voted": ((G, R), np.uint8),
+        "term": ((G, R), np.int32), "last": ((G, R), np.int32),
+        "commit": ((G, R), np.int32), "deadline": ((G, R), np.int32),
+        "timeout": ((G, R), np.int32), "match": ((G, R, R), np.int32),
+        "fault": ((G,), np.uint8), "log_term": ((G, R, K), np.int32),
+        "log_value": ((G, R, K), np.int64),
+    }
+
+
+def empty_state(groups, replicas, ring_depth):
+    return {k: np.zeros(s, d) for k, (s, d) in state_shapes(groups, replicas, ring_depth).items()}
+
+
+def make_view(state):
+    v = StateView()
+    for k in STATE_FIELDS:
+        a = state.get(k)
+        if a is not None:
+            assert a.flags["C_CONTIGUOUS"], k
+            setattr(v, k, a.ctypes.data)
+    return v
+
+
+# batch records (numpy, C layout)
+AE_REQ = np.dtype([("group", "<u8"), ("to", "<u4"), ("leader_id", "<u4"), ("term", "<i8"),
+                   ("prev_log_index", "<i8"), ("prev_log_term", "<i8"), ("leader_commit", "<i8"),
+                   ("entries_offset", "<u8"), ("n_entries", "<u8")], align=True)
+AE_RESP = np.dtype([("term", "<i8"), ("match_index", "<i8"), ("success", "<i4"), ("fault", "<i4")],
+                   align=True)
+LOG_ENTRY = np.dtype([("term", "<i8"), ("value", "<i8")], align=True)
+VOTE_REQ = np.dtype([("group", "<u8"), ("to", "<u4"), ("candidate_id", "<u4"), ("term", "<i8"),
+                     ("last_log_index", "<i8"), ("last_log_term", "<i8")], align=True)
+VOTE_RESP = np.dtype([("term", "<i8"), ("vote_granted", "<i4"), ("fault", "<i4")], align=True)
+GROUP_OP = np.dtype([("group", "<u8"), ("replica", "<u4"), ("kind", "<u4"), ("arg", "<i8")], align=True)
+OP_RESULT = np.dtype([("status", "<i4"), ("fault", "<i4"), ("value", "<i8")], align=True)
+
+assert AE_REQ.itemsize == 64 and AE_RESP.itemsize == 24 and LOG_ENTRY.itemsize == 16
+assert VOTE_REQ.itemsize == 40 and VOTE_RESP.itemsize == 16
+assert GROUP_OP.itemsize == 24 and OP_RESULT.itemsize == 16
+assert C.sizeof(Config) == 120, C.sizeof(Config)
+
+# exported symbols of libraftstep.so (the C-ABI), with ctypes signatures
+P = C.c_void_p
+SIGNATURES = {
+    "raft_config_default": (None, [P]),
+    "raft_engine_create": (C.c_int, [P, C.POINTER(C.c_void_p)]),
+    "raft_engine_destroy": (C.c_int, [P]),
+    "raft_last_error": (C.c_char_p, []),
+    "raft_engine_info": (C.c_int, [P, P, P]),
+    "raft_init_new_nodes": (C.c_int, [P, C.c_int64]),
+    "raft_init_steady": (C.c_int, [P, C.c_int32, C.c_int64]),
+    "raft_load_state": (C.c_int, [P, P]),
+    "raft_store_state": (C.c_int, [P, P]),
+    "raft_tick": (C.c_int, [P, C.c_int64, C.c_uint32, P]),
+    "raft_sync": (C.c_int, [P]),
+    "raft_append_entries_batch": (C.c_int, [P, C.c_int64, P, C.c_size_t, P, C.c_size_t, P]),
+    "raft_request_vote_batch": (C.c_int, [P, C.c_int64, P, C.c_size_t, P]),
+    "raft_group_ops_batch": (C.c_int, [P, C.c_int64, P, C.c_size_t, P]),
+    "raft_comm_unique_id": (C.c_int, [P]),
+    "raft_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),
+    "raft_comm_allreduce_stats": (C.c_int, [P, P]),
+    "raft_profile_enable": (C.c_int, [P, C.c_int]),
+    "raft_profile_read": (C.c_int, [P, P, P]),
+}
+
+
+def bind(lib):
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib

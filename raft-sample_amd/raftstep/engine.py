@@ -1,0 +1,169 @@
+"""Python handle over libraftstep.so (the HIP engine), through the C-ABI only.
+
+There is deliberately no CPU fallback: if the library or a GPU is missing
+the constructor raises. The CPU restatement lives in oracle/ and is test
+infrastructure, never imported from here.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libraftstep.so"))
+_lib = None
+
+
+class RaftError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"raftstep error {code}: {msg}")
+        self.code = code
+
+
+def load_library(path=None):
+    """Load and bind libraftstep.so; raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is None or path:
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RaftError(-2, f"{p} not built (run __graft_entry__.build() or make -C raft-sample_amd/csrc)")
+        _lib = abi.bind(C.CDLL(p))
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RaftError(rc, load_library().raft_last_error().decode(errors="replace"))
+
+
+def _ptr(a):
+    return a.ctypes.data if a is not None and a.size else None
+
+
+class Engine:
+    """One engine = the groups of one GPU (config.group_base.. +groups)."""
+
+    def __init__(self, cfg=None, **kw):
+        self.lib = load_library()
+        self.cfg = cfg if cfg is not None else abi.default_config(**kw)
+        if cfg is not None and kw:
+            for k, v in kw.items():
+                setattr(self.cfg, k, v)
+        h = C.c_void_p()
+        _check(self.lib.raft_engine_create(C.byref(self.cfg), C.byref(h)))
+        self.h = h
+
+    # -- lifecycle -----------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.raft_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def groups(self):
+        return self.cfg.groups
+
+    @property
+    def replicas(self):
+        return self.cfg.replicas
+
+    def device_bytes(self):
+        b = C.c_uint64()
+        _check(self.lib.raft_engine_info(self.h, None, C.byref(b)))
+        return b.value
+
+    # -- state ---------------------------------------------------------
+    def init_new_nodes(self, tick0=0):
+        _check(self.lib.raft_init_new_nodes(self.h, tick0))
+
+    def init_steady(self, leader=0, tick0=0):
+        _check(self.lib.raft_init_steady(self.h, leader, tick0))
+
+    def store_state(self, logs=True):
+        st = abi.empty_state(self.cfg.groups, self.cfg.replicas, self.cfg.ring_depth)
+        if not logs:
+            st.pop("log_term")
+            st.pop("log_value")
+        v = abi.make_view(st)
+        _check(self.lib.raft_store_state(self.h, C.byref(v)))
+        return st
+
+    def load_state(self, st):
+        st = {k: np.ascontiguousarray(st[k]) for k in abi.STATE_FIELDS}
+        v = abi.make_view(st)
+        _check(self.lib.raft_load_state(self.h, C.byref(v)))
+
+    # -- the fused tick ------------------------------------------------
+    def tick(self, first_tick, nticks=1, stats=True):
+        if stats:
+            s = abi.TickStats()
+            _check(self.lib.raft_tick(self.h, first_tick, nticks, C.byref(s)))
+            return np.array(s.v, dtype=np.int64)
+        _check(self.lib.raft_tick(self.h, first_tick, nticks, None))
+        return None
+
+    def sync(self):
+        _check(self.lib.raft_sync(self.h))
+
+    # -- handler batches -----------------------------------------------
+    def append_entries(self, now_tick, reqs, entries=None):
+        reqs = np.ascontiguousarray(reqs, dtype=abi.AE_REQ)
+        ents = np.ascontiguousarray(entries if entries is not None else np.zeros(0, abi.LOG_ENTRY),
+                                    dtype=abi.LOG_ENTRY)
+        out = np.zeros(len(reqs), abi.AE_RESP)
+        _check(self.lib.raft_append_entries_batch(self.h, now_tick, _ptr(reqs), len(reqs), _ptr(ents),
+                                                  len(ents), _ptr(out)))
+        return out
+
+    def request_vote(self, now_tick, reqs):
+        reqs = np.ascontiguousarray(reqs, dtype=abi.VOTE_REQ)
+        out = np.zeros(len(reqs), abi.VOTE_RESP)
+        _check(self.lib.raft_request_vote_batch(self.h, now_tick, _ptr(reqs), len(reqs), _ptr(out)))
+        return out
+
+    def group_ops(self, now_tick, ops):
+        ops = np.ascontiguousarray(ops, dtype=abi.GROUP_OP)
+        out = np.zeros(len(ops), abi.OP_RESULT)
+        _check(self.lib.raft_group_ops_batch(self.h, now_tick, _ptr(ops), len(ops), _ptr(out)))
+        return out
+
+    # -- multi-GPU -----------------------------------------------------
+    @staticmethod
+    def comm_unique_id():
+        buf = (C.c_uint8 * 128)()
+        _check(load_library().raft_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        _check(self.lib.raft_comm_init(self.h, nranks, rank, buf))
+
+    def allreduce_stats(self, stats):
+        s = abi.TickStats()
+        for i, x in enumerate(stats):
+            s.v[i] = int(x)
+        _check(self.lib.raft_comm_allreduce_stats(self.h, C.byref(s)))
+        return np.array(s.v, dtype=np.int64)
+
+    # -- instrumentation -----------------------------------------------
+    def profile(self, enable=True):
+        _check(self.lib.raft_profile_enable(self.h, 1 if enable else 0))
+
+    def profile_read(self):
+        ms, n = C.c_double(), C.c_uint64()
+        _check(self.lib.raft_profile_read(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
