@@ -4,12 +4,13 @@
  * __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.
  * The product (libraftstep.so) never links, loads or calls this code.
  *
- * Parity pinning: the reference is Go-only and no Go toolchain exists in
- * the build container; the reference ships no tests or
- * golden vectors. The oracle is therefore pinned by the hand-derived
- * known-answer tests of SURVEY.md Appendix B (tests/test_oracle_kat.py),
- * each derived from main.go line by line, plus the CRC-free RNG check
- * vectors in tests/golden/.
+ * PARITY UNPINNED by reference outputs: the reference is Go-only, no Go
+ * toolchain exists in the build container or on the GPU box (SURVEY.md
+ * §8(c)), and the reference ships no tests, fixtures or golden vectors. The
+ * oracle is instead pinned by the hand-derived known-answer tests of
+ * SURVEY.md Appendix B (tests/kat_cases.py via tests/test_oracle_kat.py),
+ * each derived from the main.go text; tests/golden/ freezes the trace
+ * definition (RNG vectors, oracle-generated traces).
  *
  * State is array-of-structs, one group at a time, logs are growable
  * arrays like Go slices (main.go:148, 328) with int64 terms/indices like

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -63,6 +64,10 @@ struct raft_engine {
   // per-tick statistics: [cap][STAT_SLOTS][NSTAT] u64
   unsigned long long* hist = nullptr;
   uint32_t hist_cap = 0;
+  // worklist of groups the steady-state kernel hands to the general kernel
+  uint32_t* work = nullptr;
+  uint32_t* wcount = nullptr;   // [2], indexed by tick parity
+  int force_general = 0;        // debug: route every group through the general kernel
   // handler-batch staging
   void* stage = nullptr;
   size_t stage_cap = 0;
@@ -249,7 +254,9 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
       (c.isolate_min_ticks < 1 || c.isolate_max_ticks > 32 || c.isolate_min_ticks > c.isolate_max_ticks))
     return fail(RAFT_EINVAL, "isolation length must satisfy 1 <= min <= max <= 32");
   const uint64_t Gp = (c.groups + 255) & ~uint64_t(255);
-  if (Gp * c.replicas * c.ring_depth >= (uint64_t(1) << 40)) return fail(RAFT_EINVAL, "state too large");
+  // device addressing uses 32-bit byte offsets inside one replica's ring
+  if (Gp * c.ring_depth * 8 > (uint64_t(1) << 32))
+    return fail(RAFT_EINVAL, "groups x ring_depth too large for one engine (need groups*ring_depth <= 2^29)");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RAFT_ENODEV, "no HIP device");
   if (c.device < 0 || c.device >= ndev) return fail(RAFT_ENODEV, "device %d out of range", c.device);
@@ -272,6 +279,9 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.lmatch), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.xmatch), R * R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.gmeta), Gp);
+  A(reinterpret_cast<void**>(&e->P.lterm), R * Gp * 4);
+  A(reinterpret_cast<void**>(&e->work), Gp * 4);
+  A(reinterpret_cast<void**>(&e->wcount), 256);
   A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.log_value), R * K * Gp * 8);
   if (rc == RAFT_OK) {
@@ -289,6 +299,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->P.gbase = c.group_base;
   e->P.K = c.ring_depth;
   e->P.kmask = c.ring_depth - 1;
+  if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
   // zero everything once so that padding / unused rows are deterministic
   for (void* p : e->allocs) (void)p;
   hipError_t z = hipSuccess;
@@ -300,6 +311,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetAsync(e->P.lmatch, 0, R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.xmatch, 0, R * R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gmeta, NO_PRIMARY, Gp, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.lterm, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, 256, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_value, 0, R * K * Gp * 8, e->stream) : z;
   z = z == hipSuccess ? hipStreamSynchronize(e->stream) : z;
@@ -370,6 +383,8 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!rc) rc = d2h(e, xm, e->P.xmatch, R * R * Gp);
   if (!rc) rc = d2h(e, meta, e->P.gmeta, Gp);
   const bool logs = v->log_term || v->log_value;
+  std::vector<int32_t> ltm;
+  if (!rc && logs) rc = d2h(e, ltm, e->P.lterm, R * Gp);
   if (!rc && logs) rc = d2h(e, lt, e->P.log_term, R * K * Gp);
   if (!rc && logs) rc = d2h(e, lv, e->P.log_value, R * K * Gp);
   if (rc) return rc;
@@ -394,6 +409,12 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
             m = (int(r) == primary) ? lm[p * Gp + g] : xm[(r * R + p) * Gp + g];
           v->match[c * R + p] = m;
         }
+      if (logs && last[d] > 0) {
+        const int32_t want = lt[(r * K + uint64_t((last[d] - 1) & int64_t(K - 1))) * Gp + g];
+        if (ltm[d] != want)
+          return fail(RAFT_EINVAL, "internal: last-entry term cache of group %llu replica %llu is %d, ring says %d",
+                      (unsigned long long)g, (unsigned long long)r, ltm[d], want);
+      }
       if (logs) {
         const int64_t l = last[d];
         for (uint64_t s = 0; s < K; ++s) {
@@ -422,6 +443,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   std::vector<uint16_t> rs(R * Gp, 0);
   std::vector<uint8_t> meta(Gp, uint8_t(NO_PRIMARY));
   std::vector<int64_t> lv(R * K * Gp, 0);
+  std::vector<int32_t> ltm(R * Gp, 0);
   for (uint64_t g = 0; g < G; ++g) {
     if (v->fault[g] > RAFT_F_OVERFLOW) return fail(RAFT_EINVAL, "group %llu: bad fault code", (unsigned long long)g);
     int primary = NO_PRIMARY;
@@ -450,6 +472,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
         lt[(r * K + s) * Gp + g] = v->log_term[c * K + s];
         lv[(r * K + s) * Gp + g] = v->log_value[c * K + s];
       }
+      if (v->last[c] > 0) ltm[d] = v->log_term[c * K + uint64_t((v->last[c] - 1) & int64_t(K - 1))];
     }
   }
   int rc = RAFT_OK;
@@ -461,6 +484,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.lmatch, lm);
   if (!rc) rc = h2d(e, e->P.xmatch, xm);
   if (!rc) rc = h2d(e, e->P.gmeta, meta);
+  if (!rc) rc = h2d(e, e->P.lterm, ltm);
   if (!rc) rc = h2d(e, e->P.log_term, lt);
   if (!rc) rc = h2d(e, e->P.log_value, lv);
   if (rc) return rc;
@@ -475,11 +499,15 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     if (int rc = ensure_hist(e, nticks)) return rc;
     HIPCHK(hipMemsetAsync(e->hist, 0, size_t(nticks) * STAT_SLOTS * NSTAT * 8, e->stream));
   }
+  HIPCHK(hipMemsetAsync(e->wcount, 0, 2 * sizeof(uint32_t), e->stream));
   for (uint32_t i = 0; i < nticks; ++i) {
     const int64_t t = first_tick + int64_t(i);
     const Trace T = make_trace(e, t);
     const uint32_t period = e->cfg.client_period;
     const uint32_t E = (period && (t % int64_t(period)) == 0) ? e->cfg.entries_per_tick : 0;
+    unsigned long long* st = stats ? e->hist + size_t(i) * STAT_SLOTS * NSTAT : nullptr;
+    uint32_t* cnt = e->wcount + (t & 1);
+    uint32_t* next = e->wcount + ((t + 1) & 1);
     hipEvent_t a = nullptr, b = nullptr;
     if (e->prof) {
       a = next_event(e);
@@ -487,8 +515,9 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
       HIPCHK(hipEventRecord(a, e->stream));
     }
-    HIPCHK(launch_tick(e->R, e->P, T, E, stats ? e->hist + size_t(i) * STAT_SLOTS * NSTAT : nullptr, e->stream));
+    HIPCHK(launch_tick_fast(e->R, e->P, T, E, st, e->work, cnt, e->force_general, e->stream));
     if (e->prof) HIPCHK(hipEventRecord(b, e->stream));
+    HIPCHK(launch_tick_slow(e->R, e->P, T, E, st, e->work, cnt, next, e->stream));
   }
   if (stats && e->comm)
     RCCLCHK(ncclAllReduce(e->hist, e->hist, size_t(nticks) * STAT_SLOTS * NSTAT, ncclUint64, ncclSum, e->comm,

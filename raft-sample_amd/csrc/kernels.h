@@ -28,8 +28,12 @@ struct DevRes {
   int64_t value;      // AE: MatchIndex; VR: granted; ops: see raft_op_result
 };
 
-hipError_t launch_tick(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
-                       hipStream_t s);
+// Steady-state fast kernel; groups it does not take go to `work`.
+hipError_t launch_tick_fast(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
+                            uint32_t* work, uint32_t* work_count, int force_slow, hipStream_t s);
+// General kernel over the worklist; zeroes `next_count` for the next tick.
+hipError_t launch_tick_slow(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
+                            const uint32_t* work, const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
 hipError_t launch_ops(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
                       const int32_t* et, const int64_t* ev, DevRes* out, hipStream_t s);
 hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_t s);

@@ -9,6 +9,8 @@
 //  init_*_kernel<R>: NewNode state / post-election state.
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace raftstep {
 
 // EXT isolation windows (same definition as oracle_isolated()).
@@ -61,11 +63,14 @@ __device__ __forceinline__ void run_tick(Group<R>& G, const DevPlanes& P, const 
       }
       const int e0 = n_ok > int(P.K) ? n_ok - int(P.K) : 0;   // only the last K stay in the ring
       for (int e = e0; e < n_ok; ++e) {
-        const uint64_t o = G.ring(P, r, l + 1 + e);
-        P.log_term[o] = G.term[r];
-        P.log_value[o] = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+        G.ring_term(P, r, l + 1 + e) = G.term[r];
+        G.ring_value(P, r, l + 1 + e) = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
       }
-      if (n_ok) { G.last[r] = l + n_ok; G.d_last |= 1u << r; }
+      if (n_ok) {
+        G.last[r] = l + n_ok;
+        G.d_last |= 1u << r;
+        at(prow(P.lterm, r, P.Gp), G.g) = G.term[r];
+      }
       if (n_ok < int(E)) G.raise(F_OVERFLOW);
     });
   }
@@ -112,37 +117,198 @@ __device__ __forceinline__ void run_tick(Group<R>& G, const DevPlanes& P, const 
   }
 }
 
-template <int R>
-__global__ __launch_bounds__(256) void tick_kernel(DevPlanes P, Trace T, uint32_t E,
-                                                   unsigned long long* stats) {
-  const uint64_t g = uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  int st[NSTAT];
-#pragma unroll
-  for (int s = 0; s < NSTAT; ++s) st[s] = 0;
-  if (g < P.G) {
-    Group<R> G;
-    G.begin(P, T, g);
-    if (G.fault == 0) {
-      G.load(P, false);
-      run_tick<R>(G, P, T, E);
-      G.store(P);
-#pragma unroll
-      for (int s = 0; s < NSTAT; ++s) st[s] = G.st[s];
-    }
-  }
-  if (!stats) return;
-  __shared__ long long red[NSTAT][4];
+// Block-level sum of per-lane counters into the tick's stats slot (one
+// device-scope atomic per non-zero counter per block, spread over
+// STAT_SLOTS slots).
+template <int N>
+__device__ __forceinline__ void block_stats(const int (&v)[N], const int (&idx)[N], unsigned long long* stats) {
+  __shared__ long long red[N][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int s = 0; s < NSTAT; ++s) {
-    const long long w = wave_sum(st[s]);
+  for (int s = 0; s < N; ++s) {
+    const long long w = wave_sum(v[s]);
     if (lane == 0) red[s][wave] = w;
   }
   __syncthreads();
-  if (threadIdx.x < NSTAT) {
+  if (threadIdx.x < N) {
     const int s = threadIdx.x;
-    const long long v = red[s][0] + red[s][1] + red[s][2] + red[s][3];
-    if (v) atomicAdd(&stats[(blockIdx.x % STAT_SLOTS) * NSTAT + s], (unsigned long long)v);
+    const long long x = red[s][0] + red[s][1] + red[s][2] + red[s][3];
+    int which = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) which = (s == k) ? idx[k] : which;
+    if (x) atomicAdd(&stats[(blockIdx.x % STAT_SLOTS) * NSTAT + which], (unsigned long long)x);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Steady-state tick (the metric path). A group qualifies when it is not
+// frozen, its only leader is its primary, every other replica is a
+// follower, no EXT isolation touches it this tick, and every peer's
+// MatchIndex equals the leader's LastApplied (NextIndex = LastApplied+1).
+// For such a group the tick is exactly: client append (main.go:327-329),
+// one AppendEntries per follower carrying just this tick's entries
+// (main.go:341-372 -> 121-156), the responses (main.go:375-378) and the
+// commit rule (main.go:381-391); no timer can expire (every follower's timer
+// is reset by the AppendEntries, main.go:124-127). Anything else — or any
+// condition on the way that would fault, or need a ring read — sends the
+// group to the general kernel via the worklist before a single store.
+template <int R>
+__global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, uint32_t E, unsigned long long* stats,
+                                                        uint32_t* work, uint32_t* work_count, int force_slow) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  int sv[4] = {0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups
+  bool bail = false;
+  if (g < P.G) {
+    const int meta = at(P.gmeta, g);
+    const int c = meta & 0xF;
+    bail = force_slow || (meta >> 4) != 0 || c >= R;
+    int term[R], last[R], commit[R], lt[R], dur[R], m[R];
+    if (!bail) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t x = at(prow(P.rs, r, P.Gp), g);
+        const int want = (r == c) ? ROLE_L : ROLE_F;
+        bail |= int(x & 3u) != want;
+        dur[r] = int(x >> 3);
+        term[r] = at(prow(P.term, r, P.Gp), g);
+        last[r] = at(prow(P.last, r, P.Gp), g);
+        commit[r] = at(prow(P.commit, r, P.Gp), g);
+        lt[r] = at(prow(P.lterm, r, P.Gp), g);
+        m[r] = (r != c) ? at(prow(P.lmatch, r, P.Gp), g) : 0;
+      }
+    }
+    uint64_t key = 0;
+    if (!bail && (T.iso_p || E)) key = group_key(T.seed, P.gbase + g);
+    if (!bail && T.iso_p) bail = isolation_mask<R>(key, T) != 0;
+    // leader view
+    const int Lt = sel(term, c), Ll = sel(last, c), Lc = sel(commit, c), Llt = sel(lt, c);
+    const int n = int(E);
+    if (!bail) bail = int64_t(Ll) + n > I32MAX || n >= int(P.K);
+#pragma unroll
+    for (int p = 0; p < R; ++p) bail |= (p != c) && m[p] != Ll;
+    // one AppendEntries shape for every peer (NextIndex == Ll+1)
+    int prev_idx, prev_term;
+    if (n == 0 || Ll == 0) { prev_idx = Ll; prev_term = Lt; }   // heartbeat / whole-log (PrevLogIndex 0)
+    else { prev_idx = Ll; prev_term = Llt; }                      // GetLog(MatchIndex).Term
+    uint32_t okm = 0, cch = 0, mch = 0, ltch = 0;
+    if (!bail) {
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        if (p == c) continue;
+        bool ok = Lt >= term[p];                                  // main.go:129-133
+        const int l = last[p];
+        if (ok && l > 0) {                                        // main.go:135
+          if (int64_t(l) + n < prev_idx) ok = false;              // 137-140
+          else if (prev_idx < 1 || prev_idx > l || prev_idx <= l - int(P.K) || prev_idx != l) bail = true;
+          else ok = lt[p] == prev_term;                           // 142-145 (GetLog(l) == last entry)
+        }
+        if (ok && int64_t(l) + n > I32MAX) bail = true;
+        if (ok) {
+          const int nl = l + n;                                   // 148-149
+          last[p] = nl;
+          if (n && lt[p] != Lt) ltch |= 1u << p;
+          if (Lc > commit[p]) {                                   // 151-152
+            const int nc = Lc < nl + 1 ? Lc : nl + 1;
+            if (nc != commit[p]) { commit[p] = nc; cch |= 1u << p; }
+          }
+          if (nl != m[p]) { m[p] = nl; mch |= 1u << p; }          // 156 -> 375-377
+          okm |= 1u << p;
+        }
+      }
+    }
+    if (!bail) {
+      // commit rule (main.go:381-391)
+      int cm = Lc;
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        int cnt = 0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) cnt += (q != c && m[q] == m[p]) ? 1 : 0;
+        if (p != c && 2 * cnt > R && m[p] > cm) cm = m[p];
+      }
+      sv[0] = cm - Lc;
+      sv[1] = __builtin_popcount(okm);
+      sv[2] = (R - 1) - sv[1];
+      sv[3] = 1;
+      // ---- stores (no bail past this point) ----
+      const int newL = Ll + n;
+      if (n) {
+        at(P.last + uint64_t(c) * P.Gp, g) = newL;
+        if (Llt != Lt) at(P.lterm + uint64_t(c) * P.Gp, g) = Lt;
+      }
+      if (cm != Lc) at(P.commit + uint64_t(c) * P.Gp, g) = cm;
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        if (p == c) continue;
+        at(prow(P.deadline, p, P.Gp), g) = T.now + dur[p];        // timer.Reset(d), main.go:124-127
+        if ((okm >> p) & 1u) {
+          if (n) at(prow(P.last, p, P.Gp), g) = last[p];
+          if ((mch >> p) & 1u) at(prow(P.lmatch, p, P.Gp), g) = m[p];
+          if ((cch >> p) & 1u) at(prow(P.commit, p, P.Gp), g) = commit[p];
+          if ((ltch >> p) & 1u) at(prow(P.lterm, p, P.Gp), g) = Lt;
+          if (term[p] != Lt) at(prow(P.term, p, P.Gp), g) = Lt;  // main.go:155
+        }
+      }
+      // this tick's entries: leader log + every follower that accepted
+      if (n) {
+        const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+        for (int e = 0; e < n; ++e) {
+          const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+          const uint32_t o = uint32_t((Ll + e) & int(P.kmask)) * uint32_t(P.Gp) + g;
+          const uint64_t cb = uint64_t(c) * P.K * P.Gp;
+          at(P.log_term + cb, o) = Lt;
+          at(P.log_value + cb, o) = v;
+#pragma unroll
+          for (int p = 0; p < R; ++p) {
+            if (p == c || !((okm >> p) & 1u)) continue;
+            const uint32_t op = uint32_t((last[p] - n + e) & int(P.kmask)) * uint32_t(P.Gp) + g;
+            const uint64_t pb = uint64_t(p) * P.K * P.Gp;
+            at(P.log_term + pb, op) = Lt;
+            at(P.log_value + pb, op) = v;
+          }
+        }
+      }
+    }
+  }
+  // groups that need the general path go to the worklist (one atomic per wave)
+  const uint64_t bm = __ballot(bail);
+  if (bm) {
+    const int lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (lane == __builtin_ctzll(bm)) base = atomicAdd(work_count, uint32_t(__popcll(bm)));
+    base = __shfl(base, __builtin_ctzll(bm));
+    if (bail) work[base + uint32_t(__popcll(bm & ((1ull << lane) - 1ull)))] = g;
+  }
+  if (stats) {
+    const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
+    block_stats<4>(sv, idx, stats);
+  }
+}
+
+// General tick for the groups on the worklist: the full REF semantics of
+// run_tick() (elections, candidates, step-downs, faults, EXT drops).
+template <int R>
+__global__ __launch_bounds__(256) void tick_slow_kernel(DevPlanes P, Trace T, uint32_t E, unsigned long long* stats,
+                                                        const uint32_t* work, const uint32_t* work_count,
+                                                        uint32_t* next_count) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *next_count = 0;
+  const uint32_t n = *work_count;
+  int st[NSTAT];
+#pragma unroll
+  for (int s = 0; s < NSTAT; ++s) st[s] = 0;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    Group<R> G;
+    G.begin(P, T, work[i]);
+    if (G.fault) continue;
+    G.load(P, false);
+    run_tick<R>(G, P, T, E);
+    G.store(P);
+#pragma unroll
+    for (int s = 0; s < NSTAT; ++s) st[s] += G.st[s];
+  }
+  if (stats && n) {
+    const int idx[NSTAT] = {0, 1, 2, 3, 4, 5, 6, 7};
+    block_stats<NSTAT>(st, idx, stats);
   }
 }
 
@@ -161,7 +327,7 @@ __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const De
   const DevOp op = ops[i];
   DevRes res{0, 0, 0, 0, 0};
   Group<R> G;
-  G.begin(P, T, op.group);
+  G.begin(P, T, uint32_t(op.group));
   if (G.fault) {
     res.fault = G.fault;
     out[i] = res;
@@ -217,10 +383,8 @@ __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const De
       break;
     case OP_LEADER_COMMIT: {
       if (ro != ROLE_L) { res.status = -22; break; }
-      const int32_t* row = G.match_row(P, x);
       int m[R];
-#pragma unroll
-      for (int p = 0; p < R; ++p) m[p] = (p != x) ? row[uint64_t(p) * P.Gp + G.g] : 0;
+      G.load_match(P, x, m);
       const int lc = sel(G.commit, x);
       const int nc = G.commit_rule(m, x, lc);
       if (nc != lc) { put(G.commit, x, nc); G.d_commit |= 1u << x; }
@@ -249,6 +413,7 @@ __global__ __launch_bounds__(256) void init_new_kernel(DevPlanes P, Trace T) {
     P.term[i] = 0; P.last[i] = 0; P.commit[i] = 0;
     P.deadline[i] = T.now + d;
     P.rs[i] = uint16_t(ROLE_F | (uint32_t(d) << 3));
+    P.lterm[i] = 0;
   }
   P.gmeta[g] = uint8_t(NO_PRIMARY);
 }
@@ -272,6 +437,7 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
     P.deadline[i] = T.now + d;
     P.rs[i] = uint16_t((isL ? ROLE_L : ROLE_F) | (1u << 2) | (uint32_t(d) << 3));
     P.lmatch[i] = 0;
+    P.lterm[i] = 0;
   }
   P.gmeta[g] = uint8_t(L);
 }
@@ -292,9 +458,17 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
 
 static inline dim3 grid_for(uint64_t n) { return dim3(unsigned((n + 255) / 256)); }
 
-hipError_t launch_tick(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
-                       hipStream_t s) {
-  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(tick_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P, T, E, stats));
+hipError_t launch_tick_fast(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
+                            uint32_t* work, uint32_t* work_count, int force_slow, hipStream_t s) {
+  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(tick_fast_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P, T, E, stats, work,
+                                        work_count, force_slow));
+  return hipGetLastError();
+}
+hipError_t launch_tick_slow(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
+                            const uint32_t* work, const uint32_t* work_count, uint32_t* next_count, hipStream_t s) {
+  const unsigned blocks = unsigned(std::min<uint64_t>((P.G + 255) / 256, 1024));
+  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(tick_slow_kernel<RR>, dim3(blocks), dim3(256), 0, s, P, T, E, stats, work,
+                                        work_count, next_count));
   return hipGetLastError();
 }
 hipError_t launch_ops(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,

@@ -47,6 +47,7 @@ struct DevPlanes {
   int32_t* lmatch;     // [R][Gp] MatchIndex row of the group's primary leader (main.go:29)
   int32_t* xmatch;     // [R][R][Gp] rows of any further concurrent leaders (EXT only)
   uint8_t* gmeta;      // primary leader id:4 | fault:4
+  int32_t* lterm;      // [R][Gp] Log[len-1].Term: cached term of each replica's last entry
   int32_t* log_term;   // Log.Term  ring
   int64_t* log_value;  // Log.Value ring
   uint64_t Gp;         // plane pitch (groups, padded)
@@ -55,6 +56,21 @@ struct DevPlanes {
   uint32_t K;          // ring depth (power of two)
   uint32_t kmask;
 };
+
+// Addressing: every access is a wave-uniform base (SGPRs: plane + replica
+// row, or replica ring) plus a 32-bit per-lane byte offset, so the compiler
+// emits global_load/store with an SGPR base and ONE shared VGPR offset
+// instead of a 64-bit VGPR address per (plane, replica). The engine
+// guarantees every offset fits 32 bits (Gp*4 and K*Gp*8 < 2^32).
+template <typename T>
+__device__ __forceinline__ T* prow(T* plane, int r, uint64_t Gp) {
+  return plane + uint64_t(r) * Gp;
+}
+template <typename T>
+__device__ __forceinline__ T& at(T* base, uint32_t idx) {
+  using B = std::conditional_t<std::is_const_v<T>, const char, char>;
+  return *reinterpret_cast<T*>(reinterpret_cast<B*>(base) + uint32_t(idx * uint32_t(sizeof(T))));
+}
 
 struct Trace {          // per-launch trace parameters (virtual clock + RNG)
   uint64_t seed;
@@ -117,7 +133,8 @@ struct Group {
   uint32_t d_term, d_last, d_commit, d_dl, d_rs;
   int primary, fault, meta0;
   uint32_t iso;         // EXT: replicas isolated during this tick
-  uint64_t g, key;
+  uint32_t g;           // group index on this engine (lane)
+  uint64_t key;
   int64_t tick;
   int32_t now;
   int st[NSTAT];
@@ -143,7 +160,7 @@ struct Group {
   __device__ __forceinline__ bool dropped(int a, int b) const { return ((iso >> a) | (iso >> b)) & 1u; }
 
   // ---------------------------------------------------------- load/store --
-  __device__ __forceinline__ void begin(const DevPlanes& P, const Trace& T, uint64_t g_) {
+  __device__ __forceinline__ void begin(const DevPlanes& P, const Trace& T, uint32_t g_) {
     g = g_;
     key = group_key(T.seed, P.gbase + g);
     tick = T.tick;
@@ -155,7 +172,7 @@ struct Group {
     for (int s = 0; s < NSTAT; ++s) st[s] = 0;
     cache_leader = -1;
     cache_from = 0; cache_term = 0; cache_vbase = 0;
-    const int m = P.gmeta[g];
+    const int m = at(P.gmeta, g);
     meta0 = m;
     primary = m & 0xF;
     fault = m >> 4;
@@ -164,42 +181,47 @@ struct Group {
     roles = 0; voted = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const uint64_t i = uint64_t(r) * P.Gp + g;
-      term[r] = P.term[i];
-      last[r] = P.last[i];
-      commit[r] = P.commit[i];
-      const uint32_t x = P.rs[i];
+      term[r] = at(prow(P.term, r, P.Gp), g);
+      last[r] = at(prow(P.last, r, P.Gp), g);
+      commit[r] = at(prow(P.commit, r, P.Gp), g);
+      const uint32_t x = at(prow(P.rs, r, P.Gp), g);
       roles |= (x & 3u) << (2 * r);
       voted |= ((x >> 2) & 1u) << r;
       dur[r] = int(x >> 3);
-      if (with_deadlines) dl[r] = P.deadline[i];
-      else dl[r] = 0;
+      dl[r] = with_deadlines ? at(prow(P.deadline, r, P.Gp), g) : 0;
     }
     known = with_deadlines ? (1u << R) - 1u : 0u;
   }
   __device__ __forceinline__ void store(const DevPlanes& P) const {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const uint64_t i = uint64_t(r) * P.Gp + g;
-      if ((d_term >> r) & 1u) P.term[i] = term[r];
-      if ((d_last >> r) & 1u) P.last[i] = last[r];
-      if ((d_commit >> r) & 1u) P.commit[i] = commit[r];
-      if ((d_dl >> r) & 1u) P.deadline[i] = dl[r];
+      if ((d_term >> r) & 1u) at(prow(P.term, r, P.Gp), g) = term[r];
+      if ((d_last >> r) & 1u) at(prow(P.last, r, P.Gp), g) = last[r];
+      if ((d_commit >> r) & 1u) at(prow(P.commit, r, P.Gp), g) = commit[r];
+      if ((d_dl >> r) & 1u) at(prow(P.deadline, r, P.Gp), g) = dl[r];
       if ((d_rs >> r) & 1u)
-        P.rs[i] = uint16_t(((roles >> (2 * r)) & 3u) | (((voted >> r) & 1u) << 2) | (uint32_t(dur[r]) << 3));
+        at(prow(P.rs, r, P.Gp), g) =
+            uint16_t(((roles >> (2 * r)) & 3u) | (((voted >> r) & 1u) << 2) | (uint32_t(dur[r]) << 3));
     }
     const int m = primary | (fault << 4);
-    if (m != meta0) P.gmeta[g] = uint8_t(m);
+    if (m != meta0) at(P.gmeta, g) = uint8_t(m);
   }
 
-  __device__ __forceinline__ uint64_t ring(const DevPlanes& P, int r, int idx) const {
-    return (uint64_t(r) * P.K + uint32_t((idx - 1) & int(P.kmask))) * P.Gp + g;
+  // Log ring of replica r: entry idx (1-based) at slot (idx-1) mod K.
+  __device__ __forceinline__ uint32_t ring_off(const DevPlanes& P, int idx) const {
+    return uint32_t((idx - 1) & int(P.kmask)) * uint32_t(P.Gp) + g;
+  }
+  __device__ __forceinline__ int32_t& ring_term(const DevPlanes& P, int r, int idx) const {
+    return at(P.log_term + uint64_t(r) * P.K * P.Gp, ring_off(P, idx));
+  }
+  __device__ __forceinline__ int64_t& ring_value(const DevPlanes& P, int r, int idx) const {
+    return at(P.log_value + uint64_t(r) * P.K * P.Gp, ring_off(P, idx));
   }
   // Timer of replica r (lazy: only read from HBM when a timeout check needs it).
   template <int Rp>
   __device__ __forceinline__ int deadline_of(const DevPlanes& P) {
     if (!((known >> Rp) & 1u)) {
-      dl[Rp] = P.deadline[uint64_t(Rp) * P.Gp + g];
+      dl[Rp] = at(prow(P.deadline, Rp, P.Gp), g);
       known |= 1u << Rp;
     }
     return dl[Rp];
@@ -253,21 +275,25 @@ struct Group {
       if (int64_t(l) + q.n < q.prev_idx) return res;          // 137-140
       if (q.prev_idx < 1 || q.prev_idx > l) { raise(F_PANIC_GETLOG); return res; }  // 142 -> 404
       if (q.prev_idx <= l - int(P.K)) { raise(F_RING_EVICTED); return res; }
-      if (P.log_term[ring(P, Rp, q.prev_idx)] != q.prev_term) return res;          // 142-145
+      if (ring_term(P, Rp, q.prev_idx) != q.prev_term) return res;                 // 142-145
     }
     if (int64_t(l) + q.n > I32MAX) { raise(F_OVERFLOW); return res; }
     // 148-149: append all Logs at the end (no truncation); only the last K
     // positions are kept in the ring.
     const int j0 = q.n > int(P.K) ? q.n - int(P.K) : 0;
+    int tl = 0;
     for (int j = j0; j < q.n; ++j) {
-      int t; int64_t v;
-      src.fetch(j, t, v);
-      const uint64_t o = ring(P, Rp, l + 1 + j);
-      P.log_term[o] = t;
-      P.log_value[o] = v;
+      int64_t v;
+      src.fetch(j, tl, v);
+      ring_term(P, Rp, l + 1 + j) = tl;
+      ring_value(P, Rp, l + 1 + j) = v;
     }
     const int nl = l + q.n;
-    if (q.n) { last[Rp] = nl; d_last |= 1u << Rp; }
+    if (q.n) {
+      last[Rp] = nl;
+      d_last |= 1u << Rp;
+      at(prow(P.lterm, Rp, P.Gp), g) = tl;
+    }
     if (q.lc > commit[Rp]) {                                  // 151-152: min(LC, len(Log)+1)
       const int64_t cap = int64_t(nl) + 1;
       const int nc = int64_t(q.lc) < cap ? q.lc : int(cap);
@@ -356,12 +382,16 @@ struct Group {
     if (alive() && 2 * count > R) {                           // 273
       set_role(c, ROLE_L);                                    // 274
       // 275-282: MatchIndex 0 / NextIndex 1 for every peer
-      int32_t* row;
-      if (primary == NO_PRIMARY) { primary = c; row = P.lmatch; }
-      else row = P.xmatch + uint64_t(c) * R * P.Gp;
+      if (primary == NO_PRIMARY) {
+        primary = c;
 #pragma unroll
-      for (int p = 0; p < R; ++p)
-        if (p != c) row[uint64_t(p) * P.Gp + g] = 0;
+        for (int p = 0; p < R; ++p)
+          if (p != c) at(prow(P.lmatch, p, P.Gp), g) = 0;
+      } else {
+#pragma unroll
+        for (int p = 0; p < R; ++p)
+          if (p != c) at(prow(P.xmatch, c * R + p, P.Gp), g) = 0;
+      }
       ++st[S_WON];
       return 1;
     }
@@ -384,8 +414,27 @@ struct Group {
     return cm;
   }
 
-  __device__ __forceinline__ int32_t* match_row(const DevPlanes& P, int c) const {
-    return primary == c ? P.lmatch : P.xmatch + uint64_t(c) * R * P.Gp;
+  // MatchIndex row of leader c: the primary leader's row lives in the
+  // coalesced lmatch planes, any other concurrent leader's in xmatch.
+  __device__ __forceinline__ void load_match(const DevPlanes& P, int c, int (&m)[R]) const {
+    if (primary == c) {
+#pragma unroll
+      for (int p = 0; p < R; ++p) m[p] = (p != c) ? at(prow(P.lmatch, p, P.Gp), g) : 0;
+    } else {
+#pragma unroll
+      for (int p = 0; p < R; ++p) m[p] = (p != c) ? at(prow(P.xmatch, c * R + p, P.Gp), g) : 0;
+    }
+  }
+  __device__ __forceinline__ void store_match(const DevPlanes& P, int c, const int (&m)[R], uint32_t dirty) const {
+    if (primary == c) {
+#pragma unroll
+      for (int p = 0; p < R; ++p)
+        if ((dirty >> p) & 1u) at(prow(P.lmatch, p, P.Gp), g) = m[p];
+    } else {
+#pragma unroll
+      for (int p = 0; p < R; ++p)
+        if ((dirty >> p) & 1u) at(prow(P.xmatch, c * R + p, P.Gp), g) = m[p];
+    }
   }
 
   // LeaderRun default branch (main.go:332-391) for runtime leader id c.
@@ -393,14 +442,10 @@ struct Group {
   template <typename SrcF>
   __device__ __forceinline__ void leader_round(const DevPlanes& P, const Trace& T, int c, const SrcF& make_src) {
     const int lt = sel(term, c), ll = sel(last, c);
-    int lc = sel(commit, c);
-    int32_t* row = match_row(P, c);
-    int m[R], m0[R];
-#pragma unroll
-    for (int p = 0; p < R; ++p) {
-      m[p] = (p != c) ? row[uint64_t(p) * P.Gp + g] : 0;
-      m0[p] = m[p];
-    }
+    const int lc = sel(commit, c);
+    int m[R];
+    uint32_t mdirty = 0;
+    load_match(P, c, m);
     const auto src0 = make_src(c);
     static_for<R>([&](auto PI) {                              // 334-379
       constexpr int p = decltype(PI)::value;
@@ -416,7 +461,7 @@ struct Group {
         } else {                                              // 353-360
           if (nxt < 1 || m[p] > ll) { raise(F_PANIC_GETLOG); return; }
           if (m[p] <= ll - int(P.K)) { raise(F_RING_EVICTED); return; }
-          q.prev_term = P.log_term[ring(P, c, m[p])];         // GetLog(MatchIndex).Term
+          q.prev_term = ring_term(P, c, m[p]);                // GetLog(MatchIndex).Term
           q.prev_idx = m[p]; q.n = ll - nxt + 1; from = nxt;
         }
       } else {                                                // 364-371: heartbeat
@@ -426,25 +471,28 @@ struct Group {
       src.from = from;
       const AEResp a = deliver_ae<p>(P, T, q, src);           // -> 373
       if (!alive()) return;
-      if (a.ok) { m[p] = a.match; ++st[S_AE_OK]; }            // 375-378
-      else ++st[S_AE_FAIL];
+      if (a.ok) {                                             // 375-378
+        if (a.match != m[p]) { m[p] = a.match; mdirty |= 1u << p; }
+        ++st[S_AE_OK];
+      } else {
+        ++st[S_AE_FAIL];
+      }
     });
     if (alive()) {
       const int nc = commit_rule(m, c, lc);
       if (nc != lc) { put(commit, c, nc); d_commit |= 1u << c; }
     }
-#pragma unroll
-    for (int p = 0; p < R; ++p)
-      if (p != c && m[p] != m0[p]) row[uint64_t(p) * P.Gp + g] = m[p];
+    store_match(P, c, m, mdirty);
   }
 
   // Client append to leader c (main.go:327-329): Log += {Term, Value}; LastApplied++.
   __device__ __forceinline__ void client_append_value(const DevPlanes& P, int c, int64_t v) {
     const int l = sel(last, c);
     if (l >= I32MAX) { raise(F_OVERFLOW); return; }
-    const uint64_t o = ring(P, c, l + 1);
-    P.log_term[o] = sel(term, c);
-    P.log_value[o] = v;
+    const int t = sel(term, c);
+    ring_term(P, c, l + 1) = t;
+    ring_value(P, c, l + 1) = v;
+    at(P.lterm + uint64_t(c) * P.Gp, g) = t;
     put(last, c, l + 1);
     d_last |= 1u << c;
   }
@@ -467,8 +515,8 @@ struct Group {
 struct TickSrc {
   const int32_t* lt;
   const int64_t* lv;
-  uint64_t Gp, g;
-  uint32_t K, kmask;
+  uint64_t Gp;
+  uint32_t g, K, kmask;
   int leader, from;
   int cache_leader, cache_from, cache_term;
   uint64_t cache_vbase;
@@ -478,9 +526,10 @@ struct TickSrc {
       t = cache_term;
       v = int64_t(sm64(cache_vbase ^ uint64_t(uint32_t(idx - cache_from))) >> 1);
     } else {
-      const uint64_t o = (uint64_t(leader) * K + uint32_t((idx - 1) & int(kmask))) * Gp + g;
-      t = lt[o];
-      v = lv[o];
+      const uint64_t rb = uint64_t(leader) * K * Gp;
+      const uint32_t o = uint32_t((idx - 1) & int(kmask)) * uint32_t(Gp) + g;
+      t = at(lt + rb, o);
+      v = at(lv + rb, o);
     }
   }
 };

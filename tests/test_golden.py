@@ -1,0 +1,46 @@
+"""CPU: the oracle reproduces the committed golden traces and the trace RNG
+matches an independent Python restatement of its definition."""
+import json
+import os
+
+import pytest
+
+import golden_check
+
+M64 = (1 << 64) - 1
+
+
+def sm64(x):
+    x = (x + 0x9E3779B97F4A7C15) & M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M64
+    return x ^ (x >> 31)
+
+
+def rng(seed, gid, r, stream, tick):
+    k = sm64(seed ^ sm64(gid))
+    return sm64(sm64(k ^ ((stream << 32) | r)) ^ tick)
+
+
+def test_rng_vectors(oracle_mod):
+    vec = json.load(open(os.path.join(golden_check.HERE, "rng_vectors.json")))
+    o = oracle_mod.Oracle(seed=0)
+    for v in vec:
+        assert rng(v["seed"], v["gid"], v["replica"], v["stream"], v["tick"]) == v["rng"]
+        # client value e=3 of (gid, replica, tick): sm64(rng(.., stream 1 = value, ..) ^ e) >> 1
+        assert sm64(rng(v["seed"], v["gid"], v["replica"], 1, v["tick"]) ^ 3) >> 1 == v["value_e3"]
+        o.cfg.seed = v["seed"]
+        assert o.rng(v["gid"], v["replica"], v["stream"], v["tick"]) == v["rng"]
+
+
+def test_timer_draw_ranges(oracle_mod):
+    """rand.Intn(20)+10 (main.go:114) and rand.Intn(4)+10 (main.go:194)."""
+    o = oracle_mod.Oracle(seed=7)
+    f = {o.timer_draw(g, r, 0, t) for g in range(50) for r in range(3) for t in range(10)}
+    c = {o.timer_draw(g, r, 1, t) for g in range(50) for r in range(3) for t in range(10)}
+    assert f == set(range(10, 30)) and c == set(range(10, 14))
+
+
+@pytest.mark.parametrize("name", golden_check.NAMES)
+def test_oracle_matches_golden(name, oracle_mod):
+    golden_check.check(lambda kw: oracle_mod.Oracle(**kw), name)

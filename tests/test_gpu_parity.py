@@ -10,9 +10,23 @@ from raftstep import Engine, abi
 pytestmark = pytest.mark.gpu
 
 
-def pair(**kw):
+def pair(general=False, **kw):
+    """(engine, oracle) on the same config. general=True routes every group
+    through the general tick kernel (debug knob RAFTSTEP_FORCE_GENERAL), so
+    both device paths are checked against the oracle on the same traces."""
+    import os
+
     import oracle
-    return Engine(**kw), oracle.Oracle(**kw)
+    old = os.environ.get("RAFTSTEP_FORCE_GENERAL")
+    os.environ["RAFTSTEP_FORCE_GENERAL"] = "1" if general else "0"
+    try:
+        e = Engine(**kw)
+    finally:
+        if old is None:
+            del os.environ["RAFTSTEP_FORCE_GENERAL"]
+        else:
+            os.environ["RAFTSTEP_FORCE_GENERAL"] = old
+    return e, oracle.Oracle(**kw)
 
 
 def compare(e, o, what):
@@ -67,6 +81,10 @@ TRACES = {
                            isolate_per_65536=20000, isolate_min_ticks=4, isolate_max_ticks=20), "steady0", 1, 200, 5),
     "wrap_e_gt_k": (dict(replicas=3, groups=130, client_period=3, entries_per_tick=40, ring_depth=16,
                          seed=0x77), "steady0", 1, 40, 1),
+    "steady_e7_k8": (dict(replicas=5, groups=700, client_period=1, entries_per_tick=7, ring_depth=8,
+                          seed=0x78), "steady-1", 1, 30, 3),
+    "steady_heartbeats": (dict(replicas=3, groups=260, client_period=4, entries_per_tick=2, ring_depth=8,
+                               seed=0x79), "steady0", 1, 40, 1),
     "r1": (dict(replicas=1, groups=64, client_period=1, seed=1), "new", 0, 60, 5),
     "r2": (dict(replicas=2, groups=64, client_period=1, seed=2), "new", 0, 60, 5),
     "r4": (dict(replicas=4, groups=300, client_period=1, seed=4), "new", 0, 120, 5),
@@ -75,10 +93,11 @@ TRACES = {
 }
 
 
+@pytest.mark.parametrize("path", ["auto", "general"])
 @pytest.mark.parametrize("name", sorted(TRACES))
-def test_tick_trace(name):
+def test_tick_trace(name, path):
     kw, init, t0, n, every = TRACES[name]
-    e, o = pair(**kw)
+    e, o = pair(general=(path == "general"), **kw)
     for x in (e, o):
         if init == "new":
             x.init_new_nodes(t0)
@@ -112,3 +131,31 @@ def test_tick_from_random_states():
             se, so = e.tick(t, 1), o.tick(t, 1)
             assert list(se) == list(so), (R, t)
             compare(e, o, f"R={R} tick {t}")
+
+
+def test_full_size_steady_state_properties():
+    """BASELINE config C2 at full size (2^20 groups, R=5, E=1): size-independent
+    properties of the steady state after N ticks (every log has N entries,
+    leader commit N, followers N-1, per-tick stats in closed form), plus a
+    bit-exact oracle diff of a slice of groups run through an oracle that
+    owns just that slice (group_base)."""
+    import oracle
+    G, R, N = 1 << 20, 5, 24
+    kw = dict(replicas=R, groups=G, ring_depth=32, client_period=1, entries_per_tick=1, seed=0x5EED0002)
+    e = Engine(**kw)
+    e.init_steady(0, 0)
+    stats = e.tick(1, N)
+    assert list(stats) == [G * N, 0, 0, 4 * G * N, 0, 0, 0, G * N]
+    st = e.store_state(logs=False)
+    assert (st["last"] == N).all() and (st["fault"] == 0).all()
+    assert (st["commit"][:, 0] == N).all() and (st["commit"][:, 1:] == N - 1).all()
+    assert (st["deadline"][:, 1:] == 2 * N + st["timeout"][:, 1:]).all()
+    full = e.store_state(logs=True)
+    for g0 in (0, G // 2 + 123, G - 700):
+        kw2 = dict(kw, groups=700, group_base=g0)
+        o = oracle.Oracle(**kw2)
+        o.init_steady(0, 0)
+        o.tick(1, N)
+        ref = o.store_state()
+        sl = {k: v[g0:g0 + 700] for k, v in full.items()}
+        H.assert_same_state(sl, ref, f"slice at {g0}")
