@@ -65,9 +65,11 @@ struct raft_engine {
   unsigned long long* hist = nullptr;
   uint32_t hist_cap = 0;
   // worklist of groups the steady-state kernel hands to the general kernel
-  uint32_t* work = nullptr;
-  uint32_t* wcount = nullptr;   // [2], indexed by tick parity
+  uint32_t* work = nullptr;     // deferred group ids
+  int32_t* work_tick = nullptr; // tick each one was deferred at
+  uint32_t* wcount = nullptr;   // [2], indexed by window parity
   int force_general = 0;        // debug: route every group through the general kernel
+  uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
   // handler-batch staging
   void* stage = nullptr;
   size_t stage_cap = 0;
@@ -104,6 +106,9 @@ Trace make_trace(const raft_engine* e, int64_t tick) {
   T.iso_p = e->cfg.isolate_per_65536;
   T.iso_min = e->cfg.isolate_min_ticks;
   T.iso_span = e->cfg.isolate_max_ticks - e->cfg.isolate_min_ticks + 1;
+  T.secs = e->cfg.tick_seconds;
+  T.period = e->cfg.client_period;
+  T.entries = e->cfg.entries_per_tick;
   return T;
 }
 
@@ -274,13 +279,15 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.term), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.last), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.commit), R * Gp * 4);
-  A(reinterpret_cast<void**>(&e->P.deadline), R * Gp * 4);
+  A(reinterpret_cast<void**>(&e->P.tstart), R * Gp * 4);
+  A(reinterpret_cast<void**>(&e->P.hb), Gp * 4);
   A(reinterpret_cast<void**>(&e->P.rs), R * Gp * 2);
   A(reinterpret_cast<void**>(&e->P.lmatch), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.xmatch), R * R * Gp * 4);
-  A(reinterpret_cast<void**>(&e->P.gmeta), Gp);
+  A(reinterpret_cast<void**>(&e->P.gmeta), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.lterm), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->work), Gp * 4);
+  A(reinterpret_cast<void**>(&e->work_tick), Gp * 4);
   A(reinterpret_cast<void**>(&e->wcount), 256);
   A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.log_value), R * K * Gp * 8);
@@ -300,17 +307,20 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->P.K = c.ring_depth;
   e->P.kmask = c.ring_depth - 1;
   if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
+  if (const char* se = getenv("RAFTSTEP_SLOW_EVERY")) e->slow_every = std::max(1, atoi(se));
   // zero everything once so that padding / unused rows are deterministic
   for (void* p : e->allocs) (void)p;
   hipError_t z = hipSuccess;
   z = z == hipSuccess ? hipMemsetAsync(e->P.term, 0, R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.last, 0, R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.commit, 0, R * Gp * 4, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.deadline, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.tstart, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.hb, 0x80, Gp * 4, e->stream) : z;  // 0x80808080 < any time
   z = z == hipSuccess ? hipMemsetAsync(e->P.rs, 0, R * Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.lmatch, 0, R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.xmatch, 0, R * R * Gp * 4, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.gmeta, NO_PRIMARY, Gp, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(e->P.gmeta), uint16_t(NO_PRIMARY), Gp,
+                                           e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.lterm, 0, R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, 256, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
@@ -369,15 +379,15 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!e || !v) return fail(RAFT_EINVAL, "null argument");
   HIPCHK(hipSetDevice(e->cfg.device));
   const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
-  std::vector<int32_t> term, last, commit, dl, lm, xm, lt;
-  std::vector<uint16_t> rs;
-  std::vector<uint8_t> meta;
+  std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt;
+  std::vector<uint16_t> rs, meta;
   std::vector<int64_t> lv;
   int rc = RAFT_OK;
   if (!rc) rc = d2h(e, term, e->P.term, R * Gp);
   if (!rc) rc = d2h(e, last, e->P.last, R * Gp);
   if (!rc) rc = d2h(e, commit, e->P.commit, R * Gp);
-  if (!rc) rc = d2h(e, dl, e->P.deadline, R * Gp);
+  if (!rc) rc = d2h(e, ts, e->P.tstart, R * Gp);
+  if (!rc) rc = d2h(e, hb, e->P.hb, Gp);
   if (!rc) rc = d2h(e, rs, e->P.rs, R * Gp);
   if (!rc) rc = d2h(e, lm, e->P.lmatch, R * Gp);
   if (!rc) rc = d2h(e, xm, e->P.xmatch, R * R * Gp);
@@ -391,7 +401,8 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   HIPCHK(hipStreamSynchronize(e->stream));
   for (uint64_t g = 0; g < G; ++g) {
     const int primary = meta[g] & 0xF;
-    if (v->fault) v->fault[g] = uint8_t(meta[g] >> 4);
+    const bool msync = meta[g] & M_MSYNC;
+    if (v->fault) v->fault[g] = uint8_t((meta[g] >> 4) & 0xF);
     for (uint64_t r = 0; r < R; ++r) {
       const uint64_t d = r * Gp + g, c = g * R + r;
       const int role = rs[d] & 3;
@@ -400,13 +411,14 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
       if (v->term) v->term[c] = term[d];
       if (v->last) v->last[c] = last[d];
       if (v->commit) v->commit[c] = commit[d];
-      if (v->deadline) v->deadline[c] = dl[d];
+      // deadline = effective timer start + d; followers/candidates also count hb
+      if (v->deadline) v->deadline[c] = (role == ROLE_L ? ts[d] : std::max(ts[d], hb[g])) + int32_t(rs[d] >> 3);
       if (v->timeout) v->timeout[c] = int32_t(rs[d] >> 3);
       if (v->match)
         for (uint64_t p = 0; p < R; ++p) {
           int32_t m = 0;
           if (role == ROLE_L && p != r)
-            m = (int(r) == primary) ? lm[p * Gp + g] : xm[(r * R + p) * Gp + g];
+            m = (int(r) == primary) ? (msync ? last[p * Gp + g] : lm[p * Gp + g]) : xm[(r * R + p) * Gp + g];
           v->match[c * R + p] = m;
         }
       if (logs && last[d] > 0) {
@@ -438,10 +450,10 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
     return fail(RAFT_EINVAL, "raft_load_state needs every field of the view");
   HIPCHK(hipSetDevice(e->cfg.device));
   const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
-  std::vector<int32_t> term(R * Gp, 0), last(R * Gp, 0), commit(R * Gp, 0), dl(R * Gp, 0), lm(R * Gp, 0),
-      xm(R * R * Gp, 0), lt(R * K * Gp, 0);
+  std::vector<int32_t> term(R * Gp, 0), last(R * Gp, 0), commit(R * Gp, 0), ts(R * Gp, 0), lm(R * Gp, 0),
+      xm(R * R * Gp, 0), lt(R * K * Gp, 0), hb(Gp, HB_NONE);
   std::vector<uint16_t> rs(R * Gp, 0);
-  std::vector<uint8_t> meta(Gp, uint8_t(NO_PRIMARY));
+  std::vector<uint16_t> meta(Gp, uint16_t(NO_PRIMARY));
   std::vector<int64_t> lv(R * K * Gp, 0);
   std::vector<int32_t> ltm(R * Gp, 0);
   for (uint64_t g = 0; g < G; ++g) {
@@ -454,13 +466,16 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
                     (unsigned long long)r);
       if (v->role[c] == RAFT_LEADER && primary == NO_PRIMARY) primary = int(r);
     }
-    meta[g] = uint8_t(primary | (v->fault[g] << 4));
+    bool steady = primary != NO_PRIMARY;
+    for (uint64_t r = 0; r < R; ++r)
+      if (int(r) != primary && v->role[g * R + r] != RAFT_FOLLOWER) steady = false;
+    meta[g] = uint16_t(primary | (v->fault[g] << 4) | (steady ? M_STEADY : 0));
     for (uint64_t r = 0; r < R; ++r) {
       const uint64_t d = r * Gp + g, c = g * R + r;
       term[d] = v->term[c];
       last[d] = v->last[c];
       commit[d] = v->commit[c];
-      dl[d] = v->deadline[c];
+      ts[d] = v->deadline[c] - v->timeout[c];
       rs[d] = uint16_t(v->role[c] | (v->voted[c] << 2) | (uint32_t(v->timeout[c]) << 3));
       if (v->role[c] == RAFT_LEADER)
         for (uint64_t p = 0; p < R; ++p) {
@@ -479,7 +494,8 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.term, term);
   if (!rc) rc = h2d(e, e->P.last, last);
   if (!rc) rc = h2d(e, e->P.commit, commit);
-  if (!rc) rc = h2d(e, e->P.deadline, dl);
+  if (!rc) rc = h2d(e, e->P.tstart, ts);
+  if (!rc) rc = h2d(e, e->P.hb, hb);
   if (!rc) rc = h2d(e, e->P.rs, rs);
   if (!rc) rc = h2d(e, e->P.lmatch, lm);
   if (!rc) rc = h2d(e, e->P.xmatch, xm);
@@ -500,24 +516,26 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     HIPCHK(hipMemsetAsync(e->hist, 0, size_t(nticks) * STAT_SLOTS * NSTAT * 8, e->stream));
   }
   HIPCHK(hipMemsetAsync(e->wcount, 0, 2 * sizeof(uint32_t), e->stream));
+  const Trace T0 = make_trace(e, first_tick);
+  uint32_t window = 0;
   for (uint32_t i = 0; i < nticks; ++i) {
     const int64_t t = first_tick + int64_t(i);
     const Trace T = make_trace(e, t);
-    const uint32_t period = e->cfg.client_period;
-    const uint32_t E = (period && (t % int64_t(period)) == 0) ? e->cfg.entries_per_tick : 0;
     unsigned long long* st = stats ? e->hist + size_t(i) * STAT_SLOTS * NSTAT : nullptr;
-    uint32_t* cnt = e->wcount + (t & 1);
-    uint32_t* next = e->wcount + ((t + 1) & 1);
+    uint32_t* cnt = e->wcount + (window & 1);
     hipEvent_t a = nullptr, b = nullptr;
     if (e->prof) {
       a = next_event(e);
       b = next_event(e);
       if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
-      HIPCHK(hipEventRecord(a, e->stream));
     }
-    HIPCHK(launch_tick_fast(e->R, e->P, T, E, st, e->work, cnt, e->force_general, e->stream));
-    if (e->prof) HIPCHK(hipEventRecord(b, e->stream));
-    HIPCHK(launch_tick_slow(e->R, e->P, T, E, st, e->work, cnt, next, e->stream));
+    HIPCHK(launch_tick_fast(e->R, e->P, T, st, e->work, e->work_tick, cnt, e->force_general, e->stream, a, b));
+    // deferred groups catch up every slow_every ticks and at the end of the call
+    if ((i + 1) % e->slow_every == 0 || i + 1 == nticks) {
+      HIPCHK(launch_tick_slow(e->R, e->P, T0, first_tick, t, stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
+                              e->wcount + ((window + 1) & 1), e->stream));
+      ++window;
+    }
   }
   if (stats && e->comm)
     RCCLCHK(ncclAllReduce(e->hist, e->hist, size_t(nticks) * STAT_SLOTS * NSTAT, ncclUint64, ncclSum, e->comm,

@@ -28,12 +28,15 @@ struct DevRes {
   int64_t value;      // AE: MatchIndex; VR: granted; ops: see raft_op_result
 };
 
-// Steady-state fast kernel; groups it does not take go to `work`.
-hipError_t launch_tick_fast(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
-                            uint32_t* work, uint32_t* work_count, int force_slow, hipStream_t s);
-// General kernel over the worklist; zeroes `next_count` for the next tick.
-hipError_t launch_tick_slow(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
-                            const uint32_t* work, const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
+// Steady-state fast kernel; groups it does not take are DEFERred to `work`.
+// ev_start/ev_stop (may be null) time the dispatch itself (hipExtLaunchKernel).
+hipError_t launch_tick_fast(int R, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                            int32_t* work_tick, uint32_t* work_count, int force_slow, hipStream_t s,
+                            hipEvent_t ev_start, hipEvent_t ev_stop);
+// General kernel: catches every worklisted group up to last_tick; zeroes `next_count`.
+hipError_t launch_tick_slow(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
+                            unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
+                            const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
 hipError_t launch_ops(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
                       const int32_t* et, const int64_t* ev, DevRes* out, hipStream_t s);
 hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_t s);

@@ -9,6 +9,8 @@
 //  init_*_kernel<R>: NewNode state / post-election state.
 #include "kernels.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 
 namespace raftstep {
@@ -141,57 +143,68 @@ __device__ __forceinline__ void block_stats(const int (&v)[N], const int (&idx)[
 }
 
 // ---------------------------------------------------------------------------
-// Steady-state tick (the metric path). A group qualifies when it is not
-// frozen, its only leader is its primary, every other replica is a
-// follower, no EXT isolation touches it this tick, and every peer's
+// Steady-state tick (the metric path). A group qualifies when it is STEADY
+// (not frozen, its only leader is its primary, every other replica a
+// follower), no EXT isolation touches it this tick, and every peer's
 // MatchIndex equals the leader's LastApplied (NextIndex = LastApplied+1).
 // For such a group the tick is exactly: client append (main.go:327-329),
 // one AppendEntries per follower carrying just this tick's entries
 // (main.go:341-372 -> 121-156), the responses (main.go:375-378) and the
-// commit rule (main.go:381-391); no timer can expire (every follower's timer
-// is reset by the AppendEntries, main.go:124-127). Anything else — or any
-// condition on the way that would fault, or need a ring read — sends the
-// group to the general kernel via the worklist before a single store.
+// commit rule (main.go:381-391). Every follower's timer is reset by its
+// AppendEntries (main.go:124-127) — recorded once per group as hb = now —
+// so no timer can expire. Anything else, or any condition on the way that
+// would fault or need a ring read, defers the group to the general kernel
+// (worklist + DEFER flag) before a single store; a DEFERred group is left
+// alone until the general kernel has caught it up.
+// MSYNC: after a fast tick every follower's MatchIndex equals its
+// LastApplied (main.go:156 -> 376), so the row is kept implicit.
 template <int R>
-__global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, uint32_t E, unsigned long long* stats,
-                                                        uint32_t* work, uint32_t* work_count, int force_slow) {
+__global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, unsigned long long* stats,
+                                                        uint32_t* work, int32_t* work_tick, uint32_t* work_count,
+                                                        int force_slow) {
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
   int sv[4] = {0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups
   bool bail = false;
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
     const int c = meta & 0xF;
-    bail = force_slow || (meta >> 4) != 0 || c >= R;
-    int term[R], last[R], commit[R], lt[R], dur[R], m[R];
-    if (!bail) {
+    const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
+    bail = !skip && (force_slow || !(meta & M_STEADY));
+    int term[R], last[R], commit[R], lt[R], m[R];
+    const bool go = !skip && !bail;
+    if (go) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const uint32_t x = at(prow(P.rs, r, P.Gp), g);
-        const int want = (r == c) ? ROLE_L : ROLE_F;
-        bail |= int(x & 3u) != want;
-        dur[r] = int(x >> 3);
         term[r] = at(prow(P.term, r, P.Gp), g);
         last[r] = at(prow(P.last, r, P.Gp), g);
         commit[r] = at(prow(P.commit, r, P.Gp), g);
         lt[r] = at(prow(P.lterm, r, P.Gp), g);
-        m[r] = (r != c) ? at(prow(P.lmatch, r, P.Gp), g) : 0;
+      }
+      if (meta & M_MSYNC) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) m[r] = (r != c) ? last[r] : 0;
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) m[r] = (r != c) ? at(prow(P.lmatch, r, P.Gp), g) : 0;
       }
     }
+    const int n = int(T.client_entries());
     uint64_t key = 0;
-    if (!bail && (T.iso_p || E)) key = group_key(T.seed, P.gbase + g);
-    if (!bail && T.iso_p) bail = isolation_mask<R>(key, T) != 0;
+    if (go && (T.iso_p || n)) key = group_key(T.seed, P.gbase + g);
+    if (go && T.iso_p) bail = isolation_mask<R>(key, T) != 0;
     // leader view
     const int Lt = sel(term, c), Ll = sel(last, c), Lc = sel(commit, c), Llt = sel(lt, c);
-    const int n = int(E);
-    if (!bail) bail = int64_t(Ll) + n > I32MAX || n >= int(P.K);
+    if (go && !bail) bail = int64_t(Ll) + n > I32MAX || n >= int(P.K);
+    if (go) {
 #pragma unroll
-    for (int p = 0; p < R; ++p) bail |= (p != c) && m[p] != Ll;
+      for (int p = 0; p < R; ++p) bail |= (p != c) && m[p] != Ll;
+    }
     // one AppendEntries shape for every peer (NextIndex == Ll+1)
     int prev_idx, prev_term;
     if (n == 0 || Ll == 0) { prev_idx = Ll; prev_term = Lt; }   // heartbeat / whole-log (PrevLogIndex 0)
     else { prev_idx = Ll; prev_term = Llt; }                      // GetLog(MatchIndex).Term
     uint32_t okm = 0, cch = 0, mch = 0, ltch = 0;
-    if (!bail) {
+    if (go && !bail) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == c) continue;
@@ -216,46 +229,47 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, ui
         }
       }
     }
-    if (!bail) {
+    if (go && !bail) {
       // commit rule (main.go:381-391)
       int cm = Lc;
+      bool sync = true;
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         int cnt = 0;
 #pragma unroll
         for (int q = 0; q < R; ++q) cnt += (q != c && m[q] == m[p]) ? 1 : 0;
         if (p != c && 2 * cnt > R && m[p] > cm) cm = m[p];
+        sync &= (p == c) || m[p] == last[p];
       }
       sv[0] = cm - Lc;
       sv[1] = __builtin_popcount(okm);
       sv[2] = (R - 1) - sv[1];
       sv[3] = 1;
       // ---- stores (no bail past this point) ----
-      const int newL = Ll + n;
       if (n) {
-        at(P.last + uint64_t(c) * P.Gp, g) = newL;
+        at(P.last + uint64_t(c) * P.Gp, g) = Ll + n;
         if (Llt != Lt) at(P.lterm + uint64_t(c) * P.Gp, g) = Lt;
       }
       if (cm != Lc) at(P.commit + uint64_t(c) * P.Gp, g) = cm;
+      at(P.hb, g) = T.now;                                        // timer.Reset(d) of every follower
 #pragma unroll
       for (int p = 0; p < R; ++p) {
-        if (p == c) continue;
-        at(prow(P.deadline, p, P.Gp), g) = T.now + dur[p];        // timer.Reset(d), main.go:124-127
-        if ((okm >> p) & 1u) {
-          if (n) at(prow(P.last, p, P.Gp), g) = last[p];
-          if ((mch >> p) & 1u) at(prow(P.lmatch, p, P.Gp), g) = m[p];
-          if ((cch >> p) & 1u) at(prow(P.commit, p, P.Gp), g) = commit[p];
-          if ((ltch >> p) & 1u) at(prow(P.lterm, p, P.Gp), g) = Lt;
-          if (term[p] != Lt) at(prow(P.term, p, P.Gp), g) = Lt;  // main.go:155
-        }
+        if (p == c || !((okm >> p) & 1u)) continue;
+        if (n) at(prow(P.last, p, P.Gp), g) = last[p];
+        if (!sync && ((mch >> p) & 1u)) at(prow(P.lmatch, p, P.Gp), g) = m[p];
+        if ((cch >> p) & 1u) at(prow(P.commit, p, P.Gp), g) = commit[p];
+        if ((ltch >> p) & 1u) at(prow(P.lterm, p, P.Gp), g) = Lt;
+        if (term[p] != Lt) at(prow(P.term, p, P.Gp), g) = Lt;    // main.go:155
       }
+      const int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
+      if (nm != meta) at(P.gmeta, g) = uint16_t(nm);
       // this tick's entries: leader log + every follower that accepted
       if (n) {
         const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+        const uint64_t cb = uint64_t(c) * P.K * P.Gp;
         for (int e = 0; e < n; ++e) {
           const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
           const uint32_t o = uint32_t((Ll + e) & int(P.kmask)) * uint32_t(P.Gp) + g;
-          const uint64_t cb = uint64_t(c) * P.K * P.Gp;
           at(P.log_term + cb, o) = Lt;
           at(P.log_value + cb, o) = v;
 #pragma unroll
@@ -269,6 +283,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, ui
         }
       }
     }
+    if (bail) at(P.gmeta, g) = uint16_t(meta | M_DEFER);
   }
   // groups that need the general path go to the worklist (one atomic per wave)
   const uint64_t bm = __ballot(bail);
@@ -277,7 +292,11 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, ui
     uint32_t base = 0;
     if (lane == __builtin_ctzll(bm)) base = atomicAdd(work_count, uint32_t(__popcll(bm)));
     base = __shfl(base, __builtin_ctzll(bm));
-    if (bail) work[base + uint32_t(__popcll(bm & ((1ull << lane) - 1ull)))] = g;
+    if (bail) {
+      const uint32_t slot = base + uint32_t(__popcll(bm & ((1ull << lane) - 1ull)));
+      work[slot] = g;
+      work_tick[slot] = int32_t(T.tick);
+    }
   }
   if (stats) {
     const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
@@ -285,30 +304,37 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, ui
   }
 }
 
-// General tick for the groups on the worklist: the full REF semantics of
-// run_tick() (elections, candidates, step-downs, faults, EXT drops).
+// General tick over the worklist: every deferred group is caught up, tick
+// by tick in order, from the tick it was deferred at to `last_tick`, with
+// the full REF semantics of run_tick() (elections, candidates, step-downs,
+// faults, EXT drops); stats go to each tick's own record.
 template <int R>
-__global__ __launch_bounds__(256) void tick_slow_kernel(DevPlanes P, Trace T, uint32_t E, unsigned long long* stats,
-                                                        const uint32_t* work, const uint32_t* work_count,
+__global__ __launch_bounds__(256) void tick_slow_kernel(DevPlanes P, Trace T0, int64_t first_tick, int64_t last_tick,
+                                                        unsigned long long* stats, const uint32_t* work,
+                                                        const int32_t* work_tick, const uint32_t* work_count,
                                                         uint32_t* next_count) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *next_count = 0;
   const uint32_t n = *work_count;
-  int st[NSTAT];
-#pragma unroll
-  for (int s = 0; s < NSTAT; ++s) st[s] = 0;
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-    Group<R> G;
-    G.begin(P, T, work[i]);
-    if (G.fault) continue;
-    G.load(P, false);
-    run_tick<R>(G, P, T, E);
-    G.store(P);
+    const uint32_t g = work[i];
+    for (int64_t t = work_tick[i]; t <= last_tick; ++t) {
+      const Trace T = T0.at_tick(t);
+      Group<R> G;
+      G.begin(P, T, g);
+      if (G.fault) {            // frozen earlier in this catch-up
+        if (G.meta0 & M_DEFER) at(P.gmeta, g) = uint16_t(G.meta0 & ~M_DEFER);
+        break;
+      }
+      G.load(P, false);
+      run_tick<R>(G, P, T, T.client_entries());
+      G.store(P);
+      if (stats) {
+        unsigned long long* rec = stats + size_t(t - first_tick) * STAT_SLOTS * NSTAT + (g % STAT_SLOTS) * NSTAT;
 #pragma unroll
-    for (int s = 0; s < NSTAT; ++s) st[s] += G.st[s];
-  }
-  if (stats && n) {
-    const int idx[NSTAT] = {0, 1, 2, 3, 4, 5, 6, 7};
-    block_stats<NSTAT>(st, idx, stats);
+        for (int s = 0; s < NSTAT; ++s)
+          if (G.st[s]) atomicAdd(&rec[s], (unsigned long long)G.st[s]);
+      }
+    }
   }
 }
 
@@ -411,11 +437,12 @@ __global__ __launch_bounds__(256) void init_new_kernel(DevPlanes P, Trace T) {
     const uint64_t i = uint64_t(r) * P.Gp + g;
     const int d = T.f_min + int(uint32_t(rng_k(key, r, ST_TIMER_F, uint64_t(T.tick)) >> 32) % uint32_t(T.f_span));
     P.term[i] = 0; P.last[i] = 0; P.commit[i] = 0;
-    P.deadline[i] = T.now + d;
+    P.tstart[i] = T.now;
     P.rs[i] = uint16_t(ROLE_F | (uint32_t(d) << 3));
     P.lterm[i] = 0;
   }
-  P.gmeta[g] = uint8_t(NO_PRIMARY);
+  P.hb[g] = HB_NONE;
+  P.gmeta[g] = uint16_t(NO_PRIMARY);
 }
 
 // Post-election state (KAT-1 generalised).
@@ -434,12 +461,13 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
     const int d = isL ? T.c_min + int(uint32_t(h >> 32) % uint32_t(T.c_span))
                       : T.f_min + int(uint32_t(h >> 32) % uint32_t(T.f_span));
     P.term[i] = 1; P.last[i] = 0; P.commit[i] = 0;
-    P.deadline[i] = T.now + d;
+    P.tstart[i] = T.now;
     P.rs[i] = uint16_t((isL ? ROLE_L : ROLE_F) | (1u << 2) | (uint32_t(d) << 3));
     P.lmatch[i] = 0;
     P.lterm[i] = 0;
   }
-  P.gmeta[g] = uint8_t(L);
+  P.hb[g] = HB_NONE;
+  P.gmeta[g] = uint16_t(L | M_MSYNC | M_STEADY);
 }
 
 // ------------------------------------------------------ host launchers ---
@@ -458,17 +486,19 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
 
 static inline dim3 grid_for(uint64_t n) { return dim3(unsigned((n + 255) / 256)); }
 
-hipError_t launch_tick_fast(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
-                            uint32_t* work, uint32_t* work_count, int force_slow, hipStream_t s) {
-  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(tick_fast_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P, T, E, stats, work,
-                                        work_count, force_slow));
+hipError_t launch_tick_fast(int R, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                            int32_t* work_tick, uint32_t* work_count, int force_slow, hipStream_t s,
+                            hipEvent_t ev_start, hipEvent_t ev_stop) {
+  RAFT_DISPATCH_R(R, hipExtLaunchKernelGGL(tick_fast_kernel<RR>, grid_for(P.G), dim3(256), 0, s, ev_start, ev_stop, 0,
+                                           P, T, stats, work, work_tick, work_count, force_slow));
   return hipGetLastError();
 }
-hipError_t launch_tick_slow(int R, const DevPlanes& P, const Trace& T, uint32_t E, unsigned long long* stats,
-                            const uint32_t* work, const uint32_t* work_count, uint32_t* next_count, hipStream_t s) {
+hipError_t launch_tick_slow(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
+                            unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
+                            const uint32_t* work_count, uint32_t* next_count, hipStream_t s) {
   const unsigned blocks = unsigned(std::min<uint64_t>((P.G + 255) / 256, 1024));
-  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(tick_slow_kernel<RR>, dim3(blocks), dim3(256), 0, s, P, T, E, stats, work,
-                                        work_count, next_count));
+  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(tick_slow_kernel<RR>, dim3(blocks), dim3(256), 0, s, P, T0, first_tick,
+                                        last_tick, stats, work, work_tick, work_count, next_count));
   return hipGetLastError();
 }
 hipError_t launch_ops(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,

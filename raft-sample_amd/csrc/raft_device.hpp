@@ -32,6 +32,11 @@ enum : int {
   S_FAULTS = 6, S_LEADER_GROUPS = 7, NSTAT = 8
 };
 constexpr int NO_PRIMARY = 0xF;
+// gmeta flag bits (above primary:4 | fault:4)
+constexpr int M_DEFER = 1 << 8;   // on the worklist with ticks pending; the fast kernel leaves it alone
+constexpr int M_MSYNC = 1 << 9;   // primary's MatchIndex[p] == LastApplied[p] for every peer; lmatch is stale
+constexpr int M_STEADY = 1 << 10; // exactly one leader (the primary), every other replica a follower
+constexpr int HB_NONE = -2147483647 - 1;
 constexpr int I32MAX = 2147483647;
 constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to cut atomic contention
 
@@ -42,11 +47,12 @@ struct DevPlanes {
   int32_t* term;       // Node.Term                 (main.go:19)
   int32_t* last;       // Node.LastApplied=len(Log) (main.go:25)
   int32_t* commit;     // Node.CommitIndex          (main.go:24)
-  int32_t* deadline;   // election timer deadline, virtual seconds
+  int32_t* tstart;     // election timer start (virtual s); deadline = start + d
+  int32_t* hb;         // [Gp] time of the last steady-state heartbeat that reset every follower
   uint16_t* rs;        // role:2 | voted:1 | timer duration d:13 (main.go:16, 20, 114, 194)
   int32_t* lmatch;     // [R][Gp] MatchIndex row of the group's primary leader (main.go:29)
   int32_t* xmatch;     // [R][R][Gp] rows of any further concurrent leaders (EXT only)
-  uint8_t* gmeta;      // primary leader id:4 | fault:4
+  uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
   int32_t* lterm;      // [R][Gp] Log[len-1].Term: cached term of each replica's last entry
   int32_t* log_term;   // Log.Term  ring
   int64_t* log_value;  // Log.Value ring
@@ -78,6 +84,17 @@ struct Trace {          // per-launch trace parameters (virtual clock + RNG)
   int32_t now;          // tick * tick_seconds
   int32_t f_min, f_span, c_min, c_span;
   uint32_t iso_p, iso_min, iso_span;
+  int32_t secs;         // tick_seconds
+  uint32_t period, entries;  // client event every `period` ticks, `entries` each
+  __device__ __forceinline__ Trace at_tick(int64_t t) const {
+    Trace x = *this;
+    x.tick = t;
+    x.now = int32_t(t * secs);
+    return x;
+  }
+  __device__ __forceinline__ uint32_t client_entries() const {
+    return (period && (tick % int64_t(period)) == 0) ? entries : 0u;
+  }
 };
 
 // ------------------------------------------------------------------ RNG --
@@ -131,7 +148,7 @@ struct Group {
   uint32_t voted;       // 1 bit per replica
   uint32_t known;       // deadline register valid
   uint32_t d_term, d_last, d_commit, d_dl, d_rs;
-  int primary, fault, meta0;
+  int primary, fault, meta0, hbt;
   uint32_t iso;         // EXT: replicas isolated during this tick
   uint32_t g;           // group index on this engine (lane)
   uint64_t key;
@@ -175,10 +192,15 @@ struct Group {
     const int m = at(P.gmeta, g);
     meta0 = m;
     primary = m & 0xF;
-    fault = m >> 4;
+    fault = (m >> 4) & 0xF;
+    hbt = HB_NONE;
   }
+  // Effective timer start: followers/candidates also count the last
+  // steady-state heartbeat (hb), which resets every follower at once.
+  __device__ __forceinline__ int eff_start(int ts, int r) const { return role(r) == ROLE_L ? ts : max(ts, hbt); }
   __device__ __forceinline__ void load(const DevPlanes& P, bool with_deadlines) {
     roles = 0; voted = 0;
+    hbt = at(P.hb, g);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       term[r] = at(prow(P.term, r, P.Gp), g);
@@ -188,9 +210,16 @@ struct Group {
       roles |= (x & 3u) << (2 * r);
       voted |= ((x >> 2) & 1u) << r;
       dur[r] = int(x >> 3);
-      dl[r] = with_deadlines ? at(prow(P.deadline, r, P.Gp), g) : 0;
     }
+#pragma unroll
+    for (int r = 0; r < R; ++r) dl[r] = with_deadlines ? eff_start(at(prow(P.tstart, r, P.Gp), g), r) + dur[r] : 0;
     known = with_deadlines ? (1u << R) - 1u : 0u;
+    // materialise a MatchIndex row that the fast kernel kept implicit
+    if ((meta0 & M_MSYNC) && primary < R) {
+#pragma unroll
+      for (int p = 0; p < R; ++p)
+        if (p != primary) at(prow(P.lmatch, p, P.Gp), g) = last[p];
+    }
   }
   __device__ __forceinline__ void store(const DevPlanes& P) const {
 #pragma unroll
@@ -198,13 +227,15 @@ struct Group {
       if ((d_term >> r) & 1u) at(prow(P.term, r, P.Gp), g) = term[r];
       if ((d_last >> r) & 1u) at(prow(P.last, r, P.Gp), g) = last[r];
       if ((d_commit >> r) & 1u) at(prow(P.commit, r, P.Gp), g) = commit[r];
-      if ((d_dl >> r) & 1u) at(prow(P.deadline, r, P.Gp), g) = dl[r];
+      if ((d_dl >> r) & 1u) at(prow(P.tstart, r, P.Gp), g) = dl[r] - dur[r];
       if ((d_rs >> r) & 1u)
         at(prow(P.rs, r, P.Gp), g) =
             uint16_t(((roles >> (2 * r)) & 3u) | (((voted >> r) & 1u) << 2) | (uint32_t(dur[r]) << 3));
     }
-    const int m = primary | (fault << 4);
-    if (m != meta0) at(P.gmeta, g) = uint8_t(m);
+    // DEFER and MSYNC are consumed by the general path; STEADY is recomputed
+    const bool steady = primary < R && role(primary) == ROLE_L && (roles & ~(3u << (2 * primary))) == 0u;
+    const int m = primary | (fault << 4) | (steady ? M_STEADY : 0);
+    if (m != meta0) at(P.gmeta, g) = uint16_t(m);
   }
 
   // Log ring of replica r: entry idx (1-based) at slot (idx-1) mod K.
@@ -221,7 +252,7 @@ struct Group {
   template <int Rp>
   __device__ __forceinline__ int deadline_of(const DevPlanes& P) {
     if (!((known >> Rp) & 1u)) {
-      dl[Rp] = at(prow(P.deadline, Rp, P.Gp), g);
+      dl[Rp] = eff_start(at(prow(P.tstart, Rp, P.Gp), g), Rp) + dur[Rp];
       known |= 1u << Rp;
     }
     return dl[Rp];

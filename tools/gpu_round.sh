@@ -9,4 +9,5 @@ mkdir -p $OUT
 STEPS=${STEPS:-200}
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 \
 && timeout -k 10 240 python -u bench.py --steps $STEPS --warmup 20 > $OUT/bench.log 2>&1 \
+&& timeout -k 10 240 python -u bench.py --steps 100 --warmup 10 --groups-per-gpu 4194304 --no-cpu-baseline > $OUT/bench_4m.log 2>&1 \
 && timeout -k 10 180 rocprofv3 --kernel-trace --stats -T -d $OUT/prof -o run --output-format csv -- python -u bench.py --steps 50 --warmup 5 --no-cpu-baseline > $OUT/prof.log 2>&1
