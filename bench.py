@@ -27,28 +27,42 @@ R_DEFAULT = 5
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def algorithmic_bytes(R, E):
+def algorithmic_bytes(R, E, crc=False):
     """minimal SoA bytes per group-step, REF steady state:
-    B(R,E) = 25 + 37(R-1) + 12 E R (233 B at R=5, E=1)."""
-    return 25 + 37 * (R - 1) + 12 * E * R
+    B(R,E) = 25 + 37(R-1) + 12 E R (233 B at R=5, E=1), + 4 E R with a
+    CRC32C stamp per entry (C5: 5293 B)."""
+    return 25 + 37 * (R - 1) + 12 * E * R + (4 * E * R if crc else 0)
 
 
-def cpu_baseline(args, R, E):
+# SURVEY.md §8(d) workloads runnable by this bench (per GPU)
+WORKLOADS = {
+    "C2": dict(groups=1 << 20, entries=1, ring_depth=32, crc=0,
+               desc="steady-state AppendEntries+commit"),
+    "C3": dict(groups=1 << 21, entries=1, ring_depth=32, crc=0,
+               desc="steady-state AppendEntries+commit, 2^21 groups per GPU (16M over 8 GPUs)"),
+    "C5": dict(groups=1 << 20, entries=64, ring_depth=128, crc=1,
+               desc="64-entry AppendEntries batches with per-entry CRC32C stamp+verify"),
+}
+
+
+def cpu_baseline(args, R, E, K, crc):
     """The oracle (C restatement of main.go's handlers, oracle/) timed on the
     host cores on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     G, T = args.cpu_groups, args.cpu_ticks
-    o = oracle.Oracle(replicas=R, groups=G, ring_depth=32, client_period=1, entries_per_tick=E,
-                      seed=0x5EED0002)
+    if E > 1:   # keep the sample's CPU time and memory bounded for big batches
+        G, T = max(1024, G // E), max(16, T // 4)
+    o = oracle.Oracle(replicas=R, groups=G, ring_depth=K, client_period=1, entries_per_tick=E,
+                      payload_crc=crc, seed=0x5EED0002)
     o.init_steady(0, 0)
     t0 = time.perf_counter()
     o.tick(1, T, threads=threads)
     dt = time.perf_counter() - t0
     o.close()
     return {"value": G * T / dt, "unit": "group-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{G} groups x {T} ticks, R={R}, E={E}, steady state from init_steady, "
+            "sample": f"{G} groups x {T} ticks, R={R}, E={E}, crc={crc}, steady state from init_steady, "
                       f"{threads} pthreads over contiguous group ranges ({dt:.2f} s)"}
 
 
@@ -70,10 +84,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--groups-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--groups-per-gpu", type=int, default=None)
     ap.add_argument("--replicas", type=int, default=R_DEFAULT)
-    ap.add_argument("--entries", type=int, default=1)
-    ap.add_argument("--ring-depth", type=int, default=32)
+    ap.add_argument("--entries", type=int, default=None)
+    ap.add_argument("--ring-depth", type=int, default=None)
     ap.add_argument("--leader", type=int, default=0, help="steady-state leader replica (-1: hashed per group)")
     ap.add_argument("--cpu-groups", type=int, default=131072)
     ap.add_argument("--cpu-ticks", type=int, default=256)
@@ -88,20 +103,32 @@ def main():
 
     import torch
     dist = None
+    # test hook: several ranks on ONE GPU (gloo for torch.distributed, no engine
+    # RCCL communicator) to rehearse the N>1 path on a one-GPU box
+    same_dev = os.environ.get("RAFTSTEP_BENCH_SAME_DEVICE") == "1"
+    if same_dev:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if same_dev:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from raftstep import Engine, STAT_NAMES
 
-    R, E, G = args.replicas, args.entries, args.groups_per_gpu
-    eng = Engine(replicas=R, groups=G, group_base=rank * G, ring_depth=args.ring_depth,
-                 entries_per_tick=E, client_period=1, seed=0x5EED0002, device=local)
-    if dist is not None:
-        uid = [Engine.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(world, rank, uid[0])
+    wl = WORKLOADS[args.workload]
+    R = args.replicas
+    G = args.groups_per_gpu or wl["groups"]
+    E = args.entries or wl["entries"]
+    K = args.ring_depth or wl["ring_depth"]
+    crc = wl["crc"]
+    eng = Engine(replicas=R, groups=G, group_base=rank * G, ring_depth=K, entries_per_tick=E, client_period=1,
+                 payload_crc=crc, seed=0x5EED0002, device=local)
+    if dist is not None and not same_dev:
+        from raftstep import dist as rdist
+        eng.comm_init(world, rank, rdist.exchange_comm_id(dist, rank, Engine.comm_unique_id))
     eng.init_steady(args.leader, 0)
 
     tick = 1
@@ -115,18 +142,19 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    eng.profile(True)
+    eng.profile(2)   # one HIP event pair on the engine stream around the timed ticks
     barrier()
     t0 = time.perf_counter()
     stats = eng.tick(tick, args.steps, stats=True)   # K fused tick launches + per-tick stats (+RCCL sum)
     barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms, launches = eng.profile_read()
-    eng.profile(False)
+    eng.profile(0)
     if dist is not None:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        from raftstep import dist as rdist
+        elapsed = rdist.max_over_ranks(dist, elapsed, device=None if same_dev else "cuda")
+        if same_dev:   # no engine communicator: sum the stats through torch.distributed
+            stats = rdist.sum_over_ranks(dist, stats)
 
     total_steps = G * world * args.steps
     value = total_steps / elapsed
@@ -135,10 +163,10 @@ def main():
     expect_commit = G * world * args.steps * E
     ok = stats[STAT_NAMES.index("committed")] == expect_commit and stats[STAT_NAMES.index("faults")] == 0
 
-    B = algorithmic_bytes(R, E)
-    avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)
+    B = algorithmic_bytes(R, E, crc)
+    avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)   # region events / launches: tick kernel + gaps
     achieved = B * G / avg_kernel_s / 1e9
-    workload = f"C2: {G} x {R}-replica groups per GPU, steady-state AppendEntries+commit, E={E}"
+    workload = f"{args.workload}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}"
     traffic = load_pmc(workload)
     result = {
         "metric": "Raft group-steps/sec at 1M 5-replica groups, 1-8 GPUs; % of HBM peak",
@@ -154,7 +182,7 @@ def main():
         "dtype": "int32",
         "data": "synthetic (seeded splitmix64 trace; post-election steady state, SURVEY.md §8(d) C2)",
         "config": {"workload": workload, "groups_per_gpu": G, "groups_total": G * world, "replicas": R,
-                   "entries_per_tick": E, "ring_depth": args.ring_depth, "leader": args.leader,
+                   "entries_per_tick": E, "ring_depth": K, "payload_crc32c": bool(crc), "leader": args.leader,
                    "semantics": "REF (main.go)", "parallelism": f"group-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -163,7 +191,7 @@ def main():
         "stats_check": bool(ok),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, R, E)
+        result["cpu_baseline"] = cpu_baseline(args, R, E, K, crc)
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RAFT_ABI_VERSION 1u
+#define RAFT_ABI_VERSION 2u
 #define RAFT_MAX_REPLICAS 8u
 
 /* Node.State (main.go:51-57). */
@@ -97,7 +97,9 @@ typedef struct raft_config {
   uint32_t isolate_min_ticks;  /* EXT: isolation length range, 1..32 */
   uint32_t isolate_max_ticks;
   int32_t device;              /* HIP device ordinal */
-  uint32_t reserved[8];
+  uint32_t payload_crc;        /* EXT (config C5): stamp every entry with CRC32C(term||value), followers verify */
+  uint32_t corrupt_per_65536;  /* EXT: probability that an AppendEntries' last entry arrives with a flipped bit */
+  uint32_t reserved[6];
 } raft_config;
 
 /* Canonical host view of engine state, group-major:
@@ -118,6 +120,7 @@ typedef struct raft_state_view {
   uint8_t* fault;     /* per group, enum raft_fault */
   int32_t* log_term;  /* Log.Term (main.go:47) */
   int64_t* log_value; /* Log.Value (main.go:48) */
+  uint32_t* log_crc;  /* EXT: CRC32C of each ring entry (0 when payload_crc is off) */
 } raft_state_view;
 
 typedef struct raft_engine raft_engine;
@@ -231,9 +234,15 @@ int raft_comm_init(raft_engine* e, int nranks, int rank, const uint8_t id[128]);
 int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats);
 
 /* ---- instrumentation -----------------------------------------------------
- * When enabled, every tick launch is bracketed by HIP events on the engine
- * stream; raft_profile_read() syncs and returns the summed kernel time. */
-int raft_profile_enable(raft_engine* e, int enable);
+ * mode 1: every steady-state tick kernel is timed by events attached to its
+ *         own dispatch (hipExtLaunchKernel) — kernel-exact, but the events
+ *         cost ~5 us per launch of wall time;
+ * mode 2: one event pair on the engine stream around all launches of each
+ *         raft_tick call (no per-launch cost; includes the general kernel and
+ *         launch gaps, so it upper-bounds the tick kernel's duration);
+ * mode 0: off. raft_profile_read() syncs and returns the summed milliseconds
+ * and the number of tick launches covered. */
+int raft_profile_enable(raft_engine* e, int mode);
 int raft_profile_read(raft_engine* e, double* total_ms, uint64_t* launches);
 
 #ifdef __cplusplus

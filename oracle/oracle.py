@@ -48,6 +48,9 @@ def load(path=None):
             "oracle_isolated": (C.c_int, [P, C.c_uint64, C.c_uint32, C.c_int64]),
             "oracle_steady_leader": (C.c_uint32, [P, C.c_uint64, C.c_int32]),
             "oracle_nodelog": (C.c_int, [P, C.c_uint64, C.c_char_p, C.c_size_t]),
+            "oracle_crc32c": (C.c_uint32, [C.c_char_p, C.c_size_t]),
+            "oracle_entry_crc": (C.c_uint32, [C.c_int64, C.c_int64]),
+            "oracle_corrupted": (C.c_int, [P, C.c_uint64, C.c_uint32, C.c_int64]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -104,8 +107,8 @@ class Oracle:
     def store_state(self, logs=True):
         st = abi.empty_state(self.cfg.groups, self.cfg.replicas, self.cfg.ring_depth)
         if not logs:
-            st.pop("log_term")
-            st.pop("log_value")
+            for k in ("log_term", "log_value", "log_crc"):
+                st.pop(k)
         v = abi.make_view(st)
         self.lib.oracle_store_state(self.h, C.byref(v))
         return st
@@ -158,5 +161,16 @@ class Oracle:
     def isolated(self, gid, replica, tick):
         return bool(self.lib.oracle_isolated(C.byref(self.cfg), gid, replica, tick))
 
+    def corrupted(self, gid, replica, tick):
+        return bool(self.lib.oracle_corrupted(C.byref(self.cfg), gid, replica, tick))
+
     def steady_leader(self, gid, leader):
         return self.lib.oracle_steady_leader(C.byref(self.cfg), gid, leader)
+
+
+def crc32c(data):
+    return load().oracle_crc32c(bytes(data), len(data))
+
+
+def entry_crc(term, value):
+    return load().oracle_entry_crc(term, value)

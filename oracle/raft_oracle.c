@@ -23,7 +23,7 @@
 
 #define I32MAX 2147483647LL
 
-enum { ST_VALUE = 1, ST_TIMER_F = 2, ST_TIMER_C = 3, ST_ISOLATE = 4 };
+enum { ST_VALUE = 1, ST_TIMER_F = 2, ST_TIMER_C = 3, ST_ISOLATE = 4, ST_CORRUPT = 5 };
 
 /* ---------------------------------------------------------------- RNG ---- */
 static uint64_t sm64(uint64_t x) {
@@ -66,8 +66,35 @@ int oracle_isolated(const raft_config* c, uint64_t gid, uint32_t replica, int64_
   return 0;
 }
 
+/* EXT (config C5): CRC32C (Castagnoli, reflected poly 0x82F63B78, init and
+ * final xor 0xFFFFFFFF) of an entry's 12 payload bytes: Term as 4 bytes
+ * little-endian, then Value as 8 bytes little-endian. Bitwise reference
+ * implementation; check value CRC32C("123456789") = 0xE3069283. */
+uint32_t oracle_crc32c(const uint8_t* p, size_t n) {
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; ++i) {
+    c ^= p[i];
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+  }
+  return c ^ 0xFFFFFFFFu;
+}
+uint32_t oracle_entry_crc(int64_t term, int64_t value) {
+  uint8_t b[12];
+  uint32_t t = (uint32_t)term;
+  uint64_t v = (uint64_t)value;
+  for (int i = 0; i < 4; ++i) b[i] = (uint8_t)(t >> (8 * i));
+  for (int i = 0; i < 8; ++i) b[4 + i] = (uint8_t)(v >> (8 * i));
+  return oracle_crc32c(b, 12);
+}
+/* EXT: does the AppendEntries delivered to `replica` at `tick` arrive with its
+ * last entry's Value bit 0 flipped? */
+int oracle_corrupted(const raft_config* c, uint64_t gid, uint32_t replica, int64_t tick) {
+  if (!c->payload_crc || !c->corrupt_per_65536) return 0;
+  return (oracle_rng(c->seed, gid, replica, ST_CORRUPT, (uint64_t)tick) & 0xFFFF) < c->corrupt_per_65536;
+}
+
 /* ------------------------------------------------------------ state ---- */
-typedef struct { int64_t term, value; } o_ent;   /* Log (main.go:46-49) */
+typedef struct { int64_t term, value; uint32_t crc; } o_ent;   /* Log (main.go:46-49) + EXT crc */
 
 typedef struct {                                 /* Node (main.go:14-39) */
   int role;                                      /* State */
@@ -103,6 +130,7 @@ typedef struct {                                 /* AppendEntriesRequest (main.g
   int64_t term, prev_idx, prev_term, lc;
   const o_ent* ents;
   int64_t n;
+  int corrupt;                                   /* EXT: last entry arrives with a flipped bit */
 } o_ae;
 typedef struct { int64_t term, match; int ok; } o_aer;  /* AppendEntriesResponse (main.go:298-302) */
 
@@ -159,6 +187,13 @@ static o_aer follower_ae(const o_ctx* c, o_group* G, int x, const o_ae* r) {
     if (t != r->prev_term) return res;                   /* 142-145 */
   }
   if (n->last + r->n > I32MAX) { set_fault(G, RAFT_F_OVERFLOW); return res; }
+  if (c->cfg->payload_crc) {                             /* EXT: verify what will be stored (last K) */
+    int64_t j0 = r->n > (int64_t)c->cfg->ring_depth ? r->n - (int64_t)c->cfg->ring_depth : 0;
+    for (int64_t j = j0; j < r->n; ++j) {
+      int64_t v = r->ents[j].value ^ ((r->corrupt && j == r->n - 1) ? 1 : 0);
+      if (oracle_entry_crc(r->ents[j].term, v) != r->ents[j].crc) return res;
+    }
+  }
   log_append(n, r->ents, r->n);                          /* 148-149 */
   if (r->lc > n->commit)                                 /* 151-152: min(LC, len(Log)+1) */
     n->commit = r->lc < n->last + 1 ? r->lc : n->last + 1;
@@ -287,6 +322,7 @@ static void leader_round(o_ctx* c, o_group* G, int L) {
     if (dropped(c, L, p)) { c->st[RAFT_STAT_AE_FAIL]++; continue; }  /* EXT */
     o_ae r;
     r.term = n->term; r.lc = n->commit;
+    r.corrupt = oracle_corrupted(c->cfg, c->gid, (uint32_t)p, c->tick);
     int64_t nxt = n->match[p] + 1;                       /* NextIndex == MatchIndex + 1 */
     if (nxt <= n->last) {                                /* 341 */
       if (nxt == 1) {                                    /* 343-351: whole log, PrevLogIndex 0 */
@@ -328,7 +364,7 @@ static void timeout_fire(o_ctx* c, o_group* G, int x) {
 static void client_append(const o_ctx* c, o_group* G, int L, int64_t value) {
   o_node* n = &G->n[L];
   if (n->last >= I32MAX) { set_fault(G, RAFT_F_OVERFLOW); return; }
-  o_ent e = {n->term, value};
+  o_ent e = {n->term, value, c->cfg->payload_crc ? oracle_entry_crc(n->term, value) : 0u};
   log_append(n, &e, 1);
 }
 
@@ -458,6 +494,8 @@ int oracle_load_state(oracle* o, const raft_state_view* v) {
           uint64_t s = i * K + (uint64_t)((idx - 1) & (K - 1));
           tmp[idx - 1].term = v->log_term[s];
           tmp[idx - 1].value = v->log_value[s];
+          tmp[idx - 1].crc = v->log_crc ? v->log_crc[s]
+                           : (o->cfg.payload_crc ? oracle_entry_crc(v->log_term[s], v->log_value[s]) : 0u);
         }
         log_append(n, tmp, last);
         free(tmp);
@@ -488,12 +526,14 @@ void oracle_store_state(const oracle* o, raft_state_view* v) {
       for (uint32_t s = 0; s < K; ++s) {
         if (v->log_term) v->log_term[i * K + s] = 0;
         if (v->log_value) v->log_value[i * K + s] = 0;
+        if (v->log_crc) v->log_crc[i * K + s] = 0;
       }
       int64_t lo = n->last > K ? n->last - K + 1 : 1;
       for (int64_t idx = lo; idx <= n->last; ++idx) {
         uint64_t s = i * K + (uint64_t)((idx - 1) & (K - 1));
         if (v->log_term) v->log_term[s] = (int32_t)n->log[idx - 1].term;
         if (v->log_value) v->log_value[s] = n->log[idx - 1].value;
+        if (v->log_crc) v->log_crc[s] = n->log[idx - 1].crc;
       }
     }
   }
@@ -576,11 +616,19 @@ int oracle_append_entries(oracle* o, int64_t now_tick, const raft_ae_req* reqs, 
     raft_ae_resp* rs = &out[i];
     memset(rs, 0, sizeof *rs);
     if (G->fault) { rs->fault = G->fault; continue; }
+    o_ent* ents = (o_ent*)calloc(q->n_entries ? q->n_entries : 1, sizeof(o_ent));
+    for (uint64_t k = 0; k < q->n_entries; ++k) {   /* host payloads are stamped on ingest */
+      const raft_log_entry* le = &entries[q->entries_offset + k];
+      ents[k].term = le->term; ents[k].value = le->value;
+      ents[k].crc = o->cfg.payload_crc ? oracle_entry_crc(le->term, le->value) : 0u;
+    }
     o_ae r;
     r.term = q->term; r.prev_idx = q->prev_log_index; r.prev_term = q->prev_log_term;
     r.lc = q->leader_commit; r.n = (int64_t)q->n_entries;
-    r.ents = (const o_ent*)(entries + q->entries_offset);
+    r.ents = ents;
+    r.corrupt = 0;
     o_aer a = deliver_ae(&c, G, (int)q->to, &r);
+    free(ents);
     rs->term = a.term; rs->match_index = a.match; rs->success = G->fault ? 0 : a.ok;
     rs->fault = G->fault;
   }
@@ -625,7 +673,7 @@ int oracle_group_ops(oracle* o, int64_t now_tick, const raft_group_op* ops, size
     o_node* nd = &G->n[x];
     if (G->fault) { rs->fault = G->fault; continue; }
     switch (q->kind) {
-      case RAFT_OP_CLIENT_APPEND:
+      case RAFT_OP_CLIENT_APPEND:  /* arg = Value */
         if (nd->role != RAFT_LEADER) { rs->status = RAFT_EINVAL; break; }
         client_append(&c, G, x, q->arg);
         rs->value = nd->last;

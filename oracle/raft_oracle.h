@@ -49,6 +49,10 @@ int32_t oracle_timer_draw(const raft_config* cfg, uint64_t gid, uint32_t replica
 int oracle_isolated(const raft_config* cfg, uint64_t gid, uint32_t replica, int64_t tick);
 /* Leader replica of raft_init_steady (leader < 0: hashed per group). */
 uint32_t oracle_steady_leader(const raft_config* cfg, uint64_t gid, int32_t leader);
+/* EXT CRC32C (Castagnoli) and the entry stamp CRC32C(term_le32 || value_le64). */
+uint32_t oracle_crc32c(const uint8_t* p, size_t n);
+uint32_t oracle_entry_crc(int64_t term, int64_t value);
+int oracle_corrupted(const raft_config* cfg, uint64_t gid, uint32_t replica, int64_t tick);
 /* nodelog-format dump of one group (main.go:399-401), for debugging. */
 int oracle_nodelog(const oracle* o, uint64_t group, char* buf, size_t cap);
 

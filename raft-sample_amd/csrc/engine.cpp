@@ -49,6 +49,31 @@ int fail(int code, const char* fmt, ...) {
 
 constexpr int I32 = 2147483647;
 
+// CRC32C (Castagnoli, reflected 0x82F63B78) slice-by-8 tables, T[k][b].
+std::vector<uint32_t> crc32c_tables() {
+  std::vector<uint32_t> T(8 * 256);
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t c = b;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    T[b] = c;
+  }
+  for (int k = 1; k < 8; ++k)
+    for (uint32_t b = 0; b < 256; ++b) T[k * 256 + b] = (T[(k - 1) * 256 + b] >> 8) ^ T[T[(k - 1) * 256 + b] & 255];
+  return T;
+}
+const std::vector<uint32_t>& crc_tab_host() {
+  static const std::vector<uint32_t> T = crc32c_tables();
+  return T;
+}
+uint32_t host_entry_crc(int32_t term, int64_t value) {
+  const std::vector<uint32_t>& T = crc_tab_host();
+  uint32_t c = 0xFFFFFFFFu ^ uint32_t(term);
+  c = T[768 + (c & 255)] ^ T[512 + ((c >> 8) & 255)] ^ T[256 + ((c >> 16) & 255)] ^ T[c >> 24];
+  const uint32_t lo = c ^ uint32_t(uint64_t(value)), hi = uint32_t(uint64_t(value) >> 32);
+  return ~(T[1792 + (lo & 255)] ^ T[1536 + ((lo >> 8) & 255)] ^ T[1280 + ((lo >> 16) & 255)] ^ T[1024 + (lo >> 24)] ^
+           T[768 + (hi & 255)] ^ T[512 + ((hi >> 8) & 255)] ^ T[256 + ((hi >> 16) & 255)] ^ T[hi >> 24]);
+}
+
 bool fits32(int64_t v) { return v >= -int64_t(I32) - 1 && v <= int64_t(I32); }
 
 }  // namespace
@@ -70,11 +95,13 @@ struct raft_engine {
   uint32_t* wcount = nullptr;   // [2], indexed by window parity
   int force_general = 0;        // debug: route every group through the general kernel
   uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
+  int write_through = 0;        // fast kernel stores with sc1 (write-through) instead of write-back
   // handler-batch staging
   void* stage = nullptr;
   size_t stage_cap = 0;
-  // profiling
-  bool prof = false;
+  // profiling: 0 off, 1 per fast-kernel dispatch (hipExtLaunchKernel events),
+  // 2 one event pair around each raft_tick call's launches (no per-launch cost)
+  int prof = 0;
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
   double prof_ms = 0.0;
@@ -174,27 +201,29 @@ int check_distinct(const raft_engine* e, const uint64_t* first, size_t stride, s
 
 // Runs a prepared DevOp batch (+ entries) through ops_kernel and returns the results.
 int run_ops(raft_engine* e, int64_t now_tick, const std::vector<DevOp>& ops, const std::vector<int32_t>& et,
-            const std::vector<int64_t>& ev, std::vector<DevRes>& res) {
+            const std::vector<int64_t>& ev, const std::vector<uint32_t>& ec, std::vector<DevRes>& res) {
   const size_t n = ops.size();
   res.assign(n, DevRes{});
   if (!n) return RAFT_OK;
   if (int rc = check_ticks(e, now_tick, 1)) return rc;
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t b_ops = al(n * sizeof(DevOp)), b_res = al(n * sizeof(DevRes));
-  const size_t b_et = al(et.size() * 4 + 4), b_ev = al(ev.size() * 8 + 8);
-  if (int rc = ensure_stage(e, b_ops + b_res + b_et + b_ev)) return rc;
+  const size_t b_et = al(et.size() * 4 + 4), b_ev = al(ev.size() * 8 + 8), b_ec = al(ec.size() * 4 + 4);
+  if (int rc = ensure_stage(e, b_ops + b_res + b_et + b_ev + b_ec)) return rc;
   char* base = static_cast<char*>(e->stage);
   DevOp* d_ops = reinterpret_cast<DevOp*>(base);
   DevRes* d_res = reinterpret_cast<DevRes*>(base + b_ops);
   int32_t* d_et = reinterpret_cast<int32_t*>(base + b_ops + b_res);
   int64_t* d_ev = reinterpret_cast<int64_t*>(base + b_ops + b_res + b_et);
+  uint32_t* d_ec = reinterpret_cast<uint32_t*>(base + b_ops + b_res + b_et + b_ev);
   HIPCHK(hipMemcpyAsync(d_ops, ops.data(), n * sizeof(DevOp), hipMemcpyHostToDevice, e->stream));
   if (!et.empty()) {
     HIPCHK(hipMemcpyAsync(d_et, et.data(), et.size() * 4, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(d_ev, ev.data(), ev.size() * 8, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(d_ec, ec.data(), ec.size() * 4, hipMemcpyHostToDevice, e->stream));
   }
   const Trace T = make_trace(e, now_tick);
-  HIPCHK(launch_ops(e->R, e->P, T, d_ops, uint32_t(n), d_et, d_ev, d_res, e->stream));
+  HIPCHK(launch_ops(e->R, e->P, T, d_ops, uint32_t(n), d_et, d_ev, d_ec, d_res, e->stream));
   HIPCHK(hipMemcpyAsync(res.data(), d_res, n * sizeof(DevRes), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return RAFT_OK;
@@ -255,6 +284,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
       c.candidate_timeout_min + c.candidate_timeout_span > 8192)
     return fail(RAFT_EINVAL, "timer ranges must be >= 1 and below 8192 s");
   if (c.isolate_per_65536 > 65536) return fail(RAFT_EINVAL, "isolate_per_65536 must be <= 65536");
+  if (c.payload_crc > 1) return fail(RAFT_EINVAL, "payload_crc must be 0 or 1");
+  if (c.corrupt_per_65536 > 65536) return fail(RAFT_EINVAL, "corrupt_per_65536 must be <= 65536");
   if (c.isolate_per_65536 &&
       (c.isolate_min_ticks < 1 || c.isolate_max_ticks > 32 || c.isolate_min_ticks > c.isolate_max_ticks))
     return fail(RAFT_EINVAL, "isolation length must satisfy 1 <= min <= max <= 32");
@@ -291,6 +322,10 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->wcount), 256);
   A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.log_value), R * K * Gp * 8);
+  if (c.payload_crc) A(reinterpret_cast<void**>(&e->P.log_crc), R * K * Gp * 4);
+  uint32_t* d_tab = nullptr;
+  A(reinterpret_cast<void**>(&d_tab), 8 * 256 * 4);
+  e->P.crc_tab = d_tab;
   if (rc == RAFT_OK) {
     hipError_t h = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (h != hipSuccess) rc = fail(RAFT_EHIP, "hipStreamCreate: %s", hipGetErrorString(h));
@@ -306,8 +341,11 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->P.gbase = c.group_base;
   e->P.K = c.ring_depth;
   e->P.kmask = c.ring_depth - 1;
+  e->P.crc_on = c.payload_crc;
+  e->P.corrupt_p = c.corrupt_per_65536;
   if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
   if (const char* se = getenv("RAFTSTEP_SLOW_EVERY")) e->slow_every = std::max(1, atoi(se));
+  if (const char* wt = getenv("RAFTSTEP_WRITE_THROUGH")) e->write_through = atoi(wt) != 0;
   // zero everything once so that padding / unused rows are deterministic
   for (void* p : e->allocs) (void)p;
   hipError_t z = hipSuccess;
@@ -325,6 +363,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, 256, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_value, 0, R * K * Gp * 8, e->stream) : z;
+  if (c.payload_crc) z = z == hipSuccess ? hipMemsetAsync(e->P.log_crc, 0, R * K * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemcpyAsync(d_tab, crc_tab_host().data(), 8 * 256 * 4, hipMemcpyHostToDevice, e->stream) : z;
   z = z == hipSuccess ? hipStreamSynchronize(e->stream) : z;
   if (z != hipSuccess) {
     raft_engine_destroy(e);
@@ -382,6 +422,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt;
   std::vector<uint16_t> rs, meta;
   std::vector<int64_t> lv;
+  std::vector<uint32_t> lcrc;
   int rc = RAFT_OK;
   if (!rc) rc = d2h(e, term, e->P.term, R * Gp);
   if (!rc) rc = d2h(e, last, e->P.last, R * Gp);
@@ -392,11 +433,13 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!rc) rc = d2h(e, lm, e->P.lmatch, R * Gp);
   if (!rc) rc = d2h(e, xm, e->P.xmatch, R * R * Gp);
   if (!rc) rc = d2h(e, meta, e->P.gmeta, Gp);
-  const bool logs = v->log_term || v->log_value;
+  const bool logs = v->log_term || v->log_value || v->log_crc;
   std::vector<int32_t> ltm;
   if (!rc && logs) rc = d2h(e, ltm, e->P.lterm, R * Gp);
   if (!rc && logs) rc = d2h(e, lt, e->P.log_term, R * K * Gp);
   if (!rc && logs) rc = d2h(e, lv, e->P.log_value, R * K * Gp);
+  const bool crcs = v->log_crc && e->cfg.payload_crc;
+  if (!rc && crcs) rc = d2h(e, lcrc, e->P.log_crc, R * K * Gp);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(e->stream));
   for (uint64_t g = 0; g < G; ++g) {
@@ -436,6 +479,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
           const uint64_t o = (r * K + s) * Gp + g;
           if (v->log_term) v->log_term[c * K + s] = live ? lt[o] : 0;
           if (v->log_value) v->log_value[c * K + s] = live ? lv[o] : 0;
+          if (v->log_crc) v->log_crc[c * K + s] = (live && crcs) ? lcrc[o] : 0u;
         }
       }
     }
@@ -456,6 +500,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   std::vector<uint16_t> meta(Gp, uint16_t(NO_PRIMARY));
   std::vector<int64_t> lv(R * K * Gp, 0);
   std::vector<int32_t> ltm(R * Gp, 0);
+  std::vector<uint32_t> lcrc(e->cfg.payload_crc ? R * K * Gp : 0, 0);
   for (uint64_t g = 0; g < G; ++g) {
     if (v->fault[g] > RAFT_F_OVERFLOW) return fail(RAFT_EINVAL, "group %llu: bad fault code", (unsigned long long)g);
     int primary = NO_PRIMARY;
@@ -486,6 +531,9 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
       for (uint64_t s = 0; s < K; ++s) {
         lt[(r * K + s) * Gp + g] = v->log_term[c * K + s];
         lv[(r * K + s) * Gp + g] = v->log_value[c * K + s];
+        if (e->cfg.payload_crc)
+          lcrc[(r * K + s) * Gp + g] = v->log_crc ? v->log_crc[c * K + s]
+                                                  : host_entry_crc(v->log_term[c * K + s], v->log_value[c * K + s]);
       }
       if (v->last[c] > 0) ltm[d] = v->log_term[c * K + uint64_t((v->last[c] - 1) & int64_t(K - 1))];
     }
@@ -501,6 +549,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.xmatch, xm);
   if (!rc) rc = h2d(e, e->P.gmeta, meta);
   if (!rc) rc = h2d(e, e->P.lterm, ltm);
+  if (!rc && e->cfg.payload_crc) rc = h2d(e, e->P.log_crc, lcrc);
   if (!rc) rc = h2d(e, e->P.log_term, lt);
   if (!rc) rc = h2d(e, e->P.log_value, lv);
   if (rc) return rc;
@@ -518,24 +567,36 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   HIPCHK(hipMemsetAsync(e->wcount, 0, 2 * sizeof(uint32_t), e->stream));
   const Trace T0 = make_trace(e, first_tick);
   uint32_t window = 0;
+  hipEvent_t ra = nullptr, rb = nullptr;
+  if (e->prof == 2) {
+    ra = next_event(e);
+    rb = next_event(e);
+    if (!ra || !rb) return fail(RAFT_EHIP, "hipEventCreate failed");
+    HIPCHK(hipEventRecord(ra, e->stream));
+  }
   for (uint32_t i = 0; i < nticks; ++i) {
     const int64_t t = first_tick + int64_t(i);
     const Trace T = make_trace(e, t);
     unsigned long long* st = stats ? e->hist + size_t(i) * STAT_SLOTS * NSTAT : nullptr;
     uint32_t* cnt = e->wcount + (window & 1);
     hipEvent_t a = nullptr, b = nullptr;
-    if (e->prof) {
+    if (e->prof == 1) {
       a = next_event(e);
       b = next_event(e);
       if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
     }
-    HIPCHK(launch_tick_fast(e->R, e->P, T, st, e->work, e->work_tick, cnt, e->force_general, e->stream, a, b));
+    HIPCHK(launch_tick_fast(e->R, e->P, T, st, e->work, e->work_tick, cnt, e->force_general, e->write_through,
+                            e->stream, a, b));
     // deferred groups catch up every slow_every ticks and at the end of the call
     if ((i + 1) % e->slow_every == 0 || i + 1 == nticks) {
       HIPCHK(launch_tick_slow(e->R, e->P, T0, first_tick, t, stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
                               e->wcount + ((window + 1) & 1), e->stream));
       ++window;
     }
+  }
+  if (e->prof == 2) {
+    HIPCHK(hipEventRecord(rb, e->stream));
+    e->prof_n += nticks;
   }
   if (stats && e->comm)
     RCCLCHK(ncclAllReduce(e->hist, e->hist, size_t(nticks) * STAT_SLOTS * NSTAT, ncclUint64, ncclSum, e->comm,
@@ -577,6 +638,7 @@ int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_re
   std::vector<DevOp> ops(n);
   std::vector<int32_t> et;
   std::vector<int64_t> ev;
+  std::vector<uint32_t> ec;
   for (size_t i = 0; i < n; ++i) {
     const raft_ae_req& q = reqs[i];
     if (q.to >= e->cfg.replicas) return fail(RAFT_EINVAL, "req %zu: receiver out of range", i);
@@ -597,13 +659,14 @@ int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_re
     for (uint64_t j = 0; j < q.n_entries; ++j) {
       const raft_log_entry& le = entries[q.entries_offset + j];
       if (!fits32(le.term)) return fail(RAFT_EINVAL, "req %zu: entry term outside int32", i);
-      if (j < j0) { et.push_back(0); ev.push_back(0); continue; }
+      if (j < j0) { et.push_back(0); ev.push_back(0); ec.push_back(0); continue; }
       et.push_back(int32_t(le.term));
       ev.push_back(le.value);
+      ec.push_back(e->cfg.payload_crc ? host_entry_crc(int32_t(le.term), le.value) : 0u);  // stamped on ingest
     }
   }
   std::vector<DevRes> res;
-  if (int rc = run_ops(e, now_tick, ops, et, ev, res)) return rc;
+  if (int rc = run_ops(e, now_tick, ops, et, ev, ec, res)) return rc;
   for (size_t i = 0; i < n; ++i) {
     out[i].term = res[i].term;
     out[i].match_index = res[i].value;
@@ -627,7 +690,7 @@ int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_re
     ops[i].group = q.group; ops[i].replica = q.to; ops[i].kind = OP_VR; ops[i].term = int32_t(q.term);
   }
   std::vector<DevRes> res;
-  if (int rc = run_ops(e, now_tick, ops, {}, {}, res)) return rc;
+  if (int rc = run_ops(e, now_tick, ops, {}, {}, {}, res)) return rc;
   for (size_t i = 0; i < n; ++i) {
     out[i].term = res[i].term;
     out[i].vote_granted = res[i].ok;
@@ -651,7 +714,7 @@ int raft_group_ops_batch(raft_engine* e, int64_t now_tick, const raft_group_op* 
     ops[i].group = q.group; ops[i].replica = q.replica; ops[i].kind = q.kind; ops[i].arg = q.arg;
   }
   std::vector<DevRes> res;
-  if (int rc = run_ops(e, now_tick, ops, {}, {}, res)) return rc;
+  if (int rc = run_ops(e, now_tick, ops, {}, {}, {}, res)) return rc;
   for (size_t i = 0; i < n; ++i) {
     out[i].status = res[i].status;
     out[i].fault = res[i].fault;
@@ -697,9 +760,10 @@ int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats) {
   return RAFT_OK;
 }
 
-int raft_profile_enable(raft_engine* e, int enable) {
+int raft_profile_enable(raft_engine* e, int mode) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
-  e->prof = enable != 0;
+  if (mode < 0 || mode > 2) return fail(RAFT_EINVAL, "profile mode must be 0, 1 or 2");
+  e->prof = mode;
   e->ev_used = 0;
   e->prof_ms = 0.0;
   e->prof_n = 0;
@@ -714,7 +778,7 @@ int raft_profile_read(raft_engine* e, double* total_ms, uint64_t* launches) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, e->ev[i], e->ev[i + 1]));
     e->prof_ms += ms;
-    e->prof_n += 1;
+    if (e->prof == 1) e->prof_n += 1;   // mode 2 counts launches as it records
   }
   e->ev_used = 0;
   if (total_ms) *total_ms = e->prof_ms;

@@ -31,14 +31,14 @@ struct DevRes {
 // Steady-state fast kernel; groups it does not take are DEFERred to `work`.
 // ev_start/ev_stop (may be null) time the dispatch itself (hipExtLaunchKernel).
 hipError_t launch_tick_fast(int R, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
-                            int32_t* work_tick, uint32_t* work_count, int force_slow, hipStream_t s,
+                            int32_t* work_tick, uint32_t* work_count, int force_slow, int write_through, hipStream_t s,
                             hipEvent_t ev_start, hipEvent_t ev_stop);
 // General kernel: catches every worklisted group up to last_tick; zeroes `next_count`.
 hipError_t launch_tick_slow(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
                             unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
                             const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
 hipError_t launch_ops(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
-                      const int32_t* et, const int64_t* ev, DevRes* out, hipStream_t s);
+                      const int32_t* et, const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s);
 hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_t s);
 hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s);
 

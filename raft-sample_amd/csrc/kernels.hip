@@ -65,8 +65,10 @@ __device__ __forceinline__ void run_tick(Group<R>& G, const DevPlanes& P, const 
       }
       const int e0 = n_ok > int(P.K) ? n_ok - int(P.K) : 0;   // only the last K stay in the ring
       for (int e = e0; e < n_ok; ++e) {
+        const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
         G.ring_term(P, r, l + 1 + e) = G.term[r];
-        G.ring_value(P, r, l + 1 + e) = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+        G.ring_value(P, r, l + 1 + e) = v;
+        if (P.crc_on) G.ring_crc(P, r, l + 1 + e) = crc_entry(P.crc_tab, G.term[r], v);
       }
       if (n_ok) {
         G.last[r] = l + n_ok;
@@ -78,7 +80,7 @@ __device__ __forceinline__ void run_tick(Group<R>& G, const DevPlanes& P, const 
   }
 
   // 2. rounds in ascending replica id, against the roles as they are now.
-  const TickSrc base{P.log_term, P.log_value, P.Gp, G.g, P.K, P.kmask, 0, 1,
+  const TickSrc base{P.log_term, P.log_value, P.log_crc, P.crc_tab, P.crc_on, P.Gp, G.g, P.K, P.kmask, 0, 1,
                      G.cache_leader, G.cache_from, G.cache_term, G.cache_vbase};
   auto make_src = [base](int c) {
     TickSrc s = base;
@@ -158,11 +160,29 @@ __device__ __forceinline__ void block_stats(const int (&v)[N], const int (&idx)[
 // alone until the general kernel has caught it up.
 // MSYNC: after a fast tick every follower's MatchIndex equals its
 // LastApplied (main.go:156 -> 376), so the row is kept implicit.
-template <int R>
+// Store policy of the fast kernel: plain (write-back L2) or write-through
+// (agent-scope relaxed atomic store = global_store ... sc1, which drops the
+// line from L2 so that less dirty data is left for the end-of-kernel flush).
+template <bool WT, typename T>
+__device__ __forceinline__ void st(T* base, uint32_t idx, T v) {
+  if constexpr (WT) __hip_atomic_store(&at(base, idx), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else at(base, idx) = v;
+}
+
+template <int R, bool WT, bool CRC>
 __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, unsigned long long* stats,
                                                         uint32_t* work, int32_t* work_tick, uint32_t* work_count,
                                                         int force_slow) {
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  // EXT CRC32C tables (8 KiB) staged in LDS for the stamp/verify lookups
+  __shared__ uint32_t tab[CRC ? 2048 : 1];
+  if constexpr (CRC) {
+    const uint4* src = reinterpret_cast<const uint4*>(P.crc_tab);
+    uint4* dst = reinterpret_cast<uint4*>(tab);
+    dst[threadIdx.x] = src[threadIdx.x];
+    dst[threadIdx.x + 256] = src[threadIdx.x + 256];
+    __syncthreads();
+  }
   int sv[4] = {0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups
   bool bail = false;
   if (g < P.G) {
@@ -203,6 +223,30 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     int prev_idx, prev_term;
     if (n == 0 || Ll == 0) { prev_idx = Ll; prev_term = Lt; }   // heartbeat / whole-log (PrevLogIndex 0)
     else { prev_idx = Ll; prev_term = Llt; }                      // GetLog(MatchIndex).Term
+    // EXT: every follower verifies the CRC32C stamp of each entry it received
+    // (the term's CRC state is shared, the term bytes are never corrupted)
+    uint32_t crcbad = 0;
+    if constexpr (CRC) {
+      if (go && !bail && n) {
+        uint32_t cm = 0;   // followers whose message is corrupted this tick
+#pragma unroll
+        for (int p = 0; p < R; ++p)
+          if (p != c && P.corrupt_p && (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(T.tick)) & 0xFFFF) < P.corrupt_p)
+            cm |= 1u << p;
+        const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+        const uint32_t cs = crc_term_state(tab, Lt);
+        for (int e = 0; e < n; ++e) {
+          const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+          const uint32_t stamp = crc_value_final(tab, cs, v);               // leader's stamp
+#pragma unroll
+          for (int p = 0; p < R; ++p) {
+            if (p == c) continue;
+            const int64_t rv = v ^ ((((cm >> p) & 1u) && e == n - 1) ? 1 : 0);  // what p received
+            if (crc_value_final(tab, cs, rv) != stamp) crcbad |= 1u << p;
+          }
+        }
+      }
+    }
     uint32_t okm = 0, cch = 0, mch = 0, ltch = 0;
     if (go && !bail) {
 #pragma unroll
@@ -216,6 +260,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
           else ok = lt[p] == prev_term;                           // 142-145 (GetLog(l) == last entry)
         }
         if (ok && int64_t(l) + n > I32MAX) bail = true;
+        if (ok && ((crcbad >> p) & 1u)) ok = false;               // EXT: payload rejected
         if (ok) {
           const int nl = l + n;                                   // 148-149
           last[p] = nl;
@@ -247,19 +292,19 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       sv[3] = 1;
       // ---- stores (no bail past this point) ----
       if (n) {
-        at(P.last + uint64_t(c) * P.Gp, g) = Ll + n;
-        if (Llt != Lt) at(P.lterm + uint64_t(c) * P.Gp, g) = Lt;
+        st<WT>(P.last + uint64_t(c) * P.Gp, g, Ll + n);
+        if (Llt != Lt) st<WT>(P.lterm + uint64_t(c) * P.Gp, g, Lt);
       }
-      if (cm != Lc) at(P.commit + uint64_t(c) * P.Gp, g) = cm;
-      at(P.hb, g) = T.now;                                        // timer.Reset(d) of every follower
+      if (cm != Lc) st<WT>(P.commit + uint64_t(c) * P.Gp, g, cm);
+      st<WT>(P.hb, g, T.now);                                     // timer.Reset(d) of every follower
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == c || !((okm >> p) & 1u)) continue;
-        if (n) at(prow(P.last, p, P.Gp), g) = last[p];
-        if (!sync && ((mch >> p) & 1u)) at(prow(P.lmatch, p, P.Gp), g) = m[p];
-        if ((cch >> p) & 1u) at(prow(P.commit, p, P.Gp), g) = commit[p];
-        if ((ltch >> p) & 1u) at(prow(P.lterm, p, P.Gp), g) = Lt;
-        if (term[p] != Lt) at(prow(P.term, p, P.Gp), g) = Lt;    // main.go:155
+        if (n) st<WT>(prow(P.last, p, P.Gp), g, last[p]);
+        if (!sync && ((mch >> p) & 1u)) st<WT>(prow(P.lmatch, p, P.Gp), g, m[p]);
+        if ((cch >> p) & 1u) st<WT>(prow(P.commit, p, P.Gp), g, commit[p]);
+        if ((ltch >> p) & 1u) st<WT>(prow(P.lterm, p, P.Gp), g, Lt);
+        if (term[p] != Lt) st<WT>(prow(P.term, p, P.Gp), g, Lt);  // main.go:155
       }
       const int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
       if (nm != meta) at(P.gmeta, g) = uint16_t(nm);
@@ -267,18 +312,24 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       if (n) {
         const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
         const uint64_t cb = uint64_t(c) * P.K * P.Gp;
+        uint32_t cs = 0;
+        if constexpr (CRC) cs = crc_term_state(tab, Lt);
         for (int e = 0; e < n; ++e) {
           const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
           const uint32_t o = uint32_t((Ll + e) & int(P.kmask)) * uint32_t(P.Gp) + g;
-          at(P.log_term + cb, o) = Lt;
-          at(P.log_value + cb, o) = v;
+          uint32_t stamp = 0;
+          if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+          st<WT>(P.log_term + cb, o, Lt);
+          st<WT>(P.log_value + cb, o, v);
+          if constexpr (CRC) st<WT>(P.log_crc + cb, o, stamp);
 #pragma unroll
           for (int p = 0; p < R; ++p) {
             if (p == c || !((okm >> p) & 1u)) continue;
             const uint32_t op = uint32_t((last[p] - n + e) & int(P.kmask)) * uint32_t(P.Gp) + g;
             const uint64_t pb = uint64_t(p) * P.K * P.Gp;
-            at(P.log_term + pb, op) = Lt;
-            at(P.log_value + pb, op) = v;
+            st<WT>(P.log_term + pb, op, Lt);
+            st<WT>(P.log_value + pb, op, v);
+            if constexpr (CRC) st<WT>(P.log_crc + pb, op, stamp);
           }
         }
       }
@@ -347,7 +398,8 @@ __device__ __forceinline__ void with_replica(int x, F&& f) {
 
 template <int R>
 __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const DevOp* ops, uint32_t n,
-                                                  const int32_t* et, const int64_t* ev, DevRes* out) {
+                                                  const int32_t* et, const int64_t* ev, const uint32_t* ec,
+                                                  DevRes* out) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
   const DevOp op = ops[i];
@@ -362,7 +414,8 @@ __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const De
   G.load(P, true);
   const int x = int(op.replica);
   const int ro = G.role(x);
-  const TickSrc ring_only{P.log_term, P.log_value, P.Gp, G.g, P.K, P.kmask, 0, 1, -1, 0, 0, 0};
+  const TickSrc ring_only{P.log_term, P.log_value, P.log_crc, P.crc_tab, P.crc_on, P.Gp, G.g, P.K, P.kmask, 0, 1,
+                          -1, 0, 0, 0};
   auto make_src = [ring_only](int c) {
     TickSrc s = ring_only;
     s.leader = c;
@@ -370,8 +423,8 @@ __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const De
   };
   switch (op.kind) {
     case OP_AE: {
-      AEReq q{op.term, op.prev_idx, op.prev_term, op.lc, int(op.n)};
-      HostSrc src{et, ev, op.off, 0};
+      AEReq q{op.term, op.prev_idx, op.prev_term, op.lc, int(op.n), 0};
+      HostSrc src{et, ev, ec, op.off, 0};
       with_replica<R>(x, [&](auto PI) {
         constexpr int p = decltype(PI)::value;
         const AEResp a = G.template deliver_ae<p>(P, T, q, src);
@@ -486,11 +539,25 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
 
 static inline dim3 grid_for(uint64_t n) { return dim3(unsigned((n + 255) / 256)); }
 
+template <int R, bool WT, bool CRC>
+static void launch_fast_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                          int32_t* work_tick, uint32_t* work_count, int force_slow, hipStream_t s, hipEvent_t a,
+                          hipEvent_t b) {
+  hipExtLaunchKernelGGL(tick_fast_kernel<R, WT, CRC>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, work,
+                        work_tick, work_count, force_slow);
+}
 hipError_t launch_tick_fast(int R, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
-                            int32_t* work_tick, uint32_t* work_count, int force_slow, hipStream_t s,
+                            int32_t* work_tick, uint32_t* work_count, int force_slow, int write_through, hipStream_t s,
                             hipEvent_t ev_start, hipEvent_t ev_stop) {
-  RAFT_DISPATCH_R(R, hipExtLaunchKernelGGL(tick_fast_kernel<RR>, grid_for(P.G), dim3(256), 0, s, ev_start, ev_stop, 0,
-                                           P, T, stats, work, work_tick, work_count, force_slow));
+  const bool crc = P.crc_on != 0;
+#define RAFT_FAST(WT_, CRC_) \
+  RAFT_DISPATCH_R(R, (launch_fast_t<RR, WT_, CRC_>(P, T, stats, work, work_tick, work_count, force_slow, s, ev_start, ev_stop)))
+  if (write_through) {
+    if (crc) { RAFT_FAST(true, true); } else { RAFT_FAST(true, false); }
+  } else {
+    if (crc) { RAFT_FAST(false, true); } else { RAFT_FAST(false, false); }
+  }
+#undef RAFT_FAST
   return hipGetLastError();
 }
 hipError_t launch_tick_slow(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
@@ -502,8 +569,8 @@ hipError_t launch_tick_slow(int R, const DevPlanes& P, const Trace& T0, int64_t 
   return hipGetLastError();
 }
 hipError_t launch_ops(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
-                      const int32_t* et, const int64_t* ev, DevRes* out, hipStream_t s) {
-  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(ops_kernel<RR>, grid_for(n), dim3(256), 0, s, P, T, ops, n, et, ev, out));
+                      const int32_t* et, const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s) {
+  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(ops_kernel<RR>, grid_for(n), dim3(256), 0, s, P, T, ops, n, et, ev, ec, out));
   return hipGetLastError();
 }
 hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_t s) {

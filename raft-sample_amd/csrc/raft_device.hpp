@@ -26,7 +26,7 @@ enum : int {
   F_NONE = 0, F_PANIC_GETLOG = 1, F_DEADLOCK_VRES = 2, F_DEADLOCK_LEADER_VREQ = 3,
   F_RING_EVICTED = 4, F_OVERFLOW = 5
 };
-enum : uint32_t { ST_VALUE = 1, ST_TIMER_F = 2, ST_TIMER_C = 3, ST_ISOLATE = 4 };
+enum : uint32_t { ST_VALUE = 1, ST_TIMER_F = 2, ST_TIMER_C = 3, ST_ISOLATE = 4, ST_CORRUPT = 5 };
 enum : int {
   S_COMMITTED = 0, S_WON = 1, S_BUMPS = 2, S_AE_OK = 3, S_AE_FAIL = 4, S_VOTES = 5,
   S_FAULTS = 6, S_LEADER_GROUPS = 7, NSTAT = 8
@@ -56,6 +56,10 @@ struct DevPlanes {
   int32_t* lterm;      // [R][Gp] Log[len-1].Term: cached term of each replica's last entry
   int32_t* log_term;   // Log.Term  ring
   int64_t* log_value;  // Log.Value ring
+  uint32_t* log_crc;   // EXT: CRC32C stamp ring (payload_crc only)
+  const uint32_t* crc_tab;  // 8 x 256 slice-by-8 CRC32C tables
+  uint32_t crc_on;     // payload_crc
+  uint32_t corrupt_p;  // EXT corruption probability / 65536
   uint64_t Gp;         // plane pitch (groups, padded)
   uint64_t G;          // groups on this engine
   uint64_t gbase;      // global id of local group 0
@@ -109,6 +113,25 @@ __device__ __forceinline__ uint64_t rng_k(uint64_t key, uint32_t r, uint32_t str
   return sm64(sm64(key ^ ((uint64_t(stream) << 32) | r)) ^ tick);
 }
 
+// --------------------------------------------------------------- CRC32C --
+// EXT (config C5): CRC32C (Castagnoli, reflected) of an entry's payload =
+// Term (4 B LE) || Value (8 B LE), slice-by-4 then slice-by-8 over the
+// tables T[k][b] (T[0] = byte table, T[k][b] = T[k-1][b] >> 8 ^ T[0][T[k-1][b] & 255]),
+// which may live in global memory or in LDS. Same definition as
+// oracle_entry_crc() (bitwise reference, check value 0xE3069283).
+__device__ __forceinline__ uint32_t crc_term_state(const uint32_t* T, int term) {
+  const uint32_t c = 0xFFFFFFFFu ^ uint32_t(term);
+  return T[768 + (c & 255)] ^ T[512 + ((c >> 8) & 255)] ^ T[256 + ((c >> 16) & 255)] ^ T[c >> 24];
+}
+__device__ __forceinline__ uint32_t crc_value_final(const uint32_t* T, uint32_t c, int64_t value) {
+  const uint32_t lo = c ^ uint32_t(uint64_t(value)), hi = uint32_t(uint64_t(value) >> 32);
+  return ~(T[1792 + (lo & 255)] ^ T[1536 + ((lo >> 8) & 255)] ^ T[1280 + ((lo >> 16) & 255)] ^ T[1024 + (lo >> 24)] ^
+           T[768 + (hi & 255)] ^ T[512 + ((hi >> 8) & 255)] ^ T[256 + ((hi >> 16) & 255)] ^ T[hi >> 24]);
+}
+__device__ __forceinline__ uint32_t crc_entry(const uint32_t* T, int term, int64_t value) {
+  return crc_value_final(T, crc_term_state(T, term), value);
+}
+
 // ------------------------------------------------- register-array helpers --
 // Runtime-indexed access to a register array without letting LLVM fold the
 // select chain into a dynamic GEP (which would demote the whole Group to
@@ -137,6 +160,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 struct AEReq {          // AppendEntriesRequest (main.go:289-296), LeaderId implicit
   int term, prev_idx, prev_term, lc;
   int n;                // len(Logs)
+  int corrupt;          // EXT: the last entry arrives with Value bit 0 flipped
 };
 struct AEResp { int term, match, ok; };  // AppendEntriesResponse (main.go:298-302)
 
@@ -248,6 +272,14 @@ struct Group {
   __device__ __forceinline__ int64_t& ring_value(const DevPlanes& P, int r, int idx) const {
     return at(P.log_value + uint64_t(r) * P.K * P.Gp, ring_off(P, idx));
   }
+  __device__ __forceinline__ uint32_t& ring_crc(const DevPlanes& P, int r, int idx) const {
+    return at(P.log_crc + uint64_t(r) * P.K * P.Gp, ring_off(P, idx));
+  }
+  // EXT: is the AppendEntries delivered to replica p this tick corrupted?
+  __device__ __forceinline__ int corrupted(const DevPlanes& P, int p) const {
+    if (!P.crc_on || !P.corrupt_p) return 0;
+    return (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(tick)) & 0xFFFF) < P.corrupt_p;
+  }
   // Timer of replica r (lazy: only read from HBM when a timeout check needs it).
   template <int Rp>
   __device__ __forceinline__ int deadline_of(const DevPlanes& P) {
@@ -312,12 +344,21 @@ struct Group {
     // 148-149: append all Logs at the end (no truncation); only the last K
     // positions are kept in the ring.
     const int j0 = q.n > int(P.K) ? q.n - int(P.K) : 0;
+    if (P.crc_on) {   // EXT: verify the payload that will be stored; a bad entry rejects the request
+      for (int j = j0; j < q.n; ++j) {
+        int t; int64_t v; uint32_t c;
+        src.fetch(j, t, v, c);
+        if (q.corrupt && j == q.n - 1) v ^= 1;
+        if (crc_entry(P.crc_tab, t, v) != c) return res;
+      }
+    }
     int tl = 0;
     for (int j = j0; j < q.n; ++j) {
-      int64_t v;
-      src.fetch(j, tl, v);
+      int64_t v; uint32_t c;
+      src.fetch(j, tl, v, c);
       ring_term(P, Rp, l + 1 + j) = tl;
       ring_value(P, Rp, l + 1 + j) = v;
+      if (P.crc_on) ring_crc(P, Rp, l + 1 + j) = c;
     }
     const int nl = l + q.n;
     if (q.n) {
@@ -484,6 +525,7 @@ struct Group {
       if (dropped(c, p)) { ++st[S_AE_FAIL]; return; }
       AEReq q;
       q.term = lt; q.lc = lc;
+      q.corrupt = corrupted(P, p);
       const int nxt = m[p] + 1;                               // NextIndex == MatchIndex + 1
       int from = 1;
       if (nxt <= ll) {                                        // 341
@@ -523,6 +565,7 @@ struct Group {
     const int t = sel(term, c);
     ring_term(P, c, l + 1) = t;
     ring_value(P, c, l + 1) = v;
+    if (P.crc_on) ring_crc(P, c, l + 1) = crc_entry(P.crc_tab, t, v);
     at(P.lterm + uint64_t(c) * P.Gp, g) = t;
     put(last, c, l + 1);
     d_last |= 1u << c;
@@ -546,34 +589,43 @@ struct Group {
 struct TickSrc {
   const int32_t* lt;
   const int64_t* lv;
+  const uint32_t* lc;
+  const uint32_t* tab;
+  uint32_t crc_on;
   uint64_t Gp;
   uint32_t g, K, kmask;
   int leader, from;
   int cache_leader, cache_from, cache_term;
   uint64_t cache_vbase;
-  __device__ __forceinline__ void fetch(int j, int& t, int64_t& v) const {
+  __device__ __forceinline__ void fetch(int j, int& t, int64_t& v, uint32_t& c) const {
     const int idx = from + j;
+    c = 0;
     if (leader == cache_leader && idx >= cache_from) {
       t = cache_term;
       v = int64_t(sm64(cache_vbase ^ uint64_t(uint32_t(idx - cache_from))) >> 1);
+      if (crc_on) c = crc_entry(tab, t, v);   // the leader's stamp of its own fresh entry
     } else {
       const uint64_t rb = uint64_t(leader) * K * Gp;
       const uint32_t o = uint32_t((idx - 1) & int(kmask)) * uint32_t(Gp) + g;
       t = at(lt + rb, o);
       v = at(lv + rb, o);
+      if (crc_on) c = at(lc + rb, o);
     }
   }
 };
 
-// Entry source of a host-supplied AppendEntriesRequest (handler batch API).
+// Entry source of a host-supplied AppendEntriesRequest (handler batch API);
+// host payloads are stamped on ingest.
 struct HostSrc {
   const int32_t* et;
   const int64_t* ev;
+  const uint32_t* ec;
   uint64_t off;
   int from;
-  __device__ __forceinline__ void fetch(int j, int& t, int64_t& v) const {
+  __device__ __forceinline__ void fetch(int j, int& t, int64_t& v, uint32_t& c) const {
     t = et[off + uint64_t(j)];
     v = ev[off + uint64_t(j)];
+    c = ec[off + uint64_t(j)];
   }
 };
 

@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-RAFT_ABI_VERSION = 1
+RAFT_ABI_VERSION = 2
 RAFT_MAX_REPLICAS = 8
 
 FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
@@ -38,7 +38,8 @@ class Config(C.Structure):
         ("isolate_per_65536", C.c_uint32), ("isolate_min_ticks", C.c_uint32),
         ("isolate_max_ticks", C.c_uint32),
         ("device", C.c_int32),
-        ("reserved", C.c_uint32 * 8),
+        ("payload_crc", C.c_uint32), ("corrupt_per_65536", C.c_uint32),
+        ("reserved", C.c_uint32 * 6),
     ]
 
 
@@ -59,6 +60,8 @@ def default_config(**kw):
     c.isolate_per_65536 = 0
     c.isolate_min_ticks, c.isolate_max_ticks = 8, 32
     c.device = 0
+    c.payload_crc = 0
+    c.corrupt_per_65536 = 0
     for k, v in kw.items():
         if not hasattr(c, k):
             raise TypeError(f"unknown config field {k!r}")
@@ -75,12 +78,12 @@ class StateView(C.Structure):
         ("role", C.c_void_p), ("voted", C.c_void_p), ("term", C.c_void_p),
         ("last", C.c_void_p), ("commit", C.c_void_p), ("deadline", C.c_void_p),
         ("timeout", C.c_void_p), ("match", C.c_void_p), ("fault", C.c_void_p),
-        ("log_term", C.c_void_p), ("log_value", C.c_void_p),
+        ("log_term", C.c_void_p), ("log_value", C.c_void_p), ("log_crc", C.c_void_p),
     ]
 
 
 STATE_FIELDS = ("role", "voted", "term", "last", "commit", "deadline", "timeout",
-                "match", "fault", "log_term", "log_value")
+                "match", "fault", "log_term", "log_value", "log_crc")
 
 
 def state_shapes(groups, replicas, ring_depth):
@@ -91,7 +94,7 @@ def state_shapes(groups, replicas, ring_depth):
         "commit": ((G, R), np.int32), "deadline": ((G, R), np.int32),
         "timeout": ((G, R), np.int32), "match": ((G, R, R), np.int32),
         "fault": ((G,), np.uint8), "log_term": ((G, R, K), np.int32),
-        "log_value": ((G, R, K), np.int64),
+        "log_value": ((G, R, K), np.int64), "log_crc": ((G, R, K), np.uint32),
     }
 
 

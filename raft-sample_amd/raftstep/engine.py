@@ -96,8 +96,8 @@ class Engine:
     def store_state(self, logs=True):
         st = abi.empty_state(self.cfg.groups, self.cfg.replicas, self.cfg.ring_depth)
         if not logs:
-            st.pop("log_term")
-            st.pop("log_value")
+            for k in ("log_term", "log_value", "log_crc"):
+                st.pop(k)
         v = abi.make_view(st)
         _check(self.lib.raft_store_state(self.h, C.byref(v)))
         return st
@@ -160,8 +160,9 @@ class Engine:
         return np.array(s.v, dtype=np.int64)
 
     # -- instrumentation -----------------------------------------------
-    def profile(self, enable=True):
-        _check(self.lib.raft_profile_enable(self.h, 1 if enable else 0))
+    def profile(self, mode=1):
+        """0 off, 1 per-dispatch kernel events, 2 one event pair per tick() call."""
+        _check(self.lib.raft_profile_enable(self.h, int(mode)))
 
     def profile_read(self):
         ms, n = C.c_double(), C.c_uint64()

@@ -31,7 +31,8 @@ TRACES = {
     "c2_r5_steady": dict(cfg=dict(replicas=5, groups=64, client_period=1, ring_depth=16, seed=0x5EED0002),
                          init="steady-1", ticks=128, every=8),
     "c5_r5_e64": dict(cfg=dict(replicas=5, groups=16, client_period=1, entries_per_tick=64, ring_depth=128,
-                               seed=0x5EED0005), init="steady0", ticks=12, every=1),
+                               seed=0x5EED0005, payload_crc=1, corrupt_per_65536=4000), init="steady0",
+                      ticks=12, every=1),
 }
 
 RNG_INPUTS = [(0x5EED0001, 0, 0, 1, 0), (0x5EED0002, 1048575, 4, 2, 17), (1, 2**40 + 5, 7, 3, 2**33),

@@ -87,13 +87,14 @@ def state_hash(st):
 
 
 def group_hashes(st):
-    """Per-group digest (uint64) of every field — for per-tick trace diffs."""
+    """Per-group digest (uint64) of every field — for per-tick trace diffs
+    (log_crc only when present and non-zero, i.e. with payload_crc on)."""
     G = st["fault"].shape[0]
     acc = np.zeros(G, dtype=np.uint64)
     mult = np.uint64(0x100000001B3)
     with np.errstate(over="ignore"):
         for k in abi.STATE_FIELDS:
-            if k not in st:
+            if k not in st or (k == "log_crc" and not st[k].any()):
                 continue
             a = np.ascontiguousarray(st[k]).reshape(G, -1).astype(np.int64).view(np.uint64)
             for j in range(a.shape[1]):
@@ -141,6 +142,34 @@ def ops(items):
         o[i]["kind"] = it["kind"]
         o[i]["arg"] = it.get("arg", 0)
     return o
+
+
+def crc32c(data):
+    """Bitwise CRC32C (Castagnoli, reflected 0x82F63B78) — independent of both implementations."""
+    c = 0xFFFFFFFF
+    for b in data:
+        c ^= b
+        for _ in range(8):
+            c = (c >> 1) ^ (0x82F63B78 & -(c & 1))
+    return c ^ 0xFFFFFFFF
+
+
+def entry_crc(term, value):
+    """EXT stamp of a log entry: CRC32C(Term as 4 B LE || Value as 8 B LE)."""
+    return crc32c((int(term) & 0xFFFFFFFF).to_bytes(4, "little") + (int(value) & (2**64 - 1)).to_bytes(8, "little"))
+
+
+def stamp_crcs(st):
+    """Fill log_crc with the stamps of the visible ring entries."""
+    G, R, K = st["log_term"].shape
+    st["log_crc"][:] = 0
+    for g in range(G):
+        for r in range(R):
+            last = int(st["last"][g, r])
+            for i in range(max(1, last - K + 1), last + 1):
+                s = (i - 1) % K
+                st["log_crc"][g, r, s] = entry_crc(int(st["log_term"][g, r, s]), int(st["log_value"][g, r, s]))
+    return st
 
 
 def random_state(rng, G, R, K, max_term=6, max_log=12):

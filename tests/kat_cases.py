@@ -8,6 +8,7 @@ implementation; each case cites the lines it exercises.
 """
 import numpy as np
 
+import harness
 from harness import C, F, L, ae_reqs, build_state, log_of, node, ops, vote_reqs
 from raftstep import abi
 
@@ -345,8 +346,28 @@ def kat22_tick_steady(make):
         assert stats[abi.STAT_NAMES.index(k)] == 0, k
 
 
+def kat23_crc_reject(make):
+    """EXT (config C5): with payload CRC32C on, a follower whose copy of the
+    last entry arrives with a flipped bit rejects the whole AppendEntries
+    (nothing appended; its timer was already reset, main.go:124-127); the
+    leader's MatchIndex does not move (main.go:375) and nothing commits."""
+    e = _impl(make, 3, K=16, payload_crc=1, corrupt_per_65536=65536, client_period=1)
+    e.init_steady(0, 0)
+    s = e.tick(1, 3)
+    st = e.store_state()
+    assert list(st["last"][0]) == [3, 0, 0] and list(st["commit"][0]) == [0, 0, 0]
+    assert s[abi.STAT_NAMES.index("ae_fail")] == 6 and s[abi.STAT_NAMES.index("ae_ok")] == 0
+    assert st["log_crc"][0, 0, 0] == harness.entry_crc(1, st["log_value"][0, 0, 0])
+    e2 = _impl(make, 3, K=16, payload_crc=1, corrupt_per_65536=0, client_period=1)
+    e2.init_steady(0, 0)
+    e2.tick(1, 3)
+    st2 = e2.store_state()
+    assert list(st2["last"][0]) == [3, 3, 3] and list(st2["commit"][0]) == [3, 2, 2]
+    assert (st2["log_crc"][0, :, :3] == st2["log_crc"][0, 0, :3]).all()
+
+
 ALL = [kat01_election, kat02_heartbeat_empty, kat03_first_entry, kat04_commit_propagates, kat05_suffix,
        kat06_commit_plus_one, kat07_10_commit_rule, kat11_panic_getlog, kat12_stale_term,
        kat13_candidate_steps_down, kat14_leader_steps_down, kat15_sticky_vote, kat16_prev_term_mismatch,
        kat17_deadlocks, kat18_edge_replicas, kat19_role_checks, kat20_ext_limits, kat21_tick_election,
-       kat22_tick_steady]
+       kat22_tick_steady, kat23_crc_reject]

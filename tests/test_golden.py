@@ -33,6 +33,19 @@ def test_rng_vectors(oracle_mod):
         assert o.rng(v["gid"], v["replica"], v["stream"], v["tick"]) == v["rng"]
 
 
+def test_crc32c_check_value(oracle_mod):
+    """CRC32C (Castagnoli) standard check value (RFC 3720 / iSCSI), and the
+    entry stamp against an independent Python restatement."""
+    import random
+
+    import harness
+    assert oracle_mod.crc32c(b"123456789") == 0xE3069283 == harness.crc32c(b"123456789")
+    rnd = random.Random(5)
+    for _ in range(200):
+        t, v = rnd.randrange(-2**31, 2**31), rnd.randrange(-2**63, 2**63)
+        assert oracle_mod.entry_crc(t, v) == harness.entry_crc(t, v)
+
+
 def test_timer_draw_ranges(oracle_mod):
     """rand.Intn(20)+10 (main.go:114) and rand.Intn(4)+10 (main.go:194)."""
     o = oracle_mod.Oracle(seed=7)

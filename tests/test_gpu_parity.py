@@ -33,12 +33,14 @@ def compare(e, o, what):
     H.assert_same_state(e.store_state(), o.store_state(), what)
 
 
-@pytest.mark.parametrize("R", [1, 2, 3, 4, 5, 6, 7, 8])
-def test_handler_batches_random_states(R):
-    rng = np.random.default_rng(1000 + R)
+@pytest.mark.parametrize("R,crc", [(1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (3, 1), (5, 1)])
+def test_handler_batches_random_states(R, crc):
+    rng = np.random.default_rng(1000 + R + 50 * crc)
     G, K = 192, 8
-    e, o = pair(replicas=R, groups=G, ring_depth=K, seed=0xABC + R)
+    e, o = pair(replicas=R, groups=G, ring_depth=K, seed=0xABC + R, payload_crc=crc)
     st = H.random_state(rng, G, R, K)
+    if crc:
+        H.stamp_crcs(st)
     e.load_state(st)
     o.load_state(st)
     compare(e, o, "after load")
@@ -85,6 +87,11 @@ TRACES = {
                           seed=0x78), "steady-1", 1, 30, 3),
     "steady_heartbeats": (dict(replicas=3, groups=260, client_period=4, entries_per_tick=2, ring_depth=8,
                                seed=0x79), "steady0", 1, 40, 1),
+    "c5_crc_corrupt": (dict(replicas=5, groups=200, client_period=1, entries_per_tick=64, ring_depth=128,
+                            payload_crc=1, corrupt_per_65536=3000, seed=0x5EED0005), "steady0", 1, 16, 2),
+    "crc_newnode_iso": (dict(replicas=3, groups=300, client_period=1, entries_per_tick=2, ring_depth=16,
+                             payload_crc=1, corrupt_per_65536=5000, isolate_per_65536=12000,
+                             seed=0xC5C), "new", 0, 150, 5),
     "r1": (dict(replicas=1, groups=64, client_period=1, seed=1), "new", 0, 60, 5),
     "r2": (dict(replicas=2, groups=64, client_period=1, seed=2), "new", 0, 60, 5),
     "r4": (dict(replicas=4, groups=300, client_period=1, seed=4), "new", 0, 120, 5),
@@ -119,12 +126,15 @@ def test_tick_trace(name, path):
 def test_tick_from_random_states():
     """Random (well-formed) states exercise multi-leader groups, stale
     candidates, deadlocks and panics inside the fused tick."""
-    for R in (3, 5, 7):
-        rng = np.random.default_rng(77 + R)
+    for R, crc in ((3, 0), (5, 0), (7, 0), (5, 1)):
+        rng = np.random.default_rng(77 + R + crc)
         G, K = 512, 16
-        kw = dict(replicas=R, groups=G, ring_depth=K, client_period=2, seed=900 + R, isolate_per_65536=8000)
+        kw = dict(replicas=R, groups=G, ring_depth=K, client_period=2, seed=900 + R, isolate_per_65536=8000,
+                  payload_crc=crc, corrupt_per_65536=6000 * crc)
         e, o = pair(**kw)
         st = H.random_state(rng, G, R, K)
+        if crc:
+            H.stamp_crcs(st)
         e.load_state(st)
         o.load_state(st)
         for t in range(30, 60):
