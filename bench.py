@@ -53,7 +53,7 @@ def cpu_baseline(args, R, E, K, crc):
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     G, T = args.cpu_groups, args.cpu_ticks
     if E > 1:   # keep the sample's CPU time and memory bounded for big batches
-        G, T = max(1024, G // E), max(16, T // 4)
+        G, T = max(1024, 4 * G // E), max(16, T // 4)
     o = oracle.Oracle(replicas=R, groups=G, ring_depth=K, client_period=1, entries_per_tick=E,
                       payload_crc=crc, seed=0x5EED0002)
     o.init_steady(0, 0)
