@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RAFT_ABI_VERSION 2u
+#define RAFT_ABI_VERSION 3u
 #define RAFT_MAX_REPLICAS 8u
 
 /* Node.State (main.go:51-57). */
@@ -49,7 +49,11 @@ enum raft_fault {
   RAFT_F_OVERFLOW = 5             /* EXT: a term/index would leave int32 (Go int is 64-bit) */
 };
 
-enum raft_semantics { RAFT_SEM_REF = 0 };
+/* REF = main.go bit for bit (the drop-in). RAFT = EXT mode with the
+ * Raft-paper rules (votedFor, up-to-date check, truncate-on-conflict,
+ * nextIndex backoff, majority commit with the current-term rule) on the same
+ * tick model and layout, for churn workloads where REF faults (config C4). */
+enum raft_semantics { RAFT_SEM_REF = 0, RAFT_SEM_RAFT = 1 };
 
 /* Error codes (negative returns). */
 #define RAFT_OK 0
@@ -86,7 +90,7 @@ typedef struct raft_config {
   uint32_t ring_depth;         /* K: log entries kept per replica, power of two */
   uint32_t entries_per_tick;   /* E: client entries appended per client event (main.go:92) */
   uint32_t client_period;      /* ticks between client events; 0 = no client */
-  uint32_t semantics;          /* RAFT_SEM_REF */
+  uint32_t semantics;          /* enum raft_semantics */
   uint64_t seed;               /* trace seed (splitmix64 counter RNG) */
   int32_t tick_seconds;        /* 2 (main.go:394) */
   int32_t follower_timeout_min;   /* 10 s  (main.go:114: rand.Intn(20)+10) */
@@ -105,12 +109,12 @@ typedef struct raft_config {
 /* Canonical host view of engine state, group-major:
  *   per-replica arrays are indexed [g*R + r], match is [(g*R + leader)*R + peer],
  *   log arrays are [(g*R + r)*K + slot] where log index i (1-based) lives at
- *   slot (i-1) mod K and only i in (max(0,last-K), last] is meaningful (other
+ *   slot (i-1) mod K and only i in (max(0,hwm-K), last] is meaningful (other
  *   slots read back as 0). match rows of replicas that are not leaders read
  *   back as 0. Any pointer may be NULL on store (field skipped). */
 typedef struct raft_state_view {
   uint8_t* role;      /* Node.State (main.go:16) */
-  uint8_t* voted;     /* Node.Voted (main.go:20) */
+  uint8_t* voted;     /* REF: Node.Voted (main.go:20); RAFT: votedFor + 1 (0 = none) */
   int32_t* term;      /* Node.Term (main.go:19) */
   int32_t* last;      /* Node.LastApplied == len(Node.Log) (main.go:25, 148-149, 328-329) */
   int32_t* commit;    /* Node.CommitIndex (main.go:24) */
@@ -121,6 +125,10 @@ typedef struct raft_state_view {
   int32_t* log_term;  /* Log.Term (main.go:47) */
   int64_t* log_value; /* Log.Value (main.go:48) */
   uint32_t* log_crc;  /* EXT: CRC32C of each ring entry (0 when payload_crc is off) */
+  int32_t* next;      /* Node.NextIndex [(g*R + leader)*R + peer] (REF: match+1); 0 for non-leaders.
+                         Optional on load: absent or 0 derives match+1 (REF ignores it) */
+  int32_t* hwm;       /* [g*R + r] highest LastApplied ever (== last in REF); the ring holds (hwm-K, last].
+                         Optional on load: absent or < last means last (REF ignores it) */
 } raft_state_view;
 
 typedef struct raft_engine raft_engine;

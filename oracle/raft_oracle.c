@@ -103,7 +103,9 @@ typedef struct {                                 /* Node (main.go:14-39) */
   int64_t last;                                  /* LastApplied == len(Log) */
   int64_t commit;                                /* CommitIndex */
   int64_t deadline, timeout;                     /* timer (virtual seconds) */
-  int64_t match[RAFT_MAX_REPLICAS];              /* MatchIndex; NextIndex = match+1 */
+  int64_t match[RAFT_MAX_REPLICAS];              /* MatchIndex; REF: NextIndex = match+1 */
+  int64_t next[RAFT_MAX_REPLICAS];               /* NextIndex (RAFT mode only; REF derives it) */
+  int64_t hwm;                                   /* highest LastApplied ever (ring window; == last in REF) */
   o_ent* log;
   int64_t cap;
 } o_node;
@@ -149,13 +151,15 @@ static void log_append(o_node* n, const o_ent* src, int64_t cnt) {
   }
   memmove(n->log + n->last, src, (size_t)cnt * sizeof(o_ent));
   n->last += cnt;
+  if (n->last > n->hwm) n->hwm = n->last;
 }
 
 /* GetLog(i) = Log[i-1] (main.go:403-405): panics outside [1, len]; the
- * EXT ring-depth rule makes entries at or below last-K unreadable. */
+ * EXT ring-depth rule makes entries at or below hwm-K unreadable (hwm is
+ * the highest length the log ever had; == last without truncation). */
 static int get_log_term(const o_ctx* c, o_group* G, const o_node* n, int64_t i, int64_t* out) {
   if (i < 1 || i > n->last) { set_fault(G, RAFT_F_PANIC_GETLOG); return 0; }
-  if (i <= n->last - (int64_t)c->cfg->ring_depth) { set_fault(G, RAFT_F_RING_EVICTED); return 0; }
+  if (i <= n->hwm - (int64_t)c->cfg->ring_depth) { set_fault(G, RAFT_F_RING_EVICTED); return 0; }
   *out = n->log[i - 1].term;
   return 1;
 }
@@ -368,6 +372,183 @@ static void client_append(const o_ctx* c, o_group* G, int L, int64_t value) {
   log_append(n, &e, 1);
 }
 
+
+/* ======================================================================
+ * RAFT-paper semantics (EXT mode RAFT_SEM_RAFT; Ongaro & Ousterhout,
+ * "In Search of an Understandable Consensus Algorithm", Figure 2) on the
+ * same tick model, for churn workloads where the
+ * reference's own semantics fault. Divergences from main.go, by line:
+ * votedFor instead of the sticky bool (20, 160); up-to-date check (185-186,
+ * 264); consistency check + truncate-on-conflict (135-149); nextIndex
+ * backoff (376-377); majority order statistic with the current-term rule
+ * (382-391); commit = min(LC, last new entry) (152); any higher term steps
+ * down (265-268, 373-378). voted holds votedFor (-1 = none).
+ * ==================================================================== */
+static int64_t last_term_of(const o_node* n) { return n->last ? n->log[n->last - 1].term : 0; }
+
+/* Figure 2, all servers: a higher term in any RPC -> adopt it, forget the
+ * vote, and (if not already) become a follower. */
+static void r_observe_term(const o_ctx* c, o_group* G, int x, int64_t t) {
+  o_node* n = &G->n[x];
+  if (t <= n->term) return;
+  n->term = t;
+  n->voted = -1;
+  if (n->role != RAFT_FOLLOWER) {
+    enter_follower(c, n, x);
+    memset(n->match, 0, sizeof n->match);
+    memset(n->next, 0, sizeof n->next);
+  }
+}
+
+static int r_deliver_vr(const o_ctx* c, o_group* G, int x, int64_t term, int cand, int64_t llast,
+                        int64_t llterm, int64_t* resp_term) {
+  o_node* n = &G->n[x];
+  r_observe_term(c, G, x, term);
+  *resp_term = n->term;
+  if (term < n->term) return 0;
+  int64_t mt = last_term_of(n);
+  int uptodate = llterm > mt || (llterm == mt && llast >= n->last);
+  if ((n->voted < 0 || n->voted == cand) && uptodate) {
+    n->voted = cand;
+    n->deadline = c->now + n->timeout;     /* granting a vote resets the election timer */
+    return 1;
+  }
+  return 0;
+}
+
+/* On failure res.match is the hint H: the leader retries from min(next-1, H+1). */
+static o_aer r_deliver_ae(const o_ctx* c, o_group* G, int x, const o_ae* r) {
+  o_node* n = &G->n[x];
+  r_observe_term(c, G, x, r->term);
+  o_aer res = {n->term, n->last, 0};
+  if (r->term < n->term) return res;
+  if (n->role == RAFT_LEADER) return res;          /* same-term second leader: cannot happen (election safety) */
+  if (n->role == RAFT_CANDIDATE) {                 /* a current leader exists: step down */
+    enter_follower(c, n, x);
+    memset(n->match, 0, sizeof n->match);
+    memset(n->next, 0, sizeof n->next);
+  }
+  n->deadline = c->now + n->timeout;               /* AppendEntries from the current leader resets the timer */
+  if (r->prev_idx > n->last) return res;           /* log too short: hint = last */
+  if (r->prev_idx > 0) {
+    int64_t t;
+    if (!get_log_term(c, G, n, r->prev_idx, &t)) return res;
+    if (t != r->prev_term) { res.match = r->prev_idx - 1; return res; }
+  }
+  if (c->cfg->payload_crc) {                       /* EXT: verify what will be stored */
+    int64_t j0 = r->n > (int64_t)c->cfg->ring_depth ? r->n - (int64_t)c->cfg->ring_depth : 0;
+    for (int64_t j = j0; j < r->n; ++j) {
+      int64_t v = r->ents[j].value ^ ((r->corrupt && j == r->n - 1) ? 1 : 0);
+      if (oracle_entry_crc(r->ents[j].term, v) != r->ents[j].crc) { res.match = r->prev_idx; return res; }
+    }
+  }
+  if (r->prev_idx + r->n > I32MAX) { set_fault(G, RAFT_F_OVERFLOW); return res; }
+  /* skip entries already present, truncate at the first conflict, append the rest */
+  int64_t j = 0;
+  for (; j < r->n; ++j) {
+    int64_t idx = r->prev_idx + 1 + j;
+    if (idx > n->last) break;
+    int64_t t;
+    if (!get_log_term(c, G, n, idx, &t)) return res;
+    if (t != r->ents[j].term) { n->last = idx - 1; break; }
+  }
+  log_append(n, r->ents + j, r->n - j);
+  int64_t last_new = r->prev_idx + r->n;
+  if (r->lc > n->commit) n->commit = r->lc < last_new ? r->lc : last_new;
+  res.term = n->term; res.match = last_new; res.ok = 1;
+  return res;
+}
+
+static int r_candidate_round(o_ctx* c, o_group* G, int cand) {
+  const int R = (int)c->cfg->replicas;
+  o_node* n = &G->n[cand];
+  int count = 1;                                   /* its own vote (votedFor = self since the timeout) */
+  for (int p = 0; p < R; ++p) {
+    if (p == cand) continue;
+    if (n->role != RAFT_CANDIDATE) return 0;
+    if (dropped(c, cand, p)) continue;
+    int64_t rt;
+    int grant = r_deliver_vr(c, G, p, n->term, cand, n->last, last_term_of(n), &rt);
+    if (G->fault) return 0;
+    if (rt > n->term) { r_observe_term(c, G, cand, rt); return 0; }
+    if (grant) { count++; c->st[RAFT_STAT_VOTES_GRANTED]++; }
+  }
+  if (n->role == RAFT_CANDIDATE && 2 * count > R) {
+    n->role = RAFT_LEADER;
+    for (int p = 0; p < R; ++p) { n->match[p] = 0; n->next[p] = n->last + 1; }
+    c->st[RAFT_STAT_ELECTIONS_WON]++;
+    return 1;
+  }
+  return 0;
+}
+
+/* commitIndex = the largest N replicated on a majority (leader included),
+ * only if log[N].term == currentTerm. */
+static void r_leader_commit(o_ctx* c, o_group* G, int L) {
+  const int R = (int)c->cfg->replicas;
+  o_node* n = &G->n[L];
+  int64_t v[RAFT_MAX_REPLICAS];
+  for (int p = 0; p < R; ++p) v[p] = p == L ? n->last : n->match[p];
+  for (int i = 1; i < R; ++i)                      /* insertion sort, descending */
+    for (int k = i; k > 0 && v[k] > v[k - 1]; --k) { int64_t t = v[k]; v[k] = v[k - 1]; v[k - 1] = t; }
+  int64_t N = v[R / 2];
+  if (N > n->commit) {
+    int64_t t;
+    if (!get_log_term(c, G, n, N, &t)) return;
+    if (t == n->term) {
+      c->st[RAFT_STAT_COMMITTED] += N - n->commit;
+      n->commit = N;
+    }
+  }
+}
+
+static void r_leader_round(o_ctx* c, o_group* G, int L) {
+  const int R = (int)c->cfg->replicas;
+  o_node* n = &G->n[L];
+  for (int p = 0; p < R; ++p) {
+    if (p == L) continue;
+    if (n->role != RAFT_LEADER) return;
+    if (dropped(c, L, p)) { c->st[RAFT_STAT_AE_FAIL]++; continue; }
+    o_ae r;
+    r.term = n->term; r.lc = n->commit;
+    r.corrupt = oracle_corrupted(c->cfg, c->gid, (uint32_t)p, c->tick);
+    int64_t nxt = n->next[p];
+    if (nxt < 1 || nxt > n->last + 1) { set_fault(G, RAFT_F_PANIC_GETLOG); return; }
+    if (nxt <= n->hwm - (int64_t)c->cfg->ring_depth) { set_fault(G, RAFT_F_RING_EVICTED); return; }
+    r.prev_idx = nxt - 1;
+    r.prev_term = 0;
+    if (r.prev_idx > 0 && !get_log_term(c, G, n, r.prev_idx, &r.prev_term)) return;
+    r.ents = n->log + (nxt - 1);
+    r.n = n->last - nxt + 1;
+    o_aer res = r_deliver_ae(c, G, p, &r);
+    if (G->fault) return;
+    if (res.term > n->term) { r_observe_term(c, G, L, res.term); c->st[RAFT_STAT_AE_FAIL]++; return; }
+    if (res.ok) {
+      n->match[p] = res.match;
+      n->next[p] = res.match + 1;
+      c->st[RAFT_STAT_AE_OK]++;
+    } else {
+      int64_t nn = n->next[p] - 1 < res.match + 1 ? n->next[p] - 1 : res.match + 1;
+      n->next[p] = nn < 1 ? 1 : nn;
+      c->st[RAFT_STAT_AE_FAIL]++;
+    }
+  }
+  r_leader_commit(c, G, L);
+}
+
+static void r_timeout_fire(o_ctx* c, o_group* G, int x) {
+  o_node* n = &G->n[x];
+  if (n->term >= I32MAX) { set_fault(G, RAFT_F_OVERFLOW); return; }
+  n->term++;
+  n->voted = x;                                    /* votes for itself */
+  c->st[RAFT_STAT_TERM_BUMPS]++;
+  enter_candidate(c, n, x);
+  memset(n->match, 0, sizeof n->match);
+  memset(n->next, 0, sizeof n->next);
+}
+
+static int is_raft(const o_ctx* c) { return c->cfg->semantics == RAFT_SEM_RAFT; }
+
 /* One tick of one group. */
 static void tick_group(o_ctx* c, o_group* G) {
   const int R = (int)c->cfg->replicas;
@@ -382,8 +563,8 @@ static void tick_group(o_ctx* c, o_group* G) {
   }
   /* 2. rounds, ascending replica id */
   for (int r = 0; r < R && !G->fault; ++r) {
-    if (G->n[r].role == RAFT_LEADER) leader_round(c, G, r);
-    else if (G->n[r].role == RAFT_CANDIDATE) candidate_round(c, G, r);
+    if (G->n[r].role == RAFT_LEADER) { if (is_raft(c)) r_leader_round(c, G, r); else leader_round(c, G, r); }
+    else if (G->n[r].role == RAFT_CANDIDATE) { if (is_raft(c)) r_candidate_round(c, G, r); else candidate_round(c, G, r); }
   }
   /* 3. expired timers in (deadline, id) order; a new candidate runs its
    *    vote round at once (CandidateRun's default branch). */
@@ -395,9 +576,9 @@ static void tick_group(o_ctx* c, o_group* G) {
       if (best < 0 || n->deadline < G->n[best].deadline) best = r;
     }
     if (best < 0) break;
-    timeout_fire(c, G, best);
+    if (is_raft(c)) r_timeout_fire(c, G, best); else timeout_fire(c, G, best);
     if (G->fault) break;
-    candidate_round(c, G, best);
+    if (is_raft(c)) r_candidate_round(c, G, best); else candidate_round(c, G, best);
   }
   if (G->fault) { c->st[RAFT_STAT_FAULTS]++; return; }
   for (int r = 0; r < R; ++r)
@@ -406,7 +587,7 @@ static void tick_group(o_ctx* c, o_group* G) {
 
 /* ------------------------------------------------------------- API ----- */
 oracle* oracle_create(const raft_config* cfg) {
-  if (!cfg || cfg->replicas < 1 || cfg->replicas > RAFT_MAX_REPLICAS) return NULL;
+  if (!cfg || cfg->replicas < 1 || cfg->replicas > RAFT_MAX_REPLICAS || cfg->semantics > RAFT_SEM_RAFT) return NULL;
   oracle* o = (oracle*)calloc(1, sizeof *o);
   o->cfg = *cfg;
   o->g = (o_group*)calloc(cfg->groups ? cfg->groups : 1, sizeof(o_group));
@@ -445,7 +626,10 @@ void oracle_init_new_nodes(oracle* o, int64_t tick0) {
   for (uint64_t g = 0; g < o->cfg.groups; ++g) {
     o_ctx c = make_ctx(o, g, tick0);
     memset(&o->g[g], 0, sizeof(o_group));
-    for (uint32_t r = 0; r < o->cfg.replicas; ++r) enter_follower(&c, &o->g[g].n[r], (int)r);
+    for (uint32_t r = 0; r < o->cfg.replicas; ++r) {
+      enter_follower(&c, &o->g[g].n[r], (int)r);
+      o->g[g].n[r].voted = o->cfg.semantics == RAFT_SEM_RAFT ? -1 : 0;
+    }
   }
 }
 
@@ -464,9 +648,15 @@ void oracle_init_steady(oracle* o, int32_t leader, int64_t tick0) {
     uint32_t L = oracle_steady_leader(&o->cfg, c.gid, leader);
     for (uint32_t r = 0; r < o->cfg.replicas; ++r) {
       o_node* n = &G->n[r];
-      n->term = 1; n->voted = 1;
-      if (r == L) { enter_candidate(&c, n, (int)r); n->role = RAFT_LEADER; }
-      else enter_follower(&c, n, (int)r);
+      n->term = 1;
+      n->voted = o->cfg.semantics == RAFT_SEM_RAFT ? (int)L : 1;   /* RAFT: everyone voted for L */
+      if (r == L) {
+        enter_candidate(&c, n, (int)r);
+        n->role = RAFT_LEADER;
+        for (uint32_t p = 0; p < o->cfg.replicas; ++p) n->next[p] = 1;
+      } else {
+        enter_follower(&c, n, (int)r);
+      }
     }
   }
 }
@@ -481,16 +671,25 @@ int oracle_load_state(oracle* o, const raft_state_view* v) {
     for (uint32_t r = 0; r < R; ++r) {
       uint64_t i = g * R + r;
       o_node* n = &G->n[r];
-      n->role = v->role[i]; n->voted = v->voted[i];
+      n->role = v->role[i];
+      n->voted = o->cfg.semantics == RAFT_SEM_RAFT ? (int)v->voted[i] - 1 : v->voted[i];
       n->term = v->term[i]; n->commit = v->commit[i];
       n->deadline = v->deadline[i]; n->timeout = v->timeout[i];
-      for (uint32_t p = 0; p < R; ++p) n->match[p] = v->match[i * R + p];
+      for (uint32_t p = 0; p < R; ++p) {
+        n->match[p] = v->match[i * R + p];
+        /* RAFT: a zero (or absent) NextIndex derives match+1, as REF always does */
+        int32_t nx = (o->cfg.semantics == RAFT_SEM_RAFT && v->next) ? v->next[i * R + p] : 0;
+        n->next[p] = nx > 0 ? nx : n->match[p] + 1;
+      }
       int64_t last = v->last[i];
       if (last < 0) return RAFT_EINVAL;
+      /* hwm below last (e.g. an all-zero plane) means "= last"; REF never truncates so hwm == last */
+      int64_t hwm = (o->cfg.semantics == RAFT_SEM_RAFT && v->hwm && v->hwm[i] > last) ? v->hwm[i] : last;
+      if (last > 0 && last <= hwm - (int64_t)K) return RAFT_EINVAL;   /* last entry outside the ring window */
       n->last = 0;
       if (last > 0) {
         o_ent* tmp = (o_ent*)calloc((size_t)last, sizeof(o_ent));
-        for (int64_t idx = last > K ? last - K + 1 : 1; idx <= last; ++idx) {
+        for (int64_t idx = hwm > K ? hwm - K + 1 : 1; idx <= last; ++idx) {
           uint64_t s = i * K + (uint64_t)((idx - 1) & (K - 1));
           tmp[idx - 1].term = v->log_term[s];
           tmp[idx - 1].value = v->log_value[s];
@@ -500,6 +699,7 @@ int oracle_load_state(oracle* o, const raft_state_view* v) {
         log_append(n, tmp, last);
         free(tmp);
       }
+      n->hwm = hwm;
     }
   }
   return RAFT_OK;
@@ -514,7 +714,8 @@ void oracle_store_state(const oracle* o, raft_state_view* v) {
       uint64_t i = g * R + r;
       const o_node* n = &G->n[r];
       if (v->role) v->role[i] = (uint8_t)n->role;
-      if (v->voted) v->voted[i] = (uint8_t)n->voted;
+      if (v->voted) v->voted[i] = (uint8_t)(o->cfg.semantics == RAFT_SEM_RAFT ? n->voted + 1 : n->voted);
+      if (v->hwm) v->hwm[i] = (int32_t)n->hwm;
       if (v->term) v->term[i] = (int32_t)n->term;
       if (v->last) v->last[i] = (int32_t)n->last;
       if (v->commit) v->commit[i] = (int32_t)n->commit;
@@ -523,12 +724,17 @@ void oracle_store_state(const oracle* o, raft_state_view* v) {
       if (v->match)
         for (uint32_t p = 0; p < R; ++p)
           v->match[i * R + p] = (n->role == RAFT_LEADER && p != r) ? (int32_t)n->match[p] : 0;
+      if (v->next)
+        for (uint32_t p = 0; p < R; ++p)
+          v->next[i * R + p] = (n->role == RAFT_LEADER && p != r)
+                                   ? (int32_t)(o->cfg.semantics == RAFT_SEM_RAFT ? n->next[p] : n->match[p] + 1)
+                                   : 0;
       for (uint32_t s = 0; s < K; ++s) {
         if (v->log_term) v->log_term[i * K + s] = 0;
         if (v->log_value) v->log_value[i * K + s] = 0;
         if (v->log_crc) v->log_crc[i * K + s] = 0;
       }
-      int64_t lo = n->last > K ? n->last - K + 1 : 1;
+      int64_t lo = n->hwm > K ? n->hwm - K + 1 : 1;
       for (int64_t idx = lo; idx <= n->last; ++idx) {
         uint64_t s = i * K + (uint64_t)((idx - 1) & (K - 1));
         if (v->log_term) v->log_term[s] = (int32_t)n->log[idx - 1].term;
@@ -627,7 +833,7 @@ int oracle_append_entries(oracle* o, int64_t now_tick, const raft_ae_req* reqs, 
     r.lc = q->leader_commit; r.n = (int64_t)q->n_entries;
     r.ents = ents;
     r.corrupt = 0;
-    o_aer a = deliver_ae(&c, G, (int)q->to, &r);
+    o_aer a = is_raft(&c) ? r_deliver_ae(&c, G, (int)q->to, &r) : deliver_ae(&c, G, (int)q->to, &r);
     free(ents);
     rs->term = a.term; rs->match_index = a.match; rs->success = G->fault ? 0 : a.ok;
     rs->fault = G->fault;
@@ -640,7 +846,9 @@ int oracle_request_vote(oracle* o, int64_t now_tick, const raft_vote_req* reqs, 
   int rc = check_distinct(o, &reqs[0].group, sizeof(raft_vote_req), n);
   if (rc) return rc;
   for (size_t i = 0; i < n; ++i)
-    if (reqs[i].to >= o->cfg.replicas || !fits32(reqs[i].term)) return RAFT_EINVAL;
+    if (reqs[i].to >= o->cfg.replicas || reqs[i].candidate_id >= o->cfg.replicas || !fits32(reqs[i].term) ||
+        !fits32(reqs[i].last_log_index) || !fits32(reqs[i].last_log_term))
+      return RAFT_EINVAL;
   for (size_t i = 0; i < n; ++i) {
     const raft_vote_req* q = &reqs[i];
     o_group* G = &o->g[q->group];
@@ -649,7 +857,9 @@ int oracle_request_vote(oracle* o, int64_t now_tick, const raft_vote_req* reqs, 
     memset(rs, 0, sizeof *rs);
     if (G->fault) { rs->fault = G->fault; continue; }
     int64_t rt;
-    int grant = deliver_vr(&c, G, (int)q->to, q->term, &rt);
+    int grant = is_raft(&c) ? r_deliver_vr(&c, G, (int)q->to, q->term, (int)q->candidate_id, q->last_log_index,
+                                           q->last_log_term, &rt)
+                            : deliver_vr(&c, G, (int)q->to, q->term, &rt);
     rs->term = rt; rs->vote_granted = grant; rs->fault = G->fault;
   }
   return RAFT_OK;
@@ -680,21 +890,21 @@ int oracle_group_ops(oracle* o, int64_t now_tick, const raft_group_op* ops, size
         break;
       case RAFT_OP_LEADER_ROUND:
         if (nd->role != RAFT_LEADER) { rs->status = RAFT_EINVAL; break; }
-        leader_round(&c, G, x);
+        if (is_raft(&c)) r_leader_round(&c, G, x); else leader_round(&c, G, x);
         rs->value = nd->commit;
         break;
       case RAFT_OP_CANDIDATE_ROUND:
         if (nd->role != RAFT_CANDIDATE) { rs->status = RAFT_EINVAL; break; }
-        rs->value = candidate_round(&c, G, x);
+        rs->value = is_raft(&c) ? r_candidate_round(&c, G, x) : candidate_round(&c, G, x);
         break;
       case RAFT_OP_TIMEOUT:
         if (nd->role == RAFT_LEADER) { rs->status = RAFT_EINVAL; break; }
-        timeout_fire(&c, G, x);
+        if (is_raft(&c)) r_timeout_fire(&c, G, x); else timeout_fire(&c, G, x);
         rs->value = nd->term;
         break;
       case RAFT_OP_LEADER_COMMIT:
         if (nd->role != RAFT_LEADER) { rs->status = RAFT_EINVAL; break; }
-        leader_commit(&c, G, x);
+        if (is_raft(&c)) r_leader_commit(&c, G, x); else leader_commit(&c, G, x);
         rs->value = nd->commit;
         break;
     }

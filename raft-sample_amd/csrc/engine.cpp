@@ -223,7 +223,7 @@ int run_ops(raft_engine* e, int64_t now_tick, const std::vector<DevOp>& ops, con
     HIPCHK(hipMemcpyAsync(d_ec, ec.data(), ec.size() * 4, hipMemcpyHostToDevice, e->stream));
   }
   const Trace T = make_trace(e, now_tick);
-  HIPCHK(launch_ops(e->R, e->P, T, d_ops, uint32_t(n), d_et, d_ev, d_ec, d_res, e->stream));
+  HIPCHK(launch_ops(e->R, int(e->cfg.semantics), e->P, T, d_ops, uint32_t(n), d_et, d_ev, d_ec, d_res, e->stream));
   HIPCHK(hipMemcpyAsync(res.data(), d_res, n * sizeof(DevRes), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return RAFT_OK;
@@ -277,12 +277,13 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (c.groups < 1) return fail(RAFT_EINVAL, "groups must be >= 1");
   if (c.ring_depth < 2 || c.ring_depth > 4096 || (c.ring_depth & (c.ring_depth - 1)))
     return fail(RAFT_EINVAL, "ring_depth must be a power of two in [2, 4096]");
-  if (c.semantics != RAFT_SEM_REF) return fail(RAFT_EINVAL, "only RAFT_SEM_REF is implemented");
+  if (c.semantics != RAFT_SEM_REF && c.semantics != RAFT_SEM_RAFT)
+    return fail(RAFT_EINVAL, "semantics must be RAFT_SEM_REF or RAFT_SEM_RAFT");
   if (c.tick_seconds < 1) return fail(RAFT_EINVAL, "tick_seconds must be >= 1");
   if (c.follower_timeout_min < 1 || c.follower_timeout_span < 1 || c.candidate_timeout_min < 1 ||
-      c.candidate_timeout_span < 1 || c.follower_timeout_min + c.follower_timeout_span > 8192 ||
-      c.candidate_timeout_min + c.candidate_timeout_span > 8192)
-    return fail(RAFT_EINVAL, "timer ranges must be >= 1 and below 8192 s");
+      c.candidate_timeout_span < 1 || c.follower_timeout_min + c.follower_timeout_span > 1024 ||
+      c.candidate_timeout_min + c.candidate_timeout_span > 1024)
+    return fail(RAFT_EINVAL, "timer ranges must be >= 1 and below 1024 s (10-bit duration field)");
   if (c.isolate_per_65536 > 65536) return fail(RAFT_EINVAL, "isolate_per_65536 must be <= 65536");
   if (c.payload_crc > 1) return fail(RAFT_EINVAL, "payload_crc must be 0 or 1");
   if (c.corrupt_per_65536 > 65536) return fail(RAFT_EINVAL, "corrupt_per_65536 must be <= 65536");
@@ -323,6 +324,12 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.log_value), R * K * Gp * 8);
   if (c.payload_crc) A(reinterpret_cast<void**>(&e->P.log_crc), R * K * Gp * 4);
+  const bool raft = c.semantics == RAFT_SEM_RAFT;
+  if (raft) {   // NextIndex rows and high-water marks exist only in RAFT mode
+    A(reinterpret_cast<void**>(&e->P.lnext), R * Gp * 4);
+    A(reinterpret_cast<void**>(&e->P.xnext), R * R * Gp * 4);
+    A(reinterpret_cast<void**>(&e->P.hwm), R * Gp * 4);
+  }
   uint32_t* d_tab = nullptr;
   A(reinterpret_cast<void**>(&d_tab), 8 * 256 * 4);
   e->P.crc_tab = d_tab;
@@ -364,6 +371,11 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_value, 0, R * K * Gp * 8, e->stream) : z;
   if (c.payload_crc) z = z == hipSuccess ? hipMemsetAsync(e->P.log_crc, 0, R * K * Gp * 4, e->stream) : z;
+  if (raft) {
+    z = z == hipSuccess ? hipMemsetAsync(e->P.lnext, 0, R * Gp * 4, e->stream) : z;
+    z = z == hipSuccess ? hipMemsetAsync(e->P.xnext, 0, R * R * Gp * 4, e->stream) : z;
+    z = z == hipSuccess ? hipMemsetAsync(e->P.hwm, 0, R * Gp * 4, e->stream) : z;
+  }
   z = z == hipSuccess ? hipMemcpyAsync(d_tab, crc_tab_host().data(), 8 * 256 * 4, hipMemcpyHostToDevice, e->stream) : z;
   z = z == hipSuccess ? hipStreamSynchronize(e->stream) : z;
   if (z != hipSuccess) {
@@ -419,7 +431,8 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!e || !v) return fail(RAFT_EINVAL, "null argument");
   HIPCHK(hipSetDevice(e->cfg.device));
   const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
-  std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt;
+  const bool raft = e->cfg.semantics == RAFT_SEM_RAFT;
+  std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt, ln, xn, hw;
   std::vector<uint16_t> rs, meta;
   std::vector<int64_t> lv;
   std::vector<uint32_t> lcrc;
@@ -433,6 +446,9 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!rc) rc = d2h(e, lm, e->P.lmatch, R * Gp);
   if (!rc) rc = d2h(e, xm, e->P.xmatch, R * R * Gp);
   if (!rc) rc = d2h(e, meta, e->P.gmeta, Gp);
+  if (!rc && raft) rc = d2h(e, ln, e->P.lnext, R * Gp);
+  if (!rc && raft) rc = d2h(e, xn, e->P.xnext, R * R * Gp);
+  if (!rc && raft) rc = d2h(e, hw, e->P.hwm, R * Gp);
   const bool logs = v->log_term || v->log_value || v->log_crc;
   std::vector<int32_t> ltm;
   if (!rc && logs) rc = d2h(e, ltm, e->P.lterm, R * Gp);
@@ -450,19 +466,30 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
       const uint64_t d = r * Gp + g, c = g * R + r;
       const int role = rs[d] & 3;
       if (v->role) v->role[c] = uint8_t(role);
-      if (v->voted) v->voted[c] = uint8_t((rs[d] >> 2) & 1);
+      if (v->voted) v->voted[c] = uint8_t((rs[d] >> 2) & 15);
       if (v->term) v->term[c] = term[d];
       if (v->last) v->last[c] = last[d];
       if (v->commit) v->commit[c] = commit[d];
       // deadline = effective timer start + d; followers/candidates also count hb
-      if (v->deadline) v->deadline[c] = (role == ROLE_L ? ts[d] : std::max(ts[d], hb[g])) + int32_t(rs[d] >> 3);
-      if (v->timeout) v->timeout[c] = int32_t(rs[d] >> 3);
+      if (v->deadline) v->deadline[c] = (role == ROLE_L ? ts[d] : std::max(ts[d], hb[g])) + int32_t(rs[d] >> 6);
+      if (v->timeout) v->timeout[c] = int32_t(rs[d] >> 6);
+      const int32_t hwm = raft ? hw[d] : last[d];
+      if (v->hwm) v->hwm[c] = hwm;
       if (v->match)
         for (uint64_t p = 0; p < R; ++p) {
           int32_t m = 0;
           if (role == ROLE_L && p != r)
             m = (int(r) == primary) ? (msync ? last[p * Gp + g] : lm[p * Gp + g]) : xm[(r * R + p) * Gp + g];
           v->match[c * R + p] = m;
+        }
+      if (v->next)
+        for (uint64_t p = 0; p < R; ++p) {
+          int32_t nx = 0;
+          if (role == ROLE_L && p != r) {
+            if (raft) nx = (int(r) == primary) ? ln[p * Gp + g] : xn[(r * R + p) * Gp + g];
+            else nx = ((int(r) == primary) ? (msync ? last[p * Gp + g] : lm[p * Gp + g]) : xm[(r * R + p) * Gp + g]) + 1;
+          }
+          v->next[c * R + p] = nx;
         }
       if (logs && last[d] > 0) {
         const int32_t want = lt[(r * K + uint64_t((last[d] - 1) & int64_t(K - 1))) * Gp + g];
@@ -475,7 +502,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
         for (uint64_t s = 0; s < K; ++s) {
           // slot s holds the largest index i <= l with (i-1) mod K == s
           int64_t idx = l >= 1 ? l - ((l - 1 - int64_t(s)) & int64_t(K - 1)) : 0;
-          const bool live = idx >= 1 && idx <= l && idx > l - int64_t(K);
+          const bool live = idx >= 1 && idx <= l && idx > int64_t(hwm) - int64_t(K);
           const uint64_t o = (r * K + s) * Gp + g;
           if (v->log_term) v->log_term[c * K + s] = live ? lt[o] : 0;
           if (v->log_value) v->log_value[c * K + s] = live ? lv[o] : 0;
@@ -501,12 +528,16 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   std::vector<int64_t> lv(R * K * Gp, 0);
   std::vector<int32_t> ltm(R * Gp, 0);
   std::vector<uint32_t> lcrc(e->cfg.payload_crc ? R * K * Gp : 0, 0);
+  const bool raft = e->cfg.semantics == RAFT_SEM_RAFT;
+  std::vector<int32_t> ln(raft ? R * Gp : 0, 0), xn(raft ? R * R * Gp : 0, 0), hw(raft ? R * Gp : 0, 0);
+  const int max_vote = raft ? int(R) : 1;   // REF Voted bool; RAFT votedFor + 1
   for (uint64_t g = 0; g < G; ++g) {
     if (v->fault[g] > RAFT_F_OVERFLOW) return fail(RAFT_EINVAL, "group %llu: bad fault code", (unsigned long long)g);
     int primary = NO_PRIMARY;
     for (uint64_t r = 0; r < R; ++r) {
       const uint64_t c = g * R + r;
-      if (v->role[c] > RAFT_LEADER || v->voted[c] > 1 || v->last[c] < 0 || v->timeout[c] < 0 || v->timeout[c] > 8191)
+      if (v->role[c] > RAFT_LEADER || v->voted[c] > max_vote || v->last[c] < 0 || v->timeout[c] < 0 ||
+          v->timeout[c] > 1023)
         return fail(RAFT_EINVAL, "group %llu replica %llu: field out of range", (unsigned long long)g,
                     (unsigned long long)r);
       if (v->role[c] == RAFT_LEADER && primary == NO_PRIMARY) primary = int(r);
@@ -521,13 +552,28 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
       last[d] = v->last[c];
       commit[d] = v->commit[c];
       ts[d] = v->deadline[c] - v->timeout[c];
-      rs[d] = uint16_t(v->role[c] | (v->voted[c] << 2) | (uint32_t(v->timeout[c]) << 3));
+      rs[d] = uint16_t(v->role[c] | (v->voted[c] << 2) | (uint32_t(v->timeout[c]) << 6));
       if (v->role[c] == RAFT_LEADER)
         for (uint64_t p = 0; p < R; ++p) {
           if (p == r) continue;
-          if (int(r) == primary) lm[p * Gp + g] = v->match[c * R + p];
-          else xm[(r * R + p) * Gp + g] = v->match[c * R + p];
+          const int32_t m = v->match[c * R + p];
+          // RAFT: NextIndex as given, 0/absent derives match+1 (the oracle's rule)
+          const int32_t nx = (v->next && v->next[c * R + p] > 0) ? v->next[c * R + p] : m + 1;
+          if (int(r) == primary) {
+            lm[p * Gp + g] = m;
+            if (raft) ln[p * Gp + g] = nx;
+          } else {
+            xm[(r * R + p) * Gp + g] = m;
+            if (raft) xn[(r * R + p) * Gp + g] = nx;
+          }
         }
+      if (raft) {
+        const int32_t h = (v->hwm && v->hwm[c] > v->last[c]) ? v->hwm[c] : v->last[c];
+        if (v->last[c] > 0 && int64_t(v->last[c]) <= int64_t(h) - int64_t(K))
+          return fail(RAFT_EINVAL, "group %llu replica %llu: last entry outside the ring window (hwm - K, hwm]",
+                      (unsigned long long)g, (unsigned long long)r);
+        hw[d] = h;
+      }
       for (uint64_t s = 0; s < K; ++s) {
         lt[(r * K + s) * Gp + g] = v->log_term[c * K + s];
         lv[(r * K + s) * Gp + g] = v->log_value[c * K + s];
@@ -549,6 +595,9 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.xmatch, xm);
   if (!rc) rc = h2d(e, e->P.gmeta, meta);
   if (!rc) rc = h2d(e, e->P.lterm, ltm);
+  if (!rc && raft) rc = h2d(e, e->P.lnext, ln);
+  if (!rc && raft) rc = h2d(e, e->P.xnext, xn);
+  if (!rc && raft) rc = h2d(e, e->P.hwm, hw);
   if (!rc && e->cfg.payload_crc) rc = h2d(e, e->P.log_crc, lcrc);
   if (!rc) rc = h2d(e, e->P.log_term, lt);
   if (!rc) rc = h2d(e, e->P.log_value, lv);
@@ -585,11 +634,13 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       b = next_event(e);
       if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
     }
-    HIPCHK(launch_tick_fast(e->R, e->P, T, st, e->work, e->work_tick, cnt, e->force_general, e->write_through,
+    // RAFT mode has no steady-state fast path yet: every group takes the general kernel
+    const int force = e->force_general || e->cfg.semantics == RAFT_SEM_RAFT;
+    HIPCHK(launch_tick_fast(e->R, e->P, T, st, e->work, e->work_tick, cnt, force, e->write_through,
                             e->stream, a, b));
     // deferred groups catch up every slow_every ticks and at the end of the call
     if ((i + 1) % e->slow_every == 0 || i + 1 == nticks) {
-      HIPCHK(launch_tick_slow(e->R, e->P, T0, first_tick, t, stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
+      HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, t, stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
                               e->wcount + ((window + 1) & 1), e->stream));
       ++window;
     }
@@ -685,9 +736,15 @@ int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_re
   for (size_t i = 0; i < n; ++i) {
     const raft_vote_req& q = reqs[i];
     if (q.to >= e->cfg.replicas) return fail(RAFT_EINVAL, "req %zu: receiver out of range", i);
-    if (!fits32(q.term)) return fail(RAFT_EINVAL, "req %zu: term outside int32", i);
+    if (q.candidate_id >= e->cfg.replicas) return fail(RAFT_EINVAL, "req %zu: candidate out of range", i);
+    if (!fits32(q.term) || !fits32(q.last_log_index) || !fits32(q.last_log_term))
+      return fail(RAFT_EINVAL, "req %zu: term/index outside int32", i);
     std::memset(&ops[i], 0, sizeof(DevOp));
     ops[i].group = q.group; ops[i].replica = q.to; ops[i].kind = OP_VR; ops[i].term = int32_t(q.term);
+    // RAFT mode only (REF ignores them): CandidateId, LastLogIndex, LastLogTerm
+    ops[i].arg = q.candidate_id;
+    ops[i].prev_idx = int32_t(q.last_log_index);
+    ops[i].prev_term = int32_t(q.last_log_term);
   }
   std::vector<DevRes> res;
   if (int rc = run_ops(e, now_tick, ops, {}, {}, {}, res)) return rc;

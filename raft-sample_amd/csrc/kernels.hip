@@ -47,8 +47,8 @@ __device__ __forceinline__ long long wave_sum(int v) {
   return x;
 }
 
-template <int R>
-__device__ __forceinline__ void run_tick(Group<R>& G, const DevPlanes& P, const Trace& T, uint32_t E) {
+template <int R, int SEM>
+__device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, const Trace& T, uint32_t E) {
   if (T.iso_p) G.iso = isolation_mask<R>(G.key, T);
 
   // 1. client: every Leader receives E NewLogRequests (main.go:87-93 -> 327-329).
@@ -74,6 +74,7 @@ __device__ __forceinline__ void run_tick(Group<R>& G, const DevPlanes& P, const 
         G.last[r] = l + n_ok;
         G.d_last |= 1u << r;
         at(prow(P.lterm, r, P.Gp), G.g) = G.term[r];
+        if constexpr (SEM == SEM_RAFT) G.template r_grew<r>(l + n_ok);
       }
       if (n_ok < int(E)) G.raise(F_OVERFLOW);
     });
@@ -93,8 +94,13 @@ __device__ __forceinline__ void run_tick(Group<R>& G, const DevPlanes& P, const 
     const uint32_t rest = active & ~((1u << (2 * c + 2)) - 1u);    // replicas after c (c=-1: all)
     if (!rest) break;
     c = int(__builtin_ctz(rest)) >> 1;
-    if (G.role(c) == ROLE_L) G.leader_round(P, T, c, make_src);    // main.go:332-391
-    else G.candidate_round(P, T, c);                               // main.go:253-284
+    if constexpr (SEM == SEM_RAFT) {
+      if (G.role(c) == ROLE_L) G.r_leader_round(P, T, c, make_src);
+      else G.r_candidate_round(P, T, c);
+    } else {
+      if (G.role(c) == ROLE_L) G.leader_round(P, T, c, make_src);  // main.go:332-391
+      else G.candidate_round(P, T, c);                             // main.go:253-284
+    }
   }
 
   // 3. expired election timers in (deadline, id) order; each new candidate
@@ -109,9 +115,11 @@ __device__ __forceinline__ void run_tick(Group<R>& G, const DevPlanes& P, const 
       if (d <= G.now && (best < 0 || d < bdl)) { best = r; bdl = d; }
     });
     if (best < 0) break;
-    G.timeout_fire(T, best);
+    if constexpr (SEM == SEM_RAFT) G.r_timeout_fire(T, best);
+    else G.timeout_fire(T, best);
     if (!G.alive()) break;
-    G.candidate_round(P, T, best);
+    if constexpr (SEM == SEM_RAFT) G.r_candidate_round(P, T, best);
+    else G.candidate_round(P, T, best);
   }
 
   if (!G.alive()) {
@@ -359,7 +367,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
 // by tick in order, from the tick it was deferred at to `last_tick`, with
 // the full REF semantics of run_tick() (elections, candidates, step-downs,
 // faults, EXT drops); stats go to each tick's own record.
-template <int R>
+template <int R, int SEM>
 __global__ __launch_bounds__(256) void tick_slow_kernel(DevPlanes P, Trace T0, int64_t first_tick, int64_t last_tick,
                                                         unsigned long long* stats, const uint32_t* work,
                                                         const int32_t* work_tick, const uint32_t* work_count,
@@ -370,14 +378,14 @@ __global__ __launch_bounds__(256) void tick_slow_kernel(DevPlanes P, Trace T0, i
     const uint32_t g = work[i];
     for (int64_t t = work_tick[i]; t <= last_tick; ++t) {
       const Trace T = T0.at_tick(t);
-      Group<R> G;
+      Group<R, SEM> G;
       G.begin(P, T, g);
       if (G.fault) {            // frozen earlier in this catch-up
         if (G.meta0 & M_DEFER) at(P.gmeta, g) = uint16_t(G.meta0 & ~M_DEFER);
         break;
       }
       G.load(P, false);
-      run_tick<R>(G, P, T, T.client_entries());
+      run_tick<R, SEM>(G, P, T, T.client_entries());
       G.store(P);
       if (stats) {
         unsigned long long* rec = stats + size_t(t - first_tick) * STAT_SLOTS * NSTAT + (g % STAT_SLOTS) * NSTAT;
@@ -396,7 +404,7 @@ __device__ __forceinline__ void with_replica(int x, F&& f) {
   });
 }
 
-template <int R>
+template <int R, int SEM>
 __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const DevOp* ops, uint32_t n,
                                                   const int32_t* et, const int64_t* ev, const uint32_t* ec,
                                                   DevRes* out) {
@@ -404,7 +412,7 @@ __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const De
   if (i >= n) return;
   const DevOp op = ops[i];
   DevRes res{0, 0, 0, 0, 0};
-  Group<R> G;
+  Group<R, SEM> G;
   G.begin(P, T, uint32_t(op.group));
   if (G.fault) {
     res.fault = G.fault;
@@ -427,7 +435,9 @@ __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const De
       HostSrc src{et, ev, ec, op.off, 0};
       with_replica<R>(x, [&](auto PI) {
         constexpr int p = decltype(PI)::value;
-        const AEResp a = G.template deliver_ae<p>(P, T, q, src);
+        AEResp a;
+        if constexpr (SEM == SEM_RAFT) a = G.template r_deliver_ae<p>(P, T, q, src);
+        else a = G.template deliver_ae<p>(P, T, q, src);
         res.term = a.term; res.ok = a.ok; res.value = a.match;
       });
       break;
@@ -436,7 +446,10 @@ __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const De
       with_replica<R>(x, [&](auto PI) {
         constexpr int p = decltype(PI)::value;
         int rt;
-        const int gr = G.template deliver_vr<p>(T, op.term, &rt);
+        int gr;
+        // RAFT: CandidateId = arg, LastLogIndex = prev_idx, LastLogTerm = prev_term
+        if constexpr (SEM == SEM_RAFT) gr = G.template r_deliver_vr<p>(P, T, op.term, int(op.arg), op.prev_idx, op.prev_term, &rt);
+        else gr = G.template deliver_vr<p>(T, op.term, &rt);
         res.term = rt; res.ok = gr; res.value = gr;
       });
       break;
@@ -448,16 +461,19 @@ __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const De
       break;
     case OP_LEADER_ROUND:
       if (ro != ROLE_L) { res.status = -22; break; }
-      G.leader_round(P, T, x, make_src);
+      if constexpr (SEM == SEM_RAFT) G.r_leader_round(P, T, x, make_src);
+      else G.leader_round(P, T, x, make_src);
       res.value = sel(G.commit, x);
       break;
     case OP_CANDIDATE_ROUND:
       if (ro != ROLE_C) { res.status = -22; break; }
-      res.value = G.candidate_round(P, T, x);
+      if constexpr (SEM == SEM_RAFT) res.value = G.r_candidate_round(P, T, x);
+      else res.value = G.candidate_round(P, T, x);
       break;
     case OP_TIMEOUT:
       if (ro == ROLE_L) { res.status = -22; break; }
-      G.timeout_fire(T, x);
+      if constexpr (SEM == SEM_RAFT) G.r_timeout_fire(T, x);
+      else G.timeout_fire(T, x);
       res.value = sel(G.term, x);
       break;
     case OP_LEADER_COMMIT: {
@@ -465,7 +481,9 @@ __global__ __launch_bounds__(256) void ops_kernel(DevPlanes P, Trace T, const De
       int m[R];
       G.load_match(P, x, m);
       const int lc = sel(G.commit, x);
-      const int nc = G.commit_rule(m, x, lc);
+      int nc;
+      if constexpr (SEM == SEM_RAFT) nc = G.r_commit_rule(P, m, x, lc);
+      else nc = G.commit_rule(m, x, lc);
       if (nc != lc) { put(G.commit, x, nc); G.d_commit |= 1u << x; }
       res.value = nc;
       break;
@@ -491,8 +509,9 @@ __global__ __launch_bounds__(256) void init_new_kernel(DevPlanes P, Trace T) {
     const int d = T.f_min + int(uint32_t(rng_k(key, r, ST_TIMER_F, uint64_t(T.tick)) >> 32) % uint32_t(T.f_span));
     P.term[i] = 0; P.last[i] = 0; P.commit[i] = 0;
     P.tstart[i] = T.now;
-    P.rs[i] = uint16_t(ROLE_F | (uint32_t(d) << 3));
+    P.rs[i] = uint16_t(ROLE_F | (uint32_t(d) << 6));   // vote 0 (REF: not voted; RAFT: votedFor none)
     P.lterm[i] = 0;
+    if (P.hwm) P.hwm[i] = 0;
   }
   P.hb[g] = HB_NONE;
   P.gmeta[g] = uint16_t(NO_PRIMARY);
@@ -513,14 +532,20 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
     const uint64_t h = rng_k(key, r, isL ? ST_TIMER_C : ST_TIMER_F, uint64_t(T.tick));
     const int d = isL ? T.c_min + int(uint32_t(h >> 32) % uint32_t(T.c_span))
                       : T.f_min + int(uint32_t(h >> 32) % uint32_t(T.f_span));
+    // REF: Voted = true; RAFT: everyone voted for L (votedFor + 1)
+    const uint32_t vote = P.hwm ? uint32_t(L + 1) : 1u;
     P.term[i] = 1; P.last[i] = 0; P.commit[i] = 0;
     P.tstart[i] = T.now;
-    P.rs[i] = uint16_t((isL ? ROLE_L : ROLE_F) | (1u << 2) | (uint32_t(d) << 3));
+    P.rs[i] = uint16_t((isL ? ROLE_L : ROLE_F) | (vote << 2) | (uint32_t(d) << 6));
     P.lmatch[i] = 0;
     P.lterm[i] = 0;
+    if (P.hwm) {                       // RAFT mode: NextIndex = last + 1 = 1, high-water 0
+      P.lnext[i] = 1;
+      P.hwm[i] = 0;
+    }
   }
   P.hb[g] = HB_NONE;
-  P.gmeta[g] = uint16_t(L | M_MSYNC | M_STEADY);
+  P.gmeta[g] = uint16_t(L | (P.hwm ? 0 : M_MSYNC) | M_STEADY);
 }
 
 // ------------------------------------------------------ host launchers ---
@@ -560,17 +585,28 @@ hipError_t launch_tick_fast(int R, const DevPlanes& P, const Trace& T, unsigned 
 #undef RAFT_FAST
   return hipGetLastError();
 }
-hipError_t launch_tick_slow(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
+hipError_t launch_tick_slow(int R, int sem, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
                             unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
                             const uint32_t* work_count, uint32_t* next_count, hipStream_t s) {
   const unsigned blocks = unsigned(std::min<uint64_t>((P.G + 255) / 256, 1024));
-  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(tick_slow_kernel<RR>, dim3(blocks), dim3(256), 0, s, P, T0, first_tick,
-                                        last_tick, stats, work, work_tick, work_count, next_count));
+  if (sem == SEM_RAFT) {
+    RAFT_DISPATCH_R(R, hipLaunchKernelGGL((tick_slow_kernel<RR, SEM_RAFT>), dim3(blocks), dim3(256), 0, s, P, T0,
+                                          first_tick, last_tick, stats, work, work_tick, work_count, next_count));
+  } else {
+    RAFT_DISPATCH_R(R, hipLaunchKernelGGL((tick_slow_kernel<RR, SEM_REF>), dim3(blocks), dim3(256), 0, s, P, T0,
+                                          first_tick, last_tick, stats, work, work_tick, work_count, next_count));
+  }
   return hipGetLastError();
 }
-hipError_t launch_ops(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
+hipError_t launch_ops(int R, int sem, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
                       const int32_t* et, const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s) {
-  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(ops_kernel<RR>, grid_for(n), dim3(256), 0, s, P, T, ops, n, et, ev, ec, out));
+  if (sem == SEM_RAFT) {
+    RAFT_DISPATCH_R(R, hipLaunchKernelGGL((ops_kernel<RR, SEM_RAFT>), grid_for(n), dim3(256), 0, s, P, T, ops, n, et,
+                                          ev, ec, out));
+  } else {
+    RAFT_DISPATCH_R(R, hipLaunchKernelGGL((ops_kernel<RR, SEM_REF>), grid_for(n), dim3(256), 0, s, P, T, ops, n, et,
+                                          ev, ec, out));
+  }
   return hipGetLastError();
 }
 hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_t s) {

@@ -22,6 +22,7 @@
 namespace raftstep {
 
 enum : int { ROLE_F = 0, ROLE_C = 1, ROLE_L = 2 };
+enum : int { SEM_REF = 0, SEM_RAFT = 1 };
 enum : int {
   F_NONE = 0, F_PANIC_GETLOG = 1, F_DEADLOCK_VRES = 2, F_DEADLOCK_LEADER_VREQ = 3,
   F_RING_EVICTED = 4, F_OVERFLOW = 5
@@ -49,9 +50,13 @@ struct DevPlanes {
   int32_t* commit;     // Node.CommitIndex          (main.go:24)
   int32_t* tstart;     // election timer start (virtual s); deadline = start + d
   int32_t* hb;         // [Gp] time of the last steady-state heartbeat that reset every follower
-  uint16_t* rs;        // role:2 | voted:1 | timer duration d:13 (main.go:16, 20, 114, 194)
+  uint16_t* rs;        // role:2 | vote:4 | timer duration d:10 (main.go:16, 20, 114, 194);
+                       // vote = Voted (REF) or votedFor+1 (RAFT, 0 = none)
   int32_t* lmatch;     // [R][Gp] MatchIndex row of the group's primary leader (main.go:29)
   int32_t* xmatch;     // [R][R][Gp] rows of any further concurrent leaders (EXT only)
+  int32_t* lnext;      // RAFT mode: [R][Gp] NextIndex row of the primary leader (REF derives match+1)
+  int32_t* xnext;      // RAFT mode: [R][R][Gp] NextIndex rows of further leaders
+  int32_t* hwm;        // RAFT mode: [R][Gp] highest LastApplied ever (== last in REF)
   uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
   int32_t* lterm;      // [R][Gp] Log[len-1].Term: cached term of each replica's last entry
   int32_t* log_term;   // Log.Term  ring
@@ -164,14 +169,17 @@ struct AEReq {          // AppendEntriesRequest (main.go:289-296), LeaderId impl
 };
 struct AEResp { int term, match, ok; };  // AppendEntriesResponse (main.go:298-302)
 
-// Group context: the R replicas of one group, in registers.
-template <int R>
+// Group context: the R replicas of one group, in registers. SEM selects the
+// handler rules: SEM_REF = main.go bit for bit, SEM_RAFT = the EXT
+// Raft-paper mode (same tick model and layout, see the r_* methods).
+template <int R, int SEM = SEM_REF>
 struct Group {
   int term[R], last[R], commit[R], dl[R], dur[R];
+  int hw[R];            // RAFT: high-water mark of each log (REF: unused)
   uint32_t roles;       // 2 bits per replica
-  uint32_t voted;       // 1 bit per replica
+  uint32_t votes;       // 4 bits per replica: REF Voted (0/1), RAFT votedFor+1
   uint32_t known;       // deadline register valid
-  uint32_t d_term, d_last, d_commit, d_dl, d_rs;
+  uint32_t d_term, d_last, d_commit, d_dl, d_rs, d_hw;
   int primary, fault, meta0, hbt;
   uint32_t iso;         // EXT: replicas isolated during this tick
   uint32_t g;           // group index on this engine (lane)
@@ -189,11 +197,13 @@ struct Group {
     roles = (roles & ~(3u << (2 * r))) | (uint32_t(v) << (2 * r));
     d_rs |= 1u << r;
   }
-  __device__ __forceinline__ bool is_voted(int r) const { return (voted >> r) & 1u; }
-  __device__ __forceinline__ void set_voted(int r, bool v) {
-    voted = v ? (voted | (1u << r)) : (voted & ~(1u << r));
+  __device__ __forceinline__ int vote(int r) const { return int(votes >> (4 * r)) & 15; }
+  __device__ __forceinline__ void set_vote(int r, int v) {
+    votes = (votes & ~(15u << (4 * r))) | (uint32_t(v) << (4 * r));
     d_rs |= 1u << r;
   }
+  __device__ __forceinline__ bool is_voted(int r) const { return vote(r) != 0; }
+  __device__ __forceinline__ void set_voted(int r, bool v) { set_vote(r, v ? 1 : 0); }
   __device__ __forceinline__ void raise(int f) {
     if (!fault) fault = f;
   }
@@ -206,7 +216,7 @@ struct Group {
     key = group_key(T.seed, P.gbase + g);
     tick = T.tick;
     now = T.now;
-    d_term = d_last = d_commit = d_dl = d_rs = 0;
+    d_term = d_last = d_commit = d_dl = d_rs = d_hw = 0;
     known = 0;
     iso = 0;
 #pragma unroll
@@ -223,7 +233,7 @@ struct Group {
   // steady-state heartbeat (hb), which resets every follower at once.
   __device__ __forceinline__ int eff_start(int ts, int r) const { return role(r) == ROLE_L ? ts : max(ts, hbt); }
   __device__ __forceinline__ void load(const DevPlanes& P, bool with_deadlines) {
-    roles = 0; voted = 0;
+    roles = 0; votes = 0;
     hbt = at(P.hb, g);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -232,8 +242,9 @@ struct Group {
       commit[r] = at(prow(P.commit, r, P.Gp), g);
       const uint32_t x = at(prow(P.rs, r, P.Gp), g);
       roles |= (x & 3u) << (2 * r);
-      voted |= ((x >> 2) & 1u) << r;
-      dur[r] = int(x >> 3);
+      votes |= ((x >> 2) & 15u) << (4 * r);
+      dur[r] = int(x >> 6);
+      hw[r] = (SEM == SEM_RAFT) ? at(prow(P.hwm, r, P.Gp), g) : 0;
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) dl[r] = with_deadlines ? eff_start(at(prow(P.tstart, r, P.Gp), g), r) + dur[r] : 0;
@@ -254,7 +265,8 @@ struct Group {
       if ((d_dl >> r) & 1u) at(prow(P.tstart, r, P.Gp), g) = dl[r] - dur[r];
       if ((d_rs >> r) & 1u)
         at(prow(P.rs, r, P.Gp), g) =
-            uint16_t(((roles >> (2 * r)) & 3u) | (((voted >> r) & 1u) << 2) | (uint32_t(dur[r]) << 3));
+            uint16_t(((roles >> (2 * r)) & 3u) | (((votes >> (4 * r)) & 15u) << 2) | (uint32_t(dur[r]) << 6));
+      if (SEM == SEM_RAFT && ((d_hw >> r) & 1u)) at(prow(P.hwm, r, P.Gp), g) = hw[r];
     }
     // DEFER and MSYNC are consumed by the general path; STEADY is recomputed
     const bool steady = primary < R && role(primary) == ROLE_L && (roles & ~(3u << (2 * primary))) == 0u;
@@ -501,11 +513,11 @@ struct Group {
     if (primary == c) {
 #pragma unroll
       for (int p = 0; p < R; ++p)
-        if ((dirty >> p) & 1u) at(prow(P.lmatch, p, P.Gp), g) = m[p];
+        if (p != c && ((dirty >> p) & 1u)) at(prow(P.lmatch, p, P.Gp), g) = m[p];
     } else {
 #pragma unroll
       for (int p = 0; p < R; ++p)
-        if ((dirty >> p) & 1u) at(prow(P.xmatch, c * R + p, P.Gp), g) = m[p];
+        if (p != c && ((dirty >> p) & 1u)) at(prow(P.xmatch, c * R + p, P.Gp), g) = m[p];
     }
   }
 
@@ -569,6 +581,7 @@ struct Group {
     at(P.lterm + uint64_t(c) * P.Gp, g) = t;
     put(last, c, l + 1);
     d_last |= 1u << c;
+    if (SEM == SEM_RAFT && l + 1 > sel(hw, c)) { put(hw, c, l + 1); d_hw |= 1u << c; }
   }
 
   // timer.C (main.go:171-177 follower -> candidate, 248-251 candidate Term++).
@@ -577,6 +590,262 @@ struct Group {
     if (t >= I32MAX) { raise(F_OVERFLOW); return; }
     put(term, c, t + 1);
     d_term |= 1u << c;
+    ++st[S_BUMPS];
+    enter_candidate(T, c);
+  }
+
+  // =====================================================================
+  // EXT RAFT-paper semantics (SEM_RAFT; Ongaro & Ousterhout, Figure 2), the
+  // device twin of oracle/raft_oracle.c's r_* functions. Same tick model.
+  // =====================================================================
+  // A higher term in any RPC: adopt it, forget the vote, become a follower.
+  template <int Rp>
+  __device__ __forceinline__ void r_observe(const Trace& T, int t) {
+    if (t <= term[Rp]) return;
+    set_term<Rp>(t);
+    set_vote(Rp, 0);
+    if (role(Rp) != ROLE_F) {
+      if (primary == Rp) primary = NO_PRIMARY;
+      enter_follower<Rp>(T);
+    }
+  }
+  __device__ __forceinline__ void r_observe_rt(const Trace& T, int c, int t) {   // runtime replica id
+    if (t <= sel(term, c)) return;
+    put(term, c, t);
+    d_term |= 1u << c;
+    set_vote(c, 0);
+    if (role(c) != ROLE_F) {
+      if (primary == c) primary = NO_PRIMARY;
+      set_role(c, ROLE_F);
+      const int d = draw(T, c, false);
+      put(dur, c, d);
+      put(dl, c, now + d);
+      known |= 1u << c;
+      d_dl |= 1u << c;
+    }
+  }
+  __device__ __forceinline__ int lterm_of(const DevPlanes& P, int r, int l) const {
+    return l > 0 ? at(P.lterm + uint64_t(r) * P.Gp, g) : 0;
+  }
+  template <int Rp>
+  __device__ __forceinline__ void r_grew(int nl) {   // the log reached length nl
+    if (nl > hw[Rp]) { hw[Rp] = nl; d_hw |= 1u << Rp; }
+  }
+
+  template <int Rp>
+  __device__ __forceinline__ int r_deliver_vr(const DevPlanes& P, const Trace& T, int t, int cand, int llast,
+                                              int llterm, int* resp_term) {
+    r_observe<Rp>(T, t);
+    *resp_term = term[Rp];
+    if (t < term[Rp]) return 0;
+    const int mt = lterm_of(P, Rp, last[Rp]);
+    const bool uptodate = llterm > mt || (llterm == mt && llast >= last[Rp]);
+    const int v = vote(Rp);
+    if ((v == 0 || v == cand + 1) && uptodate) {
+      set_vote(Rp, cand + 1);
+      reset_timer<Rp>();                          // granting a vote resets the election timer
+      return 1;
+    }
+    return 0;
+  }
+
+  // On failure res.match is the hint H: the leader retries from min(next-1, H+1).
+  template <int Rp, typename Src>
+  __device__ __forceinline__ AEResp r_deliver_ae(const DevPlanes& P, const Trace& T, const AEReq& q,
+                                                 const Src& src) {
+    r_observe<Rp>(T, q.term);
+    AEResp res{term[Rp], last[Rp], 0};
+    if (q.term < term[Rp]) return res;
+    if (role(Rp) == ROLE_L) return res;           // same-term second leader: cannot happen
+    if (role(Rp) == ROLE_C) enter_follower<Rp>(T);
+    reset_timer<Rp>();
+    const int l = last[Rp];
+    const int K = int(P.K);
+    if (q.prev_idx > l) return res;               // log too short: hint = last
+    if (q.prev_idx > 0) {
+      if (q.prev_idx <= hw[Rp] - K) { raise(F_RING_EVICTED); return res; }
+      if (ring_term(P, Rp, q.prev_idx) != q.prev_term) { res.match = q.prev_idx - 1; return res; }
+    }
+    if (P.crc_on) {                               // EXT: verify what will be stored
+      const int j0 = q.n > K ? q.n - K : 0;
+      for (int j = j0; j < q.n; ++j) {
+        int t; int64_t v; uint32_t c;
+        src.fetch(j, t, v, c);
+        if (q.corrupt && j == q.n - 1) v ^= 1;
+        if (crc_entry(P.crc_tab, t, v) != c) { res.match = q.prev_idx; return res; }
+      }
+    }
+    if (int64_t(q.prev_idx) + q.n > I32MAX) { raise(F_OVERFLOW); return res; }
+    // skip entries already present, truncate at the first conflict, append the rest
+    int j = 0;
+    for (; j < q.n; ++j) {
+      const int idx = q.prev_idx + 1 + j;
+      if (idx > l) break;
+      if (idx <= hw[Rp] - K) { raise(F_RING_EVICTED); return res; }
+      int t; int64_t v; uint32_t c;
+      src.fetch(j, t, v, c);
+      if (ring_term(P, Rp, idx) != t) break;     // conflict: entries from idx on are replaced
+    }
+    if (j < q.n) {
+      int tl = 0;
+      for (int k = j; k < q.n; ++k) {
+        int64_t v; uint32_t c;
+        src.fetch(k, tl, v, c);
+        const int idx = q.prev_idx + 1 + k;
+        ring_term(P, Rp, idx) = tl;
+        ring_value(P, Rp, idx) = v;
+        if (P.crc_on) ring_crc(P, Rp, idx) = c;
+      }
+      const int nl = q.prev_idx + q.n;
+      if (nl != l) { last[Rp] = nl; d_last |= 1u << Rp; }
+      at(prow(P.lterm, Rp, P.Gp), g) = tl;
+      r_grew<Rp>(nl);
+    }
+    const int last_new = q.prev_idx + q.n;
+    if (q.lc > commit[Rp]) {
+      const int nc = q.lc < last_new ? q.lc : last_new;
+      if (nc != commit[Rp]) { commit[Rp] = nc; d_commit |= 1u << Rp; }
+    }
+    res.term = term[Rp]; res.match = last_new; res.ok = 1;
+    return res;
+  }
+
+  __device__ __forceinline__ int r_candidate_round(const DevPlanes& P, const Trace& T, int c) {
+    int count = 1;                                // its own vote (votedFor = self since the timeout)
+    const int ct = sel(term, c), cl = sel(last, c);
+    const int clt = lterm_of(P, c, cl);
+    bool stop = false;
+    static_for<R>([&](auto PI) {
+      constexpr int p = decltype(PI)::value;
+      if (p == c || stop || !alive() || dropped(c, p)) return;
+      int rt;
+      const int gr = r_deliver_vr<p>(P, T, ct, c, cl, clt, &rt);
+      if (!alive()) return;
+      if (rt > ct) { r_observe_rt(T, c, rt); stop = true; return; }
+      if (gr) { ++count; ++st[S_VOTES]; }
+    });
+    if (alive() && !stop && role(c) == ROLE_C && 2 * count > R) {
+      set_role(c, ROLE_L);
+      int m[R], nx[R];
+#pragma unroll
+      for (int p = 0; p < R; ++p) { m[p] = 0; nx[p] = cl + 1; }
+      if (primary == NO_PRIMARY) primary = c;
+      store_match(P, c, m, (1u << R) - 1u);
+      store_next(P, c, nx, (1u << R) - 1u);
+      ++st[S_WON];
+      return 1;
+    }
+    return 0;
+  }
+
+  __device__ __forceinline__ void load_next(const DevPlanes& P, int c, int (&nx)[R]) const {
+    if (primary == c) {
+#pragma unroll
+      for (int p = 0; p < R; ++p) nx[p] = (p != c) ? at(prow(P.lnext, p, P.Gp), g) : 0;
+    } else {
+#pragma unroll
+      for (int p = 0; p < R; ++p) nx[p] = (p != c) ? at(prow(P.xnext, c * R + p, P.Gp), g) : 0;
+    }
+  }
+  __device__ __forceinline__ void store_next(const DevPlanes& P, int c, const int (&nx)[R], uint32_t dirty) const {
+    if (primary == c) {
+#pragma unroll
+      for (int p = 0; p < R; ++p)
+        if (p != c && ((dirty >> p) & 1u)) at(prow(P.lnext, p, P.Gp), g) = nx[p];
+    } else {
+#pragma unroll
+      for (int p = 0; p < R; ++p)
+        if (p != c && ((dirty >> p) & 1u)) at(prow(P.xnext, c * R + p, P.Gp), g) = nx[p];
+    }
+  }
+
+  // commitIndex = the largest N held by a majority (leader included), only
+  // if log[N].term == currentTerm.
+  __device__ __forceinline__ int r_commit_rule(const DevPlanes& P, const int (&m)[R], int c, int cm) {
+    const int ll = sel(last, c), lt = sel(term, c), lh = sel(hw, c);
+    int v[R];
+#pragma unroll
+    for (int p = 0; p < R; ++p) v[p] = (p == c) ? ll : m[p];
+    int N = -1;
+#pragma unroll
+    for (int p = 0; p < R; ++p) {   // the (R/2+1)-th largest value
+      int cnt = 0;
+#pragma unroll
+      for (int q = 0; q < R; ++q) cnt += v[q] >= v[p] ? 1 : 0;
+      if (cnt >= R / 2 + 1 && v[p] > N) N = v[p];
+    }
+    if (N > cm) {
+      if (N < 1 || N > ll) { raise(F_PANIC_GETLOG); return cm; }
+      if (N <= lh - int(P.K)) { raise(F_RING_EVICTED); return cm; }
+      if (ring_term(P, c, N) == lt) {
+        st[S_COMMITTED] += N - cm;
+        return N;
+      }
+    }
+    return cm;
+  }
+
+  template <typename SrcF>
+  __device__ __forceinline__ void r_leader_round(const DevPlanes& P, const Trace& T, int c, const SrcF& make_src) {
+    const int lt = sel(term, c), ll = sel(last, c), lc = sel(commit, c), lh = sel(hw, c);
+    const int K = int(P.K);
+    int m[R], nx[R];
+    uint32_t dirty = 0;
+    load_match(P, c, m);
+    load_next(P, c, nx);
+    const int pri = primary;   // row location of c as loaded (c may step down below)
+    const auto src0 = make_src(c);
+    bool stop = false;
+    static_for<R>([&](auto PI) {
+      constexpr int p = decltype(PI)::value;
+      if (p == c || stop || !alive()) return;
+      if (dropped(c, p)) { ++st[S_AE_FAIL]; return; }
+      const int nxt = nx[p];
+      if (nxt < 1 || nxt > ll + 1) { raise(F_PANIC_GETLOG); return; }
+      if (nxt <= lh - K) { raise(F_RING_EVICTED); return; }
+      AEReq q;
+      q.term = lt; q.lc = lc;
+      q.corrupt = corrupted(P, p);
+      q.prev_idx = nxt - 1;
+      q.prev_term = 0;
+      if (q.prev_idx > 0) {
+        if (q.prev_idx <= lh - K) { raise(F_RING_EVICTED); return; }
+        q.prev_term = ring_term(P, c, q.prev_idx);
+      }
+      q.n = ll - q.prev_idx;
+      auto src = src0;
+      src.from = nxt;
+      const AEResp a = r_deliver_ae<p>(P, T, q, src);
+      if (!alive()) return;
+      if (a.term > lt) { r_observe_rt(T, c, a.term); ++st[S_AE_FAIL]; stop = true; return; }
+      if (a.ok) {
+        m[p] = a.match; nx[p] = a.match + 1; dirty |= 1u << p;
+        ++st[S_AE_OK];
+      } else {
+        int nn = nx[p] - 1 < a.match + 1 ? nx[p] - 1 : a.match + 1;
+        nn = nn < 1 ? 1 : nn;
+        if (nn != nx[p]) { nx[p] = nn; dirty |= 1u << p; }
+        ++st[S_AE_FAIL];
+      }
+    });
+    if (alive() && !stop) {
+      const int nc = r_commit_rule(P, m, c, lc);
+      if (nc != lc) { put(commit, c, nc); d_commit |= 1u << c; }
+    }
+    // rows are written where they were read (c's rows are dead if it stepped down)
+    const int keep = primary;
+    primary = pri;
+    store_match(P, c, m, dirty);
+    store_next(P, c, nx, dirty);
+    primary = keep;
+  }
+
+  __device__ __forceinline__ void r_timeout_fire(const Trace& T, int c) {
+    const int t = sel(term, c);
+    if (t >= I32MAX) { raise(F_OVERFLOW); return; }
+    put(term, c, t + 1);
+    d_term |= 1u << c;
+    set_vote(c, c + 1);                            // votes for itself
     ++st[S_BUMPS];
     enter_candidate(T, c);
   }

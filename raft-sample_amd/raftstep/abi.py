@@ -8,10 +8,11 @@ import ctypes as C
 
 import numpy as np
 
-RAFT_ABI_VERSION = 2
+RAFT_ABI_VERSION = 3
 RAFT_MAX_REPLICAS = 8
 
 FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
+SEM_REF, SEM_RAFT = 0, 1
 ROLE_NAMES = {FOLLOWER: "follower", CANDIDATE: "candidate", LEADER: "leader"}  # main.go:51-57
 
 F_NONE, F_PANIC_GETLOG, F_DEADLOCK_VRES, F_DEADLOCK_LEADER_VREQ, F_RING_EVICTED, F_OVERFLOW = range(6)
@@ -79,11 +80,12 @@ class StateView(C.Structure):
         ("last", C.c_void_p), ("commit", C.c_void_p), ("deadline", C.c_void_p),
         ("timeout", C.c_void_p), ("match", C.c_void_p), ("fault", C.c_void_p),
         ("log_term", C.c_void_p), ("log_value", C.c_void_p), ("log_crc", C.c_void_p),
+        ("next", C.c_void_p), ("hwm", C.c_void_p),
     ]
 
 
 STATE_FIELDS = ("role", "voted", "term", "last", "commit", "deadline", "timeout",
-                "match", "fault", "log_term", "log_value", "log_crc")
+                "match", "fault", "log_term", "log_value", "log_crc", "next", "hwm")
 
 
 def state_shapes(groups, replicas, ring_depth):
@@ -95,6 +97,7 @@ def state_shapes(groups, replicas, ring_depth):
         "timeout": ((G, R), np.int32), "match": ((G, R, R), np.int32),
         "fault": ((G,), np.uint8), "log_term": ((G, R, K), np.int32),
         "log_value": ((G, R, K), np.int64), "log_crc": ((G, R, K), np.uint32),
+        "next": ((G, R, R), np.int32), "hwm": ((G, R), np.int32),
     }
 
 

@@ -86,14 +86,18 @@ def state_hash(st):
     return h.hexdigest()
 
 
-def group_hashes(st):
+def group_hashes(st, raft_fields=False):
     """Per-group digest (uint64) of every field — for per-tick trace diffs
-    (log_crc only when present and non-zero, i.e. with payload_crc on)."""
+    (log_crc only when present and non-zero, i.e. with payload_crc on;
+    next/hwm only with raft_fields: in REF mode they are derived from
+    match/last, and the committed golden digests predate them)."""
     G = st["fault"].shape[0]
     acc = np.zeros(G, dtype=np.uint64)
     mult = np.uint64(0x100000001B3)
     with np.errstate(over="ignore"):
         for k in abi.STATE_FIELDS:
+            if k in ("next", "hwm") and not raft_fields:
+                continue
             if k not in st or (k == "log_crc" and not st[k].any()):
                 continue
             a = np.ascontiguousarray(st[k]).reshape(G, -1).astype(np.int64).view(np.uint64)
