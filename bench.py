@@ -42,10 +42,16 @@ WORKLOADS = {
                desc="steady-state AppendEntries+commit, 2^21 groups per GPU (16M over 8 GPUs)"),
     "C5": dict(groups=1 << 20, entries=64, ring_depth=128, crc=1,
                desc="64-entry AppendEntries batches with per-entry CRC32C stamp+verify"),
+    # C4: NewNode start, seeded isolation churn (one replica of a group cut
+    # off for 8-32 ticks w.p. 1/8 per 32-tick epoch ~ 1/256 per tick), RAFT
+    # semantics (REF faults on a new leader's first contact, SURVEY KAT-11)
+    "C4": dict(groups=1 << 22, replicas=7, entries=1, ring_depth=128, crc=0, init="new", semantics=1, settle=48,
+               iso=(8192, 8, 32),
+               desc="NewNode start, isolation churn (elections, term bumps, truncation), RAFT semantics"),
 }
 
 
-def cpu_baseline(args, R, E, K, crc):
+def cpu_baseline(args, wl, R, E, K, crc):
     """The oracle (C restatement of main.go's handlers, oracle/) timed on the
     host cores on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -54,16 +60,32 @@ def cpu_baseline(args, R, E, K, crc):
     G, T = args.cpu_groups, args.cpu_ticks
     if E > 1:   # keep the sample's CPU time and memory bounded for big batches
         G, T = max(1024, 4 * G // E), max(16, T // 4)
-    o = oracle.Oracle(replicas=R, groups=G, ring_depth=K, client_period=1, entries_per_tick=E,
-                      payload_crc=crc, seed=0x5EED0002)
-    o.init_steady(0, 0)
+    o = oracle.Oracle(**engine_kwargs(wl, R, G, 0, K, E, crc))
+    if wl.get("init") == "new":
+        G, T = G // 2, T // 2
+        o.close()
+        o = oracle.Oracle(**engine_kwargs(wl, R, G, 0, K, E, crc))
+        o.init_new_nodes(0)
+        o.tick(0, wl["settle"], threads=threads)
+        t_first, start = wl["settle"], "after a NewNode start and %d settle ticks" % wl["settle"]
+    else:
+        o.init_steady(0, 0)
+        t_first, start = 1, "steady state from init_steady"
     t0 = time.perf_counter()
-    o.tick(1, T, threads=threads)
+    o.tick(t_first, T, threads=threads)
     dt = time.perf_counter() - t0
     o.close()
     return {"value": G * T / dt, "unit": "group-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{G} groups x {T} ticks, R={R}, E={E}, crc={crc}, steady state from init_steady, "
+            "sample": f"{G} groups x {T} ticks, R={R}, E={E}, crc={crc}, {start}, "
                       f"{threads} pthreads over contiguous group ranges ({dt:.2f} s)"}
+
+
+def engine_kwargs(wl, R, G, base, K, E, crc):
+    kw = dict(replicas=R, groups=G, group_base=base, ring_depth=K, entries_per_tick=E, client_period=1,
+              payload_crc=crc, seed=wl.get("seed", 0x5EED0002), semantics=wl.get("semantics", 0))
+    if "iso" in wl:
+        kw.update(isolate_per_65536=wl["iso"][0], isolate_min_ticks=wl["iso"][1], isolate_max_ticks=wl["iso"][2])
+    return kw
 
 
 def load_pmc(workload):
@@ -86,7 +108,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--groups-per-gpu", type=int, default=None)
-    ap.add_argument("--replicas", type=int, default=R_DEFAULT)
+    ap.add_argument("--replicas", type=int, default=None)
     ap.add_argument("--entries", type=int, default=None)
     ap.add_argument("--ring-depth", type=int, default=None)
     ap.add_argument("--leader", type=int, default=0, help="steady-state leader replica (-1: hashed per group)")
@@ -119,19 +141,23 @@ def main():
     from raftstep import Engine, STAT_NAMES
 
     wl = WORKLOADS[args.workload]
-    R = args.replicas
+    R = args.replicas or wl.get("replicas", R_DEFAULT)
     G = args.groups_per_gpu or wl["groups"]
     E = args.entries or wl["entries"]
     K = args.ring_depth or wl["ring_depth"]
     crc = wl["crc"]
-    eng = Engine(replicas=R, groups=G, group_base=rank * G, ring_depth=K, entries_per_tick=E, client_period=1,
-                 payload_crc=crc, seed=0x5EED0002, device=local)
+    churn = wl.get("init") == "new"
+    eng = Engine(device=local, **engine_kwargs(wl, R, G, rank * G, K, E, crc))
     if dist is not None and not same_dev:
         from raftstep import dist as rdist
         eng.comm_init(world, rank, rdist.exchange_comm_id(dist, rank, Engine.comm_unique_id))
-    eng.init_steady(args.leader, 0)
-
-    tick = 1
+    if churn:   # NewNode start; the first elections happen in untimed settle ticks
+        eng.init_new_nodes(0)
+        eng.tick(0, wl["settle"], stats=False)
+        tick = wl["settle"]
+    else:
+        eng.init_steady(args.leader, 0)
+        tick = 1
     if args.warmup:
         eng.tick(tick, args.warmup, stats=True)
         tick += args.warmup
@@ -159,9 +185,14 @@ def main():
     total_steps = G * world * args.steps
     value = total_steps / elapsed
     # correctness guard on the timed run: the steady state commits exactly one
-    # entry per group per tick and never faults
+    # entry per group per tick and never faults; under churn nothing faults
+    # and most groups have a leader
     expect_commit = G * world * args.steps * E
-    ok = stats[STAT_NAMES.index("committed")] == expect_commit and stats[STAT_NAMES.index("faults")] == 0
+    faults = stats[STAT_NAMES.index("faults")]
+    if churn:
+        ok = faults == 0 and stats[STAT_NAMES.index("leader_groups")] > 0.5 * G * world * args.steps
+    else:
+        ok = stats[STAT_NAMES.index("committed")] == expect_commit and faults == 0
 
     B = algorithmic_bytes(R, E, crc)
     avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)   # region events / launches: tick kernel + gaps
@@ -180,10 +211,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic (seeded splitmix64 trace; post-election steady state, SURVEY.md §8(d) C2)",
+        "data": "synthetic (seeded splitmix64 trace; %s, SURVEY.md §8(d) %s)"
+                % ("NewNode start + isolation churn" if churn else "post-election steady state", args.workload),
         "config": {"workload": workload, "groups_per_gpu": G, "groups_total": G * world, "replicas": R,
                    "entries_per_tick": E, "ring_depth": K, "payload_crc32c": bool(crc), "leader": args.leader,
-                   "semantics": "REF (main.go)", "parallelism": f"group-sharded x{world}"},
+                   "semantics": "RAFT (EXT, Raft paper)" if wl.get("semantics") else "REF (main.go)",
+                   "parallelism": f"group-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_group_step": B, "avg_kernel_us": avg_kernel_s * 1e6, "launches": launches},
@@ -191,7 +224,7 @@ def main():
         "stats_check": bool(ok),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, R, E, K, crc)
+        result["cpu_baseline"] = cpu_baseline(args, wl, R, E, K, crc)
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:

@@ -416,7 +416,9 @@ static int r_deliver_vr(const o_ctx* c, o_group* G, int x, int64_t term, int can
   return 0;
 }
 
-/* On failure res.match is the hint H: the leader retries from min(next-1, H+1). */
+/* On failure res.match is the hint H: the leader retries from min(next-1, H+1).
+ * H = last (log too short), min(prevLogIndex-1, commitIndex) (term conflict),
+ * prevLogIndex (EXT payload CRC mismatch). */
 static o_aer r_deliver_ae(const o_ctx* c, o_group* G, int x, const o_ae* r) {
   o_node* n = &G->n[x];
   r_observe_term(c, G, x, r->term);
@@ -433,7 +435,10 @@ static o_aer r_deliver_ae(const o_ctx* c, o_group* G, int x, const o_ae* r) {
   if (r->prev_idx > 0) {
     int64_t t;
     if (!get_log_term(c, G, n, r->prev_idx, &t)) return res;
-    if (t != r->prev_term) { res.match = r->prev_idx - 1; return res; }
+    /* conflict: hint = min(prevLogIndex-1, commitIndex) -- the committed prefix
+       matches every later leader's log (Leader Completeness), so the leader
+       can jump back there in one step instead of one entry per round */
+    if (t != r->prev_term) { res.match = r->prev_idx - 1 < n->commit ? r->prev_idx - 1 : n->commit; return res; }
   }
   if (c->cfg->payload_crc) {                       /* EXT: verify what will be stored */
     int64_t j0 = r->n > (int64_t)c->cfg->ring_depth ? r->n - (int64_t)c->cfg->ring_depth : 0;

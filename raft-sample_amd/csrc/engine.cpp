@@ -74,6 +74,11 @@ uint32_t host_entry_crc(int32_t term, int64_t value) {
            T[768 + (hi & 255)] ^ T[512 + ((hi >> 8) & 255)] ^ T[256 + ((hi >> 16) & 255)] ^ T[hi >> 24]);
 }
 
+// Device ring layout (raft_device.hpp ring_slot_off): [R][Gp/64][K][64].
+inline uint64_t ring_index(uint64_t r, uint64_t g, uint64_t s, uint64_t K, uint64_t Gp) {
+  return r * K * Gp + ((g >> 6) * K + s) * 64 + (g & 63);
+}
+
 bool fits32(int64_t v) { return v >= -int64_t(I32) - 1 && v <= int64_t(I32); }
 
 }  // namespace
@@ -473,7 +478,8 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
       // deadline = effective timer start + d; followers/candidates also count hb
       if (v->deadline) v->deadline[c] = (role == ROLE_L ? ts[d] : std::max(ts[d], hb[g])) + int32_t(rs[d] >> 6);
       if (v->timeout) v->timeout[c] = int32_t(rs[d] >> 6);
-      const int32_t hwm = raft ? hw[d] : last[d];
+      // RAFT + MSYNC: high-water marks and the primary's NextIndex row are implicit too
+      const int32_t hwm = (raft && !msync) ? hw[d] : last[d];
       if (v->hwm) v->hwm[c] = hwm;
       if (v->match)
         for (uint64_t p = 0; p < R; ++p) {
@@ -486,13 +492,13 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
         for (uint64_t p = 0; p < R; ++p) {
           int32_t nx = 0;
           if (role == ROLE_L && p != r) {
-            if (raft) nx = (int(r) == primary) ? ln[p * Gp + g] : xn[(r * R + p) * Gp + g];
+            if (raft) nx = (int(r) == primary) ? (msync ? last[p * Gp + g] + 1 : ln[p * Gp + g]) : xn[(r * R + p) * Gp + g];
             else nx = ((int(r) == primary) ? (msync ? last[p * Gp + g] : lm[p * Gp + g]) : xm[(r * R + p) * Gp + g]) + 1;
           }
           v->next[c * R + p] = nx;
         }
       if (logs && last[d] > 0) {
-        const int32_t want = lt[(r * K + uint64_t((last[d] - 1) & int64_t(K - 1))) * Gp + g];
+        const int32_t want = lt[ring_index(r, g, uint64_t((last[d] - 1) & int64_t(K - 1)), K, Gp)];
         if (ltm[d] != want)
           return fail(RAFT_EINVAL, "internal: last-entry term cache of group %llu replica %llu is %d, ring says %d",
                       (unsigned long long)g, (unsigned long long)r, ltm[d], want);
@@ -503,7 +509,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
           // slot s holds the largest index i <= l with (i-1) mod K == s
           int64_t idx = l >= 1 ? l - ((l - 1 - int64_t(s)) & int64_t(K - 1)) : 0;
           const bool live = idx >= 1 && idx <= l && idx > int64_t(hwm) - int64_t(K);
-          const uint64_t o = (r * K + s) * Gp + g;
+          const uint64_t o = ring_index(r, g, s, K, Gp);
           if (v->log_term) v->log_term[c * K + s] = live ? lt[o] : 0;
           if (v->log_value) v->log_value[c * K + s] = live ? lv[o] : 0;
           if (v->log_crc) v->log_crc[c * K + s] = (live && crcs) ? lcrc[o] : 0u;
@@ -575,10 +581,10 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
         hw[d] = h;
       }
       for (uint64_t s = 0; s < K; ++s) {
-        lt[(r * K + s) * Gp + g] = v->log_term[c * K + s];
-        lv[(r * K + s) * Gp + g] = v->log_value[c * K + s];
+        lt[ring_index(r, g, s, K, Gp)] = v->log_term[c * K + s];
+        lv[ring_index(r, g, s, K, Gp)] = v->log_value[c * K + s];
         if (e->cfg.payload_crc)
-          lcrc[(r * K + s) * Gp + g] = v->log_crc ? v->log_crc[c * K + s]
+          lcrc[ring_index(r, g, s, K, Gp)] = v->log_crc ? v->log_crc[c * K + s]
                                                   : host_entry_crc(v->log_term[c * K + s], v->log_value[c * K + s]);
       }
       if (v->last[c] > 0) ltm[d] = v->log_term[c * K + uint64_t((v->last[c] - 1) & int64_t(K - 1))];
@@ -634,9 +640,8 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       b = next_event(e);
       if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
     }
-    // RAFT mode has no steady-state fast path yet: every group takes the general kernel
-    const int force = e->force_general || e->cfg.semantics == RAFT_SEM_RAFT;
-    HIPCHK(launch_tick_fast(e->R, e->P, T, st, e->work, e->work_tick, cnt, force, e->write_through,
+    const int force = e->force_general;
+    HIPCHK(launch_tick_fast(e->R, int(e->cfg.semantics), e->P, T, st, e->work, e->work_tick, cnt, force, e->write_through,
                             e->stream, a, b));
     // deferred groups catch up every slow_every ticks and at the end of the call
     if ((i + 1) % e->slow_every == 0 || i + 1 == nticks) {

@@ -1,0 +1,283 @@
+// k_fast.hip — the steady-state tick kernel (the metric path).
+#include "tick_common.hpp"
+
+namespace raftstep {
+
+// ---------------------------------------------------------------------------
+// Steady-state tick (the metric path). A group qualifies when it is STEADY
+// (not frozen, its only leader is its primary, every other replica a
+// follower), no EXT isolation touches it this tick, and every peer's
+// MatchIndex equals the leader's LastApplied (NextIndex = LastApplied+1).
+// For such a group the tick is exactly: client append (main.go:327-329),
+// one AppendEntries per follower carrying just this tick's entries
+// (main.go:341-372 -> 121-156), the responses (main.go:375-378) and the
+// commit rule (main.go:381-391). Every follower's timer is reset by its
+// AppendEntries (main.go:124-127) — recorded once per group as hb = now —
+// so no timer can expire. Anything else, or any condition on the way that
+// would fault or need a ring read, defers the group to the general kernel
+// (worklist + DEFER flag) before a single store; a DEFERred group is left
+// alone until the general kernel has caught it up.
+// MSYNC: after a fast tick every follower's MatchIndex equals its
+// LastApplied (main.go:156 -> 376), so the row is kept implicit.
+// Store policy of the fast kernel: plain (write-back L2) or write-through
+// (agent-scope relaxed atomic store = global_store ... sc1, which drops the
+// line from L2 so that less dirty data is left for the end-of-kernel flush).
+template <bool WT, typename T>
+__device__ __forceinline__ void st(T* base, uint32_t idx, T v) {
+  if constexpr (WT) __hip_atomic_store(&at(base, idx), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else at(base, idx) = v;
+}
+
+template <int R, bool WT, bool CRC, int SEM>
+__global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, unsigned long long* stats,
+                                                        uint32_t* work, int32_t* work_tick, uint32_t* work_count,
+                                                        int force_slow) {
+  constexpr bool RAFT = SEM == SEM_RAFT;
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  // EXT CRC32C tables (8 KiB) staged in LDS for the stamp/verify lookups
+  __shared__ uint32_t tab[CRC ? 2048 : 1];
+  if constexpr (CRC) {
+    const uint4* src = reinterpret_cast<const uint4*>(P.crc_tab);
+    uint4* dst = reinterpret_cast<uint4*>(tab);
+    dst[threadIdx.x] = src[threadIdx.x];
+    dst[threadIdx.x + 256] = src[threadIdx.x + 256];
+    __syncthreads();
+  }
+  int sv[4] = {0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups
+  bool bail = false;
+  if (g < P.G) {
+    const int meta = at(P.gmeta, g);
+    const int c = meta & 0xF;
+    const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
+    bail = !skip && (force_slow || !(meta & M_STEADY));
+    int term[R], last[R], commit[R], lt[R], m[R];
+    const bool go = !skip && !bail;
+    if (go) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        term[r] = at(prow(P.term, r, P.Gp), g);
+        last[r] = at(prow(P.last, r, P.Gp), g);
+        commit[r] = at(prow(P.commit, r, P.Gp), g);
+        lt[r] = at(prow(P.lterm, r, P.Gp), g);
+      }
+      if (meta & M_MSYNC) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) m[r] = (r != c) ? last[r] : 0;
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) m[r] = (r != c) ? at(prow(P.lmatch, r, P.Gp), g) : 0;
+        if constexpr (RAFT) {
+          // RAFT rows kept explicitly: NextIndex must be MatchIndex+1 and no
+          // log may be shorter than its high-water mark (no pending truncation)
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            if (r != c) bail |= at(prow(P.lnext, r, P.Gp), g) != m[r] + 1;
+            bail |= at(prow(P.hwm, r, P.Gp), g) != last[r];
+          }
+        }
+      }
+    }
+    const int n = int(T.client_entries());
+    uint64_t key = 0;
+    if (go && (T.iso_p || n)) key = group_key(T.seed, P.gbase + g);
+    if (go && T.iso_p) bail |= isolation_mask<R>(key, T) != 0;
+    // leader view
+    const int Lt = sel(term, c), Ll = sel(last, c), Lc = sel(commit, c), Llt = sel(lt, c);
+    if (go && !bail) bail = int64_t(Ll) + n > I32MAX || n >= int(P.K);
+    if (go) {
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        bail |= (p != c) && m[p] != Ll;
+        // RAFT: a follower with extra entries or another term takes the general path
+        if constexpr (RAFT) bail |= (p != c) && (last[p] != Ll || term[p] != Lt);
+      }
+    }
+    // one AppendEntries shape for every peer (NextIndex == Ll+1)
+    int prev_idx, prev_term;
+    if constexpr (RAFT) { prev_idx = Ll; prev_term = Ll > 0 ? Llt : 0; }   // log[nextIndex-1].term
+    else if (n == 0 || Ll == 0) { prev_idx = Ll; prev_term = Lt; }          // REF heartbeat / whole-log
+    else { prev_idx = Ll; prev_term = Llt; }                                 // GetLog(MatchIndex).Term
+    // EXT: every follower verifies the CRC32C stamp of each entry it received
+    // (the term's CRC state is shared, the term bytes are never corrupted)
+    uint32_t crcbad = 0;
+    if constexpr (CRC) {
+      if (go && !bail && n) {
+        uint32_t cm = 0;   // followers whose message is corrupted this tick
+#pragma unroll
+        for (int p = 0; p < R; ++p)
+          if (p != c && P.corrupt_p && (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(T.tick)) & 0xFFFF) < P.corrupt_p)
+            cm |= 1u << p;
+        const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+        const uint32_t cs = crc_term_state(tab, Lt);
+        for (int e = 0; e < n; ++e) {
+          const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+          const uint32_t stamp = crc_value_final(tab, cs, v);               // leader's stamp
+#pragma unroll
+          for (int p = 0; p < R; ++p) {
+            if (p == c) continue;
+            const int64_t rv = v ^ ((((cm >> p) & 1u) && e == n - 1) ? 1 : 0);  // what p received
+            if (crc_value_final(tab, cs, rv) != stamp) crcbad |= 1u << p;
+          }
+        }
+      }
+    }
+    uint32_t okm = 0, cch = 0, mch = 0, ltch = 0;
+    if (go && !bail) {
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        if (p == c) continue;
+        const int l = last[p];
+        bool ok;
+        if constexpr (RAFT) {
+          // same term (checked), log exactly as long as the leader's before this tick
+          if (l > 0 && lt[p] != prev_term) bail = true;           // conflict: hint + backoff path
+          if ((crcbad >> p) & 1u) bail = true;                    // rejected payload: backoff path
+          ok = true;
+        } else {
+          ok = Lt >= term[p];                                     // main.go:129-133
+          if (ok && l > 0) {                                      // main.go:135
+            if (int64_t(l) + n < prev_idx) ok = false;            // 137-140
+            else if (prev_idx < 1 || prev_idx > l || prev_idx <= l - int(P.K) || prev_idx != l) bail = true;
+            else ok = lt[p] == prev_term;                         // 142-145 (GetLog(l) == last entry)
+          }
+          if (ok && int64_t(l) + n > I32MAX) bail = true;
+          if (ok && ((crcbad >> p) & 1u)) ok = false;             // EXT: payload rejected
+        }
+        if (ok) {
+          const int nl = l + n;                                   // 148-149
+          last[p] = nl;
+          if (n && lt[p] != Lt) ltch |= 1u << p;
+          if (Lc > commit[p]) {                                   // 151-152
+            // REF: min(LC, len(Log)+1); RAFT: min(leaderCommit, index of last new entry)
+            const int cap = RAFT ? nl : nl + 1;
+            const int nc = Lc < cap ? Lc : cap;
+            if (nc != commit[p]) { commit[p] = nc; cch |= 1u << p; }
+          }
+          if (nl != m[p]) { m[p] = nl; mch |= 1u << p; }          // 156 -> 375-377
+          okm |= 1u << p;
+        }
+      }
+    }
+    if (go && !bail) {
+      int cm = Lc;
+      bool sync = true;
+      if constexpr (RAFT) {
+        // every log now ends at Ll+n: the majority index is Ll+n, committed
+        // only if that entry is of the current term (this tick's entries are)
+        const int N = Ll + n;
+        if (N > Lc && (n > 0 || Llt == Lt)) cm = N;
+      } else {
+        // commit rule (main.go:381-391)
+#pragma unroll
+        for (int p = 0; p < R; ++p) {
+          int cnt = 0;
+#pragma unroll
+          for (int q = 0; q < R; ++q) cnt += (q != c && m[q] == m[p]) ? 1 : 0;
+          if (p != c && 2 * cnt > R && m[p] > cm) cm = m[p];
+          sync &= (p == c) || m[p] == last[p];
+        }
+      }
+      sv[0] = cm - Lc;
+      sv[1] = __builtin_popcount(okm);
+      sv[2] = (R - 1) - sv[1];
+      sv[3] = 1;
+      // ---- stores (no bail past this point) ----
+      if (n) {
+        st<WT>(P.last + uint64_t(c) * P.Gp, g, Ll + n);
+        if (Llt != Lt) st<WT>(P.lterm + uint64_t(c) * P.Gp, g, Lt);
+      }
+      if (cm != Lc) st<WT>(P.commit + uint64_t(c) * P.Gp, g, cm);
+      st<WT>(P.hb, g, T.now);                                     // timer.Reset(d) of every follower
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        if (p == c || !((okm >> p) & 1u)) continue;
+        if (n) st<WT>(prow(P.last, p, P.Gp), g, last[p]);
+        if (!sync && ((mch >> p) & 1u)) st<WT>(prow(P.lmatch, p, P.Gp), g, m[p]);
+        if ((cch >> p) & 1u) st<WT>(prow(P.commit, p, P.Gp), g, commit[p]);
+        if ((ltch >> p) & 1u) st<WT>(prow(P.lterm, p, P.Gp), g, Lt);
+        if (!RAFT && term[p] != Lt) st<WT>(prow(P.term, p, P.Gp), g, Lt);  // main.go:155
+      }
+      // RAFT: MSYNC also makes NextIndex (= match+1) and the high-water marks (= last) implicit
+      const int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
+      if (nm != meta) at(P.gmeta, g) = uint16_t(nm);
+      // this tick's entries: leader log + every follower that accepted
+      if (n) {
+        const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+        const uint64_t cb = uint64_t(c) * P.K * P.Gp;
+        uint32_t cs = 0;
+        if constexpr (CRC) cs = crc_term_state(tab, Lt);
+        for (int e = 0; e < n; ++e) {
+          const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+          const uint32_t o = ring_slot_off(g, P.K, uint32_t((Ll + e) & int(P.kmask)));
+          uint32_t stamp = 0;
+          if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+          st<WT>(P.log_term + cb, o, Lt);
+          st<WT>(P.log_value + cb, o, v);
+          if constexpr (CRC) st<WT>(P.log_crc + cb, o, stamp);
+#pragma unroll
+          for (int p = 0; p < R; ++p) {
+            if (p == c || !((okm >> p) & 1u)) continue;
+            const uint32_t op = ring_slot_off(g, P.K, uint32_t((last[p] - n + e) & int(P.kmask)));
+            const uint64_t pb = uint64_t(p) * P.K * P.Gp;
+            st<WT>(P.log_term + pb, op, Lt);
+            st<WT>(P.log_value + pb, op, v);
+            if constexpr (CRC) st<WT>(P.log_crc + pb, op, stamp);
+          }
+        }
+      }
+    }
+    if (bail) at(P.gmeta, g) = uint16_t(meta | M_DEFER);
+  }
+  // groups that need the general path go to the dense worklist: block-local
+  // prefix over the wave ballots, one atomic per block that defers anything
+  __shared__ uint32_t wn[4], wbase;
+  const uint64_t bm = __ballot(bail);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) wn[wave] = uint32_t(__popcll(bm));
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = wn[0] + wn[1] + wn[2] + wn[3];
+    wbase = tot ? atomicAdd(work_count, tot) : 0u;
+  }
+  __syncthreads();
+  if (bail) {
+    uint32_t off = wbase + uint32_t(__popcll(bm & ((1ull << lane) - 1ull)));
+    for (int w = 0; w < wave; ++w) off += wn[w];
+    work[off] = g;
+    work_tick[off] = int32_t(T.tick);
+  }
+  if (stats) {
+    const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
+    block_stats<4>(sv, idx, stats);
+  }
+}
+
+template <int R, bool WT, bool CRC, int SEM>
+static void launch_fast_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                          int32_t* work_tick, uint32_t* work_count, int force_slow, hipStream_t s, hipEvent_t a,
+                          hipEvent_t b) {
+  hipExtLaunchKernelGGL(tick_fast_kernel<R, WT, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, work,
+                        work_tick, work_count, force_slow);
+}
+hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                            int32_t* work_tick, uint32_t* work_count, int force_slow, int write_through, hipStream_t s,
+                            hipEvent_t ev_start, hipEvent_t ev_stop) {
+  const bool crc = P.crc_on != 0;
+#define RAFT_FAST(WT_, CRC_)                                                                                      \
+  if (sem == SEM_RAFT) {                                                                                           \
+    RAFT_DISPATCH_R(R, (launch_fast_t<RR, WT_, CRC_, SEM_RAFT>(P, T, stats, work, work_tick, work_count, force_slow, \
+                                                               s, ev_start, ev_stop)))                              \
+  } else {                                                                                                         \
+    RAFT_DISPATCH_R(R, (launch_fast_t<RR, WT_, CRC_, SEM_REF>(P, T, stats, work, work_tick, work_count, force_slow,  \
+                                                              s, ev_start, ev_stop)))                               \
+  }
+  if (write_through) {
+    if (crc) { RAFT_FAST(true, true); } else { RAFT_FAST(true, false); }
+  } else {
+    if (crc) { RAFT_FAST(false, true); } else { RAFT_FAST(false, false); }
+  }
+#undef RAFT_FAST
+  return hipGetLastError();
+}
+
+}  // namespace raftstep

@@ -1,0 +1,90 @@
+// k_init.hip — NewNode / post-election initialisation kernels and the
+// semantics dispatch of the general and handler launchers.
+#include "tick_common.hpp"
+
+namespace raftstep {
+
+// NewNode (main.go:59-76) + FollowerRun entry (main.go:113-115).
+template <int R>
+__global__ __launch_bounds__(256) void init_new_kernel(DevPlanes P, Trace T) {
+  const uint64_t g = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (g >= P.G) return;
+  const uint64_t key = group_key(T.seed, P.gbase + g);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint64_t i = uint64_t(r) * P.Gp + g;
+    const int d = T.f_min + int(uint32_t(rng_k(key, r, ST_TIMER_F, uint64_t(T.tick)) >> 32) % uint32_t(T.f_span));
+    P.term[i] = 0; P.last[i] = 0; P.commit[i] = 0;
+    P.tstart[i] = T.now;
+    P.rs[i] = uint16_t(ROLE_F | (uint32_t(d) << 6));   // vote 0 (REF: not voted; RAFT: votedFor none)
+    P.lterm[i] = 0;
+    if (P.hwm) P.hwm[i] = 0;
+  }
+  P.hb[g] = HB_NONE;
+  P.gmeta[g] = uint16_t(NO_PRIMARY);
+}
+
+// Post-election state (KAT-1 generalised).
+template <int R>
+__global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, int32_t leader) {
+  const uint64_t g = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (g >= P.G) return;
+  const uint64_t gid = P.gbase + g;
+  const uint64_t key = group_key(T.seed, gid);
+  const int L = leader >= 0 ? leader % R : int(uint32_t(sm64(T.seed ^ 0x1EADE5ULL ^ sm64(gid)) >> 33) % uint32_t(R));
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint64_t i = uint64_t(r) * P.Gp + g;
+    const bool isL = r == L;
+    const uint64_t h = rng_k(key, r, isL ? ST_TIMER_C : ST_TIMER_F, uint64_t(T.tick));
+    const int d = isL ? T.c_min + int(uint32_t(h >> 32) % uint32_t(T.c_span))
+                      : T.f_min + int(uint32_t(h >> 32) % uint32_t(T.f_span));
+    // REF: Voted = true; RAFT: everyone voted for L (votedFor + 1)
+    const uint32_t vote = P.hwm ? uint32_t(L + 1) : 1u;
+    P.term[i] = 1; P.last[i] = 0; P.commit[i] = 0;
+    P.tstart[i] = T.now;
+    P.rs[i] = uint16_t((isL ? ROLE_L : ROLE_F) | (vote << 2) | (uint32_t(d) << 6));
+    P.lmatch[i] = 0;
+    P.lterm[i] = 0;
+    if (P.hwm) {                       // RAFT mode: NextIndex = last + 1 = 1, high-water 0
+      P.lnext[i] = 1;
+      P.hwm[i] = 0;
+    }
+  }
+  P.hb[g] = HB_NONE;
+  P.gmeta[g] = uint16_t(L | (P.hwm ? 0 : M_MSYNC) | M_STEADY);
+}
+
+hipError_t launch_tick_slow_ref(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
+                                unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
+                                const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
+hipError_t launch_tick_slow_raft(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
+                                 unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
+                                 const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
+hipError_t launch_ops_ref(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n, const int32_t* et,
+                          const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s);
+hipError_t launch_ops_raft(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n, const int32_t* et,
+                           const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s);
+
+hipError_t launch_tick_slow(int R, int sem, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
+                            unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
+                            const uint32_t* work_count, uint32_t* next_count, hipStream_t s) {
+  return sem == SEM_RAFT
+             ? launch_tick_slow_raft(R, P, T0, first_tick, last_tick, stats, work, work_tick, work_count, next_count, s)
+             : launch_tick_slow_ref(R, P, T0, first_tick, last_tick, stats, work, work_tick, work_count, next_count, s);
+}
+hipError_t launch_ops(int R, int sem, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
+                      const int32_t* et, const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s) {
+  return sem == SEM_RAFT ? launch_ops_raft(R, P, T, ops, n, et, ev, ec, out, s)
+                         : launch_ops_ref(R, P, T, ops, n, et, ev, ec, out, s);
+}
+hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_t s) {
+  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(init_new_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P, T));
+  return hipGetLastError();
+}
+hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s) {
+  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(init_steady_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P, T, leader));
+  return hipGetLastError();
+}
+
+}  // namespace raftstep

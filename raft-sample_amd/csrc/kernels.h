@@ -1,4 +1,13 @@
 // kernels.h — host-side launchers and device argument records of the engine.
+//
+//  tick_fast_kernel<R,WT,CRC,SEM> (k_fast.hip): steady-state tick, one lane
+//        per group, HBM-bound (~233 B per group-step at R=5, E=1); groups it
+//        cannot take go to a worklist.
+//  tick_slow_kernel<R,SEM> (k_ref.hip / k_raft.hip): the general tick
+//        (elections, step-downs, faults, EXT drops) over the worklist.
+//  ops_kernel<R,SEM>: the message-level handler API (AppendEntries /
+//        RequestVote receivers, node steps) over distinct groups.
+//  init_*_kernel<R> (k_init.hip): NewNode state / post-election state.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,7 +39,7 @@ struct DevRes {
 
 // Steady-state fast kernel; groups it does not take are DEFERred to `work`.
 // ev_start/ev_stop (may be null) time the dispatch itself (hipExtLaunchKernel).
-hipError_t launch_tick_fast(int R, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                             int32_t* work_tick, uint32_t* work_count, int force_slow, int write_through, hipStream_t s,
                             hipEvent_t ev_start, hipEvent_t ev_stop);
 // General kernel: catches every worklisted group up to last_tick; zeroes `next_count`.

@@ -59,7 +59,7 @@ struct DevPlanes {
   int32_t* hwm;        // RAFT mode: [R][Gp] highest LastApplied ever (== last in REF)
   uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
   int32_t* lterm;      // [R][Gp] Log[len-1].Term: cached term of each replica's last entry
-  int32_t* log_term;   // Log.Term  ring
+  int32_t* log_term;   // Log.Term  ring, [R] x tiles [Gp/64][K][64] (ring_slot_off)
   int64_t* log_value;  // Log.Value ring
   uint32_t* log_crc;   // EXT: CRC32C stamp ring (payload_crc only)
   const uint32_t* crc_tab;  // 8 x 256 slice-by-8 CRC32C tables
@@ -71,6 +71,16 @@ struct DevPlanes {
   uint32_t K;          // ring depth (power of two)
   uint32_t kmask;
 };
+
+// Ring layout: each replica's ring is tiled by waves of 64 groups,
+// [R][Gp/64][K][64]: entry slot s of group g sits at ((g/64)*K + s)*64 + g%64.
+// Groups whose logs are in step (steady state) write one contiguous 256-B
+// term row / 512-B value row per wave and entry; groups whose log lengths
+// have drifted apart (churn) still stay inside one K*64-entry tile per wave
+// instead of scattering over K slabs of Gp entries (TLB misses).
+__device__ __forceinline__ uint32_t ring_slot_off(uint32_t g, uint32_t K, uint32_t slot) {
+  return ((g >> 6) * K + slot) * 64u + (g & 63u);
+}
 
 // Addressing: every access is a wave-uniform base (SGPRs: plane + replica
 // row, or replica ring) plus a 32-bit per-lane byte offset, so the compiler
@@ -249,11 +259,19 @@ struct Group {
 #pragma unroll
     for (int r = 0; r < R; ++r) dl[r] = with_deadlines ? eff_start(at(prow(P.tstart, r, P.Gp), g), r) + dur[r] : 0;
     known = with_deadlines ? (1u << R) - 1u : 0u;
-    // materialise a MatchIndex row that the fast kernel kept implicit
+    // materialise the rows the fast kernel kept implicit: MatchIndex = LastApplied
+    // (RAFT also NextIndex = LastApplied+1 and high-water mark = LastApplied)
     if ((meta0 & M_MSYNC) && primary < R) {
 #pragma unroll
-      for (int p = 0; p < R; ++p)
-        if (p != primary) at(prow(P.lmatch, p, P.Gp), g) = last[p];
+      for (int p = 0; p < R; ++p) {
+        if (p != primary) {
+          at(prow(P.lmatch, p, P.Gp), g) = last[p];
+          if constexpr (SEM == SEM_RAFT) at(prow(P.lnext, p, P.Gp), g) = last[p] + 1;
+        }
+        if constexpr (SEM == SEM_RAFT) {
+          if (hw[p] != last[p]) { hw[p] = last[p]; d_hw |= 1u << p; }
+        }
+      }
     }
   }
   __device__ __forceinline__ void store(const DevPlanes& P) const {
@@ -268,15 +286,29 @@ struct Group {
             uint16_t(((roles >> (2 * r)) & 3u) | (((votes >> (4 * r)) & 15u) << 2) | (uint32_t(dur[r]) << 6));
       if (SEM == SEM_RAFT && ((d_hw >> r) & 1u)) at(prow(P.hwm, r, P.Gp), g) = hw[r];
     }
+    // The primary leader stepped down while another replica leads: move that
+    // leader's rows into the coalesced primary planes so the group can take
+    // the steady-state kernel again (placement only; no state changes).
+    int pri = primary;
+    if (!fault && pri == NO_PRIMARY && ((roles >> 1) & 0x5555u)) {
+      const int nl = int(__builtin_ctz((roles >> 1) & 0x5555u)) >> 1;   // lowest-id leader
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        if (p == nl) continue;
+        at(prow(P.lmatch, p, P.Gp), g) = at(prow(P.xmatch, nl * R + p, P.Gp), g);
+        if constexpr (SEM == SEM_RAFT) at(prow(P.lnext, p, P.Gp), g) = at(prow(P.xnext, nl * R + p, P.Gp), g);
+      }
+      pri = nl;
+    }
     // DEFER and MSYNC are consumed by the general path; STEADY is recomputed
-    const bool steady = primary < R && role(primary) == ROLE_L && (roles & ~(3u << (2 * primary))) == 0u;
-    const int m = primary | (fault << 4) | (steady ? M_STEADY : 0);
+    const bool steady = pri < R && role(pri) == ROLE_L && (roles & ~(3u << (2 * pri))) == 0u;
+    const int m = pri | (fault << 4) | (steady ? M_STEADY : 0);
     if (m != meta0) at(P.gmeta, g) = uint16_t(m);
   }
 
   // Log ring of replica r: entry idx (1-based) at slot (idx-1) mod K.
   __device__ __forceinline__ uint32_t ring_off(const DevPlanes& P, int idx) const {
-    return uint32_t((idx - 1) & int(P.kmask)) * uint32_t(P.Gp) + g;
+    return ring_slot_off(g, P.K, uint32_t((idx - 1) & int(P.kmask)));
   }
   __device__ __forceinline__ int32_t& ring_term(const DevPlanes& P, int r, int idx) const {
     return at(P.log_term + uint64_t(r) * P.K * P.Gp, ring_off(P, idx));
@@ -650,6 +682,9 @@ struct Group {
   }
 
   // On failure res.match is the hint H: the leader retries from min(next-1, H+1).
+  // H = last (log too short), min(prevLogIndex-1, commitIndex) on a term
+  // conflict (the committed prefix matches every later leader's log), or
+  // prevLogIndex on an EXT payload CRC mismatch.
   template <int Rp, typename Src>
   __device__ __forceinline__ AEResp r_deliver_ae(const DevPlanes& P, const Trace& T, const AEReq& q,
                                                  const Src& src) {
@@ -664,7 +699,10 @@ struct Group {
     if (q.prev_idx > l) return res;               // log too short: hint = last
     if (q.prev_idx > 0) {
       if (q.prev_idx <= hw[Rp] - K) { raise(F_RING_EVICTED); return res; }
-      if (ring_term(P, Rp, q.prev_idx) != q.prev_term) { res.match = q.prev_idx - 1; return res; }
+      if (ring_term(P, Rp, q.prev_idx) != q.prev_term) {     // conflict: back off to the committed prefix
+        res.match = q.prev_idx - 1 < commit[Rp] ? q.prev_idx - 1 : commit[Rp];
+        return res;
+      }
     }
     if (P.crc_on) {                               // EXT: verify what will be stored
       const int j0 = q.n > K ? q.n - K : 0;
@@ -875,7 +913,7 @@ struct TickSrc {
       if (crc_on) c = crc_entry(tab, t, v);   // the leader's stamp of its own fresh entry
     } else {
       const uint64_t rb = uint64_t(leader) * K * Gp;
-      const uint32_t o = uint32_t((idx - 1) & int(kmask)) * uint32_t(Gp) + g;
+      const uint32_t o = ring_slot_off(g, K, uint32_t((idx - 1) & int(kmask)));
       t = at(lt + rb, o);
       v = at(lv + rb, o);
       if (crc_on) c = at(lc + rb, o);

@@ -1,0 +1,172 @@
+// tick_common.hpp — device code shared by the kernel translation units:
+// EXT isolation windows, wave/block statistic reductions, the general tick
+// (run_tick) and the R-dispatch macro of the host launchers.
+#pragma once
+#include "kernels.h"
+
+#include <hip/hip_ext.h>
+
+#include <algorithm>
+
+namespace raftstep {
+
+// EXT isolation windows (same definition as oracle_isolated()).
+template <int R>
+__device__ __forceinline__ uint32_t isolation_mask(uint64_t key, const Trace& T) {
+  uint32_t mask = 0;
+  const int64_t ep = T.tick >> 5;
+  for (int64_t e = ep; e >= ep - 1 && e >= 0; --e) {
+    const uint64_t h = rng_k(key, 0, ST_ISOLATE, uint64_t(e));
+    if ((h & 0xFFFF) >= T.iso_p) continue;
+    const uint32_t victim = uint32_t((h >> 16) & 0xFF) % uint32_t(R);
+    const int64_t start = e * 32 + int64_t((h >> 24) & 31);
+    const int64_t len = int64_t(T.iso_min) + int64_t(uint32_t(h >> 32) % T.iso_span);
+    if (T.tick >= start && T.tick < start + len) mask |= 1u << victim;
+  }
+  return mask;
+}
+
+// Sum of one small per-lane counter over the wave. Counters are almost
+// always in [0,15]: four ballots + scalar popcounts; otherwise a shuffle tree.
+__device__ __forceinline__ long long wave_sum(int v) {
+  if (__all((unsigned)v < 16u)) {
+    long long s = __popcll(__ballot(v & 1));
+    s += 2ll * __popcll(__ballot(v & 2));
+    s += 4ll * __popcll(__ballot(v & 4));
+    s += 8ll * __popcll(__ballot(v & 8));
+    return s;
+  }
+  long long x = v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+template <int R, int SEM>
+__device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, const Trace& T, uint32_t E) {
+  if (T.iso_p) G.iso = isolation_mask<R>(G.key, T);
+
+  // 1. client: every Leader receives E NewLogRequests (main.go:87-93 -> 327-329).
+  if (E) {
+    static_for<R>([&](auto RI) {
+      constexpr int r = decltype(RI)::value;
+      if (G.role(r) != ROLE_L || !G.alive()) return;
+      const uint64_t vb = rng_k(G.key, r, ST_VALUE, uint64_t(G.tick));
+      const int l = G.last[r];
+      const int room = I32MAX - l;
+      const int n_ok = int(E) <= room ? int(E) : room;
+      if (G.cache_leader < 0) {
+        G.cache_leader = r; G.cache_from = l + 1; G.cache_term = G.term[r]; G.cache_vbase = vb;
+      }
+      const int e0 = n_ok > int(P.K) ? n_ok - int(P.K) : 0;   // only the last K stay in the ring
+      for (int e = e0; e < n_ok; ++e) {
+        const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+        G.ring_term(P, r, l + 1 + e) = G.term[r];
+        G.ring_value(P, r, l + 1 + e) = v;
+        if (P.crc_on) G.ring_crc(P, r, l + 1 + e) = crc_entry(P.crc_tab, G.term[r], v);
+      }
+      if (n_ok) {
+        G.last[r] = l + n_ok;
+        G.d_last |= 1u << r;
+        at(prow(P.lterm, r, P.Gp), G.g) = G.term[r];
+        if constexpr (SEM == SEM_RAFT) G.template r_grew<r>(l + n_ok);
+      }
+      if (n_ok < int(E)) G.raise(F_OVERFLOW);
+    });
+  }
+
+  // 2. rounds in ascending replica id, against the roles as they are now.
+  const TickSrc base{P.log_term, P.log_value, P.log_crc, P.crc_tab, P.crc_on, P.Gp, G.g, P.K, P.kmask, 0, 1,
+                     G.cache_leader, G.cache_from, G.cache_term, G.cache_vbase};
+  auto make_src = [base](int c) {
+    TickSrc s = base;
+    s.leader = c;
+    return s;
+  };
+  int c = -1;
+  while (G.alive()) {
+    const uint32_t active = (G.roles | (G.roles >> 1)) & 0x5555u;  // bit 2r: role(r) != Follower
+    const uint32_t rest = active & ~((1u << (2 * c + 2)) - 1u);    // replicas after c (c=-1: all)
+    if (!rest) break;
+    c = int(__builtin_ctz(rest)) >> 1;
+    if constexpr (SEM == SEM_RAFT) {
+      if (G.role(c) == ROLE_L) G.r_leader_round(P, T, c, make_src);
+      else G.r_candidate_round(P, T, c);
+    } else {
+      if (G.role(c) == ROLE_L) G.leader_round(P, T, c, make_src);  // main.go:332-391
+      else G.candidate_round(P, T, c);                             // main.go:253-284
+    }
+  }
+
+  // 3. expired election timers in (deadline, id) order; each new candidate
+  //    runs its vote round at once (main.go:171-177, 248-251 -> 253-284).
+#pragma unroll 1
+  for (int it = 0; it < R && G.alive(); ++it) {
+    int best = -1, bdl = 0;
+    static_for<R>([&](auto RI) {
+      constexpr int r = decltype(RI)::value;
+      if (G.role(r) == ROLE_L) return;
+      const int d = G.template deadline_of<r>(P);
+      if (d <= G.now && (best < 0 || d < bdl)) { best = r; bdl = d; }
+    });
+    if (best < 0) break;
+    if constexpr (SEM == SEM_RAFT) G.r_timeout_fire(T, best);
+    else G.timeout_fire(T, best);
+    if (!G.alive()) break;
+    if constexpr (SEM == SEM_RAFT) G.r_candidate_round(P, T, best);
+    else G.candidate_round(P, T, best);
+  }
+
+  if (!G.alive()) {
+    ++G.st[S_FAULTS];
+  } else if ((G.roles >> 1) & ~G.roles & 0x5555u) {
+    ++G.st[S_LEADER_GROUPS];
+  }
+}
+
+// Block-level sum of per-lane counters into the tick's stats slot (one
+// device-scope atomic per non-zero counter per block, spread over
+// STAT_SLOTS slots).
+template <int N>
+__device__ __forceinline__ void block_stats(const int (&v)[N], const int (&idx)[N], unsigned long long* stats) {
+  __shared__ long long red[N][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int s = 0; s < N; ++s) {
+    const long long w = wave_sum(v[s]);
+    if (lane == 0) red[s][wave] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < N) {
+    const int s = threadIdx.x;
+    const long long x = red[s][0] + red[s][1] + red[s][2] + red[s][3];
+    int which = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) which = (s == k) ? idx[k] : which;
+    if (x) atomicAdd(&stats[(blockIdx.x % STAT_SLOTS) * NSTAT + which], (unsigned long long)x);
+  }
+}
+
+template <int R, typename F>
+__device__ __forceinline__ void with_replica(int x, F&& f) {
+  static_for<R>([&](auto PI) {
+    if (x == decltype(PI)::value) f(PI);
+  });
+}
+
+#define RAFT_DISPATCH_R(R_, CALL)                                              \
+  switch (R_) {                                                                \
+    case 1: { constexpr int RR = 1; CALL; } break;                             \
+    case 2: { constexpr int RR = 2; CALL; } break;                             \
+    case 3: { constexpr int RR = 3; CALL; } break;                             \
+    case 4: { constexpr int RR = 4; CALL; } break;                             \
+    case 5: { constexpr int RR = 5; CALL; } break;                             \
+    case 6: { constexpr int RR = 6; CALL; } break;                             \
+    case 7: { constexpr int RR = 7; CALL; } break;                             \
+    case 8: { constexpr int RR = 8; CALL; } break;                             \
+    default: return hipErrorInvalidValue;                                      \
+  }
+
+static inline dim3 grid_for(uint64_t n) { return dim3(unsigned((n + 255) / 256)); }
+
+}  // namespace raftstep

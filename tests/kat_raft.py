@@ -90,11 +90,14 @@ def raft04_keep_matching(make):
 
 def raft05_consistency_failures(make):
     """Log too short -> false with hint = last; term mismatch at prevLogIndex ->
-    false with hint = prevLogIndex-1; stale term -> false, timer untouched."""
+    false with hint = min(prevLogIndex-1, commitIndex); stale term -> false,
+    timer untouched."""
     e = _impl(make, 3)
-    e.load_state(_state([node(F, 1, 0, [(1, 1), (1, 2)], deadline=40, timeout=11), node(), node()], 3))
-    assert _ae(e, 4, 0, term=1, prev_idx=5, prev_term=1) == (0, 2, 1, 0)
-    assert _ae(e, 4, 0, term=1, prev_idx=2, prev_term=2) == (0, 1, 1, 0)
+    e.load_state(_state([node(F, 1, 0, [(1, 1), (1, 2), (1, 3)], commit=1, deadline=40, timeout=11), node(),
+                         node()], 3))
+    assert _ae(e, 4, 0, term=1, prev_idx=5, prev_term=1) == (0, 3, 1, 0)
+    assert _ae(e, 4, 0, term=1, prev_idx=2, prev_term=2) == (0, 1, 1, 0)    # min(1, commit 1)
+    assert _ae(e, 4, 0, term=1, prev_idx=3, prev_term=2) == (0, 1, 1, 0)    # min(2, commit 1)
     assert e.store_state()["deadline"][0, 0] == 8 + 11      # both reset the timer (current leader)
     e2 = _impl(make, 3)
     e2.load_state(_state([node(F, 4, 0, [(4, 1)], deadline=40, timeout=11), node(), node()], 3))

@@ -124,6 +124,10 @@ TRACES = {
     "raft_crc_corrupt": (dict(replicas=5, groups=200, client_period=1, entries_per_tick=8, ring_depth=64,
                               payload_crc=1, corrupt_per_65536=4000, isolate_per_65536=8000, seed=0xC5),
                          "new", 0, 120, 4),
+    # bench.py's C4 workload parameters (R=7, K=64, 8-32 tick isolations at 1/8 per epoch) on 2048 groups
+    "raft_c4_shape": (dict(replicas=7, groups=2048, client_period=1, seed=0x5EED0002, ring_depth=64,
+                           isolate_per_65536=8192, isolate_min_ticks=8, isolate_max_ticks=32),
+                      "new", 0, 400, 25),
     "raft_r1": (dict(replicas=1, groups=64, client_period=1, seed=1), "new", 0, 60, 5),
     "raft_r2": (dict(replicas=2, groups=64, client_period=1, seed=2, isolate_per_65536=9000), "new", 0, 80, 5),
     "raft_r4": (dict(replicas=4, groups=300, client_period=1, seed=4, isolate_per_65536=9000), "new", 0, 120, 5),
