@@ -151,6 +151,28 @@ int raft_init_steady(raft_engine* e, int32_t leader, int64_t tick0);
 int raft_load_state(raft_engine* e, const raft_state_view* v);
 int raft_store_state(raft_engine* e, raft_state_view* v);
 
+/* ---- audit: digests, nodelog, checkpoints ---------------------------------
+ * raft_state_digest: per-group 64-bit digest of the canonical view that
+ * raft_store_state would return (splitmix64 chain keyed by the global group
+ * id; words listed in oracle/raft_oracle.c oracle_state_digest), computed on
+ * the device without copying the state out. `per_group` (u64[groups], may be
+ * NULL) receives the digests, `total` (may be NULL) their wrapping sum, which
+ * is independent of how groups are sharded over engines. */
+int raft_state_digest(raft_engine* e, uint64_t* per_group, uint64_t* total);
+/* nodelog (main.go:399-401) lines of every replica of one group:
+ * "[Server<r>:<Term>:<CommitIndex>:<LastApplied>][<state>]\n". Returns the
+ * number of bytes written (NUL-terminated when it fits) or a negative code;
+ * RAFT_ERANGE if `cap` is too small. */
+int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap);
+/* Checkpoint = the canonical view of every group plus the engine's config,
+ * written to / read from a file (header + fields + CRC32C trailer). The
+ * persistent Node fields of main.go:18-21 (Term, Voted, Log) and the volatile
+ * ones (22-29) survive a save/load round trip bit for bit. Loading checks
+ * replicas / groups / ring depth / semantics / payload_crc against the
+ * engine's config (RAFT_EINVAL on mismatch, on a bad magic/version or CRC). */
+int raft_checkpoint_save(raft_engine* e, const char* path);
+int raft_checkpoint_load(raft_engine* e, const char* path);
+
 /* ---- the fused tick (the metric path) -----------------------------------
  * Advances every group by `nticks` ticks starting at virtual tick
  * `first_tick`. One tick per kernel launch; per tick and group, in order:
@@ -211,7 +233,9 @@ typedef struct raft_vote_resp {  /* VoteResponse (main.go:188-191) */
 int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_req* reqs, size_t n,
                             raft_vote_resp* out);
 
-/* Whole-node steps, batched over distinct groups. */
+/* Whole-node steps, batched over distinct groups. LEADER_ROUND and
+ * CANDIDATE_ROUND honour the config's EXT isolation windows at now_tick
+ * (messages to or from an isolated replica are dropped), like raft_tick. */
 enum raft_op_kind {
   RAFT_OP_CLIENT_APPEND = 1,   /* LeaderRun case LogReq (main.go:327-329); arg = Value */
   RAFT_OP_LEADER_ROUND = 2,    /* LeaderRun default: AE to each peer + commit (main.go:332-391) */

@@ -48,6 +48,7 @@ def load(path=None):
             "oracle_isolated": (C.c_int, [P, C.c_uint64, C.c_uint32, C.c_int64]),
             "oracle_steady_leader": (C.c_uint32, [P, C.c_uint64, C.c_int32]),
             "oracle_nodelog": (C.c_int, [P, C.c_uint64, C.c_char_p, C.c_size_t]),
+            "oracle_state_digest": (None, [P, P, P]),
             "oracle_crc32c": (C.c_uint32, [C.c_char_p, C.c_size_t]),
             "oracle_entry_crc": (C.c_uint32, [C.c_int64, C.c_int64]),
             "oracle_corrupted": (C.c_int, [P, C.c_uint64, C.c_uint32, C.c_int64]),
@@ -147,6 +148,13 @@ class Oracle:
         buf = C.create_string_buffer(4096)
         n = self.lib.oracle_nodelog(self.h, group, buf, 4096)
         return buf.value[:max(n, 0)].decode()
+
+    def state_digest(self):
+        """(per-group digests u64[G], wrapping sum) — raft_state_digest's definition."""
+        per = np.zeros(self.cfg.groups, np.uint64)
+        tot = C.c_uint64()
+        self.lib.oracle_state_digest(self.h, _ptr(per), C.byref(tot))
+        return per, tot.value
 
     # trace definition helpers
     def rng(self, gid, replica, stream, tick):

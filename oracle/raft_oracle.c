@@ -932,3 +932,45 @@ int oracle_nodelog(const oracle* o, uint64_t group, char* buf, size_t cap) {
   }
   return (int)off;
 }
+
+/* State digest (the engine's raft_state_digest, include/raftstep.h): per group
+ * a splitmix64 chain over the canonical host view of raft_store_state, keyed
+ * by the global group id; *total is the wrapping sum over groups (order- and
+ * shard-independent). Words, per replica r in order: role | voted<<8 | r<<16;
+ * term | last<<32; commit | deadline<<32; timeout | hwm<<32; for each peer p:
+ * match | next<<32; for each live log index i (max(1, hwm-K+1)..last):
+ * term | i<<32, value, crc; then the group's fault code. */
+static uint64_t dg_mix(uint64_t h, uint64_t w) { return sm64(h ^ w); }
+static uint64_t lo32(int64_t v) { return (uint64_t)(uint32_t)(int32_t)v; }
+void oracle_state_digest(const oracle* o, uint64_t* per_group, uint64_t* total) {
+  const uint32_t R = o->cfg.replicas, K = o->cfg.ring_depth;
+  const int raft = o->cfg.semantics == RAFT_SEM_RAFT;
+  uint64_t sum = 0;
+  for (uint64_t g = 0; g < o->cfg.groups; ++g) {
+    const o_group* G = &o->g[g];
+    uint64_t h = sm64(0x5241465444494721ULL ^ (o->cfg.group_base + g));
+    for (uint32_t r = 0; r < R; ++r) {
+      const o_node* n = &G->n[r];
+      const uint64_t voted = (uint64_t)(raft ? n->voted + 1 : n->voted);
+      h = dg_mix(h, (uint64_t)n->role | (voted << 8) | ((uint64_t)r << 16));
+      h = dg_mix(h, lo32(n->term) | (lo32(n->last) << 32));
+      h = dg_mix(h, lo32(n->commit) | (lo32(n->deadline) << 32));
+      h = dg_mix(h, lo32(n->timeout) | (lo32(n->hwm) << 32));
+      for (uint32_t p = 0; p < R; ++p) {
+        const int lead = n->role == RAFT_LEADER && p != r;
+        const int64_t m = lead ? n->match[p] : 0;
+        const int64_t nx = lead ? (raft ? n->next[p] : n->match[p] + 1) : 0;
+        h = dg_mix(h, lo32(m) | (lo32(nx) << 32));
+      }
+      for (int64_t idx = n->hwm > K ? n->hwm - K + 1 : 1; idx <= n->last; ++idx) {
+        h = dg_mix(h, lo32(n->log[idx - 1].term) | (lo32(idx) << 32));
+        h = dg_mix(h, (uint64_t)n->log[idx - 1].value);
+        h = dg_mix(h, (uint64_t)n->log[idx - 1].crc);
+      }
+    }
+    h = dg_mix(h, (uint64_t)G->fault);
+    if (per_group) per_group[g] = h;
+    sum += h;
+  }
+  if (total) *total = sum;
+}

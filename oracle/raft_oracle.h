@@ -53,6 +53,8 @@ uint32_t oracle_steady_leader(const raft_config* cfg, uint64_t gid, int32_t lead
 uint32_t oracle_crc32c(const uint8_t* p, size_t n);
 uint32_t oracle_entry_crc(int64_t term, int64_t value);
 int oracle_corrupted(const raft_config* cfg, uint64_t gid, uint32_t replica, int64_t tick);
+/* State digest, same definition as raft_state_digest (per group + wrapping sum). */
+void oracle_state_digest(const oracle* o, uint64_t* per_group, uint64_t* total);
 /* nodelog-format dump of one group (main.go:399-401), for debugging. */
 int oracle_nodelog(const oracle* o, uint64_t group, char* buf, size_t cap);
 

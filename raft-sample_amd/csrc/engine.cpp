@@ -848,4 +848,201 @@ int raft_profile_read(raft_engine* e, double* total_ms, uint64_t* launches) {
   return RAFT_OK;
 }
 
+// ---- audit: digest, nodelog, checkpoints ----------------------------------
+
+int raft_state_digest(raft_engine* e, uint64_t* per_group, uint64_t* total) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  HIPCHK(hipSetDevice(e->cfg.device));
+  const uint64_t G = e->cfg.groups;
+  uint64_t* d_pg = nullptr;
+  unsigned long long* d_tot = nullptr;
+  HIPCHK(hipMalloc(&d_pg, G * 8 + 64));
+  d_tot = reinterpret_cast<unsigned long long*>(d_pg + G);
+  int rc = RAFT_OK;
+  hipError_t h = hipMemsetAsync(d_tot, 0, 8, e->stream);
+  if (h == hipSuccess) h = launch_digest(e->R, e->P, e->cfg.semantics == RAFT_SEM_RAFT, d_pg, d_tot, e->stream);
+  if (h == hipSuccess && per_group) h = hipMemcpyAsync(per_group, d_pg, G * 8, hipMemcpyDeviceToHost, e->stream);
+  uint64_t tot = 0;
+  if (h == hipSuccess) h = hipMemcpyAsync(&tot, d_tot, 8, hipMemcpyDeviceToHost, e->stream);
+  if (h == hipSuccess) h = hipStreamSynchronize(e->stream);
+  if (h != hipSuccess) rc = fail(RAFT_EHIP, "raft_state_digest: %s", hipGetErrorString(h));
+  (void)hipFree(d_pg);
+  if (rc == RAFT_OK && total) *total = tot;
+  return rc;
+}
+
+int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap) {
+  if (!e || (!buf && cap)) return fail(RAFT_EINVAL, "null argument");
+  if (group >= e->cfg.groups) return fail(RAFT_EINVAL, "group %llu out of range", (unsigned long long)group);
+  HIPCHK(hipSetDevice(e->cfg.device));
+  static const char* names[] = {"follower", "candidate", "leader", "?"};   // State (main.go:51-57)
+  std::string out;
+  for (uint32_t r = 0; r < e->cfg.replicas; ++r) {
+    const uint64_t d = uint64_t(r) * e->Gp + group;
+    int32_t term = 0, commit = 0, last = 0;
+    uint16_t rs = 0;
+    HIPCHK(hipMemcpyAsync(&term, e->P.term + d, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&commit, e->P.commit + d, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&last, e->P.last + d, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&rs, e->P.rs + d, 2, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    char line[128];
+    snprintf(line, sizeof line, "[Server%u:%d:%d:%d][%s]\n", r, term, commit, last, names[rs & 3]);
+    out += line;
+  }
+  if (out.size() + 1 > cap) return fail(RAFT_ERANGE, "nodelog needs %zu bytes", out.size() + 1);
+  std::memcpy(buf, out.c_str(), out.size() + 1);
+  return int(out.size());
+}
+
+}  // extern "C"
+
+namespace {
+
+// CRC32C over a byte stream (slice-by-8, same tables as the entry stamps).
+uint32_t crc32c_update(uint32_t crc, const uint8_t* p, size_t n) {
+  const std::vector<uint32_t>& T = crc_tab_host();
+  uint32_t c = ~crc;
+  while (n >= 8) {
+    uint32_t lo, hi;
+    std::memcpy(&lo, p, 4);
+    std::memcpy(&hi, p + 4, 4);
+    lo ^= c;
+    c = T[1792 + (lo & 255)] ^ T[1536 + ((lo >> 8) & 255)] ^ T[1280 + ((lo >> 16) & 255)] ^ T[1024 + (lo >> 24)] ^
+        T[768 + (hi & 255)] ^ T[512 + ((hi >> 8) & 255)] ^ T[256 + ((hi >> 16) & 255)] ^ T[hi >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) c = (c >> 8) ^ T[(c ^ *p++) & 255];
+  return ~c;
+}
+
+constexpr char CKPT_MAGIC[8] = {'R', 'A', 'F', 'T', 'C', 'K', 'P', 'T'};
+constexpr uint32_t CKPT_VERSION = 1;
+struct CkptHeader {
+  char magic[8];
+  uint32_t version, nfields;
+  raft_config cfg;
+};
+struct CkptField {   // followed by count * elem bytes
+  char name[12];
+  uint32_t elem;
+  uint64_t count;
+};
+
+// The canonical view's fields in file order.
+struct ViewField {
+  const char* name;
+  void** ptr;
+  uint32_t elem;
+  uint64_t count;
+};
+std::vector<ViewField> view_fields(raft_state_view& v, uint64_t G, uint64_t R, uint64_t K) {
+  return {{"role", reinterpret_cast<void**>(&v.role), 1, G * R},
+          {"voted", reinterpret_cast<void**>(&v.voted), 1, G * R},
+          {"term", reinterpret_cast<void**>(&v.term), 4, G * R},
+          {"last", reinterpret_cast<void**>(&v.last), 4, G * R},
+          {"commit", reinterpret_cast<void**>(&v.commit), 4, G * R},
+          {"deadline", reinterpret_cast<void**>(&v.deadline), 4, G * R},
+          {"timeout", reinterpret_cast<void**>(&v.timeout), 4, G * R},
+          {"match", reinterpret_cast<void**>(&v.match), 4, G * R * R},
+          {"fault", reinterpret_cast<void**>(&v.fault), 1, G},
+          {"log_term", reinterpret_cast<void**>(&v.log_term), 4, G * R * K},
+          {"log_value", reinterpret_cast<void**>(&v.log_value), 8, G * R * K},
+          {"log_crc", reinterpret_cast<void**>(&v.log_crc), 4, G * R * K},
+          {"next", reinterpret_cast<void**>(&v.next), 4, G * R * R},
+          {"hwm", reinterpret_cast<void**>(&v.hwm), 4, G * R}};
+}
+
+struct File {
+  FILE* f = nullptr;
+  ~File() {
+    if (f) fclose(f);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int raft_checkpoint_save(raft_engine* e, const char* path) {
+  if (!e || !path) return fail(RAFT_EINVAL, "null argument");
+  const uint64_t G = e->cfg.groups, R = e->cfg.replicas, K = e->cfg.ring_depth;
+  raft_state_view v{};
+  auto fields = view_fields(v, G, R, K);
+  std::vector<std::vector<uint8_t>> bufs(fields.size());
+  for (size_t i = 0; i < fields.size(); ++i) {
+    bufs[i].assign(fields[i].count * fields[i].elem, 0);
+    *fields[i].ptr = bufs[i].data();
+  }
+  if (int rc = raft_store_state(e, &v)) return rc;
+  File f;
+  f.f = fopen(path, "wb");
+  if (!f.f) return fail(RAFT_EINVAL, "cannot open %s for writing", path);
+  uint32_t crc = 0;
+  auto put = [&](const void* p, size_t n) {
+    crc = crc32c_update(crc, static_cast<const uint8_t*>(p), n);
+    return fwrite(p, 1, n, f.f) == n;
+  };
+  CkptHeader h{};
+  std::memcpy(h.magic, CKPT_MAGIC, 8);
+  h.version = CKPT_VERSION;
+  h.nfields = uint32_t(fields.size());
+  h.cfg = e->cfg;
+  bool ok = put(&h, sizeof h);
+  for (size_t i = 0; ok && i < fields.size(); ++i) {
+    CkptField fh{};
+    std::strncpy(fh.name, fields[i].name, sizeof fh.name - 1);
+    fh.elem = fields[i].elem;
+    fh.count = fields[i].count;
+    ok = put(&fh, sizeof fh) && put(bufs[i].data(), bufs[i].size());
+  }
+  ok = ok && fwrite(&crc, 1, 4, f.f) == 4;
+  ok = ok && fflush(f.f) == 0;
+  if (!ok) return fail(RAFT_EINVAL, "short write to %s", path);
+  return RAFT_OK;
+}
+
+int raft_checkpoint_load(raft_engine* e, const char* path) {
+  if (!e || !path) return fail(RAFT_EINVAL, "null argument");
+  const uint64_t G = e->cfg.groups, R = e->cfg.replicas, K = e->cfg.ring_depth;
+  File f;
+  f.f = fopen(path, "rb");
+  if (!f.f) return fail(RAFT_EINVAL, "cannot open %s", path);
+  uint32_t crc = 0;
+  auto get = [&](void* p, size_t n) {
+    if (fread(p, 1, n, f.f) != n) return false;
+    crc = crc32c_update(crc, static_cast<const uint8_t*>(p), n);
+    return true;
+  };
+  CkptHeader h{};
+  if (!get(&h, sizeof h) || std::memcmp(h.magic, CKPT_MAGIC, 8) != 0)
+    return fail(RAFT_EINVAL, "%s: not a raftstep checkpoint", path);
+  if (h.version != CKPT_VERSION) return fail(RAFT_EINVAL, "%s: checkpoint version %u unsupported", path, h.version);
+  if (h.cfg.replicas != e->cfg.replicas || h.cfg.groups != e->cfg.groups || h.cfg.ring_depth != e->cfg.ring_depth ||
+      h.cfg.semantics != e->cfg.semantics || h.cfg.payload_crc != e->cfg.payload_crc)
+    return fail(RAFT_EINVAL, "%s: checkpoint of R=%u G=%llu K=%u sem=%u crc=%u does not fit this engine", path,
+                h.cfg.replicas, (unsigned long long)h.cfg.groups, h.cfg.ring_depth, h.cfg.semantics, h.cfg.payload_crc);
+  raft_state_view v{};
+  auto fields = view_fields(v, G, R, K);
+  if (h.nfields != fields.size()) return fail(RAFT_EINVAL, "%s: %u fields, expected %zu", path, h.nfields, fields.size());
+  std::vector<std::vector<uint8_t>> bufs(fields.size());
+  for (size_t i = 0; i < fields.size(); ++i) {
+    CkptField fh{};
+    if (!get(&fh, sizeof fh)) return fail(RAFT_EINVAL, "%s: truncated", path);
+    if (std::strncmp(fh.name, fields[i].name, sizeof fh.name) != 0 || fh.elem != fields[i].elem ||
+        fh.count != fields[i].count)
+      return fail(RAFT_EINVAL, "%s: field %zu is %.12s[%llu x %u], expected %s", path, i, fh.name,
+                  (unsigned long long)fh.count, fh.elem, fields[i].name);
+    bufs[i].resize(fh.count * fh.elem);
+    if (!get(bufs[i].data(), bufs[i].size())) return fail(RAFT_EINVAL, "%s: truncated", path);
+    *fields[i].ptr = bufs[i].data();
+  }
+  const uint32_t want = crc;
+  uint32_t stored = 0;
+  if (fread(&stored, 1, 4, f.f) != 4) return fail(RAFT_EINVAL, "%s: missing CRC32C trailer", path);
+  if (stored != want) return fail(RAFT_EINVAL, "%s: CRC32C mismatch (file %08x, computed %08x)", path, stored, want);
+  return raft_load_state(e, &v);
+}
+
 }  // extern "C"

@@ -55,6 +55,72 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
   P.gmeta[g] = uint16_t(L | (P.hwm ? 0 : M_MSYNC) | M_STEADY);
 }
 
+// State digest (raft_state_digest): one lane per group derives the canonical
+// host view exactly as raft_store_state does (implicit MSYNC rows, heartbeat
+// timer starts, REF NextIndex = MatchIndex+1) and chains it through
+// splitmix64; the per-group digests are summed with one atomic per wave.
+// Same definition as oracle_state_digest().
+__device__ __forceinline__ uint64_t dg_mix(uint64_t h, uint64_t w) { return sm64(h ^ w); }
+__device__ __forceinline__ uint64_t lo32(int v) { return uint64_t(uint32_t(v)); }
+
+template <int R>
+__global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint64_t* per_group,
+                                                     unsigned long long* total) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  uint64_t h = 0;
+  if (g < P.G) {
+    const int meta = at(P.gmeta, g);
+    const int primary = meta & 0xF, fault = (meta >> 4) & 0xF;
+    const bool msync = (meta & M_MSYNC) && primary < R;
+    const int hb = at(P.hb, g);
+    int last[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) last[r] = at(prow(P.last, r, P.Gp), g);
+    h = sm64(0x5241465444494721ULL ^ (P.gbase + g));
+#pragma unroll 1
+    for (int r = 0; r < R; ++r) {
+      const uint32_t x = at(prow(P.rs, r, P.Gp), g);
+      const int role = int(x & 3u), dur = int(x >> 6);
+      const int l = sel(last, r);
+      const int ts = at(prow(P.tstart, r, P.Gp), g);
+      const int dl = (role == ROLE_L ? ts : max(ts, hb)) + dur;
+      const int hwm = (raft && !msync) ? at(prow(P.hwm, r, P.Gp), g) : l;
+      h = dg_mix(h, uint64_t(role) | (uint64_t((x >> 2) & 15u) << 8) | (uint64_t(r) << 16));
+      h = dg_mix(h, lo32(at(prow(P.term, r, P.Gp), g)) | (lo32(l) << 32));
+      h = dg_mix(h, lo32(at(prow(P.commit, r, P.Gp), g)) | (lo32(dl) << 32));
+      h = dg_mix(h, lo32(dur) | (lo32(hwm) << 32));
+#pragma unroll 1
+      for (int p = 0; p < R; ++p) {
+        int m = 0, nx = 0;
+        if (role == ROLE_L && p != r) {
+          const int lp = sel(last, p);
+          if (r == primary) m = msync ? lp : at(prow(P.lmatch, p, P.Gp), g);
+          else m = at(prow(P.xmatch, r * R + p, P.Gp), g);
+          if (!raft) nx = m + 1;
+          else if (r == primary) nx = msync ? lp + 1 : at(prow(P.lnext, p, P.Gp), g);
+          else nx = at(prow(P.xnext, r * R + p, P.Gp), g);
+        }
+        h = dg_mix(h, lo32(m) | (lo32(nx) << 32));
+      }
+      const uint64_t rb = uint64_t(r) * P.K * P.Gp;
+#pragma unroll 1
+      for (int idx = hwm > int(P.K) ? hwm - int(P.K) + 1 : 1; idx <= l; ++idx) {
+        const uint32_t o = ring_slot_off(g, P.K, uint32_t((idx - 1) & int(P.kmask)));
+        h = dg_mix(h, lo32(at(P.log_term + rb, o)) | (lo32(idx) << 32));
+        h = dg_mix(h, uint64_t(at(P.log_value + rb, o)));
+        h = dg_mix(h, P.crc_on ? uint64_t(at(P.log_crc + rb, o)) : 0ull);
+      }
+    }
+    h = dg_mix(h, uint64_t(fault));
+    per_group[g] = h;
+  }
+  // wrapping 64-bit sum: two 32-bit halves through the shuffle tree
+  unsigned long long x = h;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  if ((threadIdx.x & 63) == 0 && x) atomicAdd(total, x);
+}
+
 hipError_t launch_tick_slow_ref(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
                                 unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
                                 const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
@@ -84,6 +150,11 @@ hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_
 }
 hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s) {
   RAFT_DISPATCH_R(R, hipLaunchKernelGGL(init_steady_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P, T, leader));
+  return hipGetLastError();
+}
+hipError_t launch_digest(int R, const DevPlanes& P, int raft, uint64_t* per_group, unsigned long long* total,
+                         hipStream_t s) {
+  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(digest_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P, raft, per_group, total));
   return hipGetLastError();
 }
 

@@ -49,6 +49,9 @@ hipError_t launch_tick_slow(int R, int sem, const DevPlanes& P, const Trace& T0,
 hipError_t launch_ops(int R, int sem, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
                       const int32_t* et, const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s);
 hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_t s);
+// Per-group state digest (same definition as oracle_state_digest) + wrapping sum.
+hipError_t launch_digest(int R, const DevPlanes& P, int raft, uint64_t* per_group, unsigned long long* total,
+                         hipStream_t s);
 hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s);
 
 }  // namespace raftstep

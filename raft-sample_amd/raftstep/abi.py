@@ -155,6 +155,10 @@ SIGNATURES = {
     "raft_comm_allreduce_stats": (C.c_int, [P, P]),
     "raft_profile_enable": (C.c_int, [P, C.c_int]),
     "raft_profile_read": (C.c_int, [P, P, P]),
+    "raft_state_digest": (C.c_int, [P, P, P]),
+    "raft_nodelog": (C.c_int, [P, C.c_uint64, C.c_char_p, C.c_size_t]),
+    "raft_checkpoint_save": (C.c_int, [P, C.c_char_p]),
+    "raft_checkpoint_load": (C.c_int, [P, C.c_char_p]),
 }
 
 

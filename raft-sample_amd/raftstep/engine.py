@@ -107,6 +107,28 @@ class Engine:
         v = abi.make_view(st)
         _check(self.lib.raft_load_state(self.h, C.byref(v)))
 
+    # -- audit ---------------------------------------------------------
+    def state_digest(self):
+        """(per-group digests u64[G], wrapping sum), computed on the device."""
+        per = np.zeros(self.cfg.groups, np.uint64)
+        tot = C.c_uint64()
+        _check(self.lib.raft_state_digest(self.h, _ptr(per), C.byref(tot)))
+        return per, tot.value
+
+    def nodelog(self, group):
+        """main.go nodelog lines (main.go:399-401) of every replica of `group`."""
+        buf = C.create_string_buffer(64 * (self.cfg.replicas + 1))
+        n = self.lib.raft_nodelog(self.h, group, buf, len(buf))
+        if n < 0:
+            _check(n)
+        return buf.value.decode()
+
+    def save_checkpoint(self, path):
+        _check(self.lib.raft_checkpoint_save(self.h, os.fsencode(path)))
+
+    def load_checkpoint(self, path):
+        _check(self.lib.raft_checkpoint_load(self.h, os.fsencode(path)))
+
     # -- the fused tick ------------------------------------------------
     def tick(self, first_tick, nticks=1, stats=True):
         if stats:

@@ -198,3 +198,33 @@ def random_state(rng, G, R, K, max_term=6, max_log=12):
                     if p != r:
                         st["match"][g, r, p] = rng.integers(0, max_log + 2)
     return st
+
+
+def random_events(impl, rng, n_events, t0=0):
+    """Drive `impl` (engine, oracle or a trace.TraceRecorder over one) through a
+    random mix of tick ranges and handler batches; returns the next tick."""
+    G, R = impl.cfg.groups, impl.cfg.replicas
+    t = t0
+    for _ in range(n_events):
+        kind = int(rng.integers(0, 5))
+        groups = rng.permutation(G)[: max(1, G // 3)]
+        if kind <= 1:
+            k = int(rng.integers(1, 6))
+            impl.tick(t, k)
+            t += k
+        elif kind == 2:
+            items = [dict(group=int(g), to=int(rng.integers(0, R)), term=int(rng.integers(0, 6)),
+                          prev_log_index=int(rng.integers(0, 8)), prev_log_term=int(rng.integers(0, 6)),
+                          leader_commit=int(rng.integers(0, 10)),
+                          logs=[(int(rng.integers(0, 6)), int(rng.integers(0, 1 << 62)))
+                                for _ in range(int(rng.integers(0, 5)))]) for g in groups]
+            reqs, ents = ae_reqs(items)
+            impl.append_entries(t, reqs, ents)
+        elif kind == 3:
+            impl.request_vote(t, vote_reqs([dict(group=int(g), to=int(rng.integers(0, R)),
+                                                 term=int(rng.integers(0, 8)),
+                                                 candidate_id=int(rng.integers(0, R))) for g in groups]))
+        else:
+            impl.group_ops(t, ops([dict(group=int(g), replica=int(rng.integers(0, R)), kind=int(rng.integers(1, 6)),
+                                        arg=int(rng.integers(0, 1 << 62))) for g in groups]))
+    return t
