@@ -128,6 +128,24 @@ __device__ __forceinline__ uint64_t rng_k(uint64_t key, uint32_t r, uint32_t str
   return sm64(sm64(key ^ ((uint64_t(stream) << 32) | r)) ^ tick);
 }
 
+// Out-of-line RNG for the general kernels' unrolled per-replica code (the
+// steady-state kernel inlines rng_k/sm64 directly).
+__device__ __attribute__((noinline)) uint64_t rng_k_call(uint64_t key, uint32_t r, uint32_t stream, uint64_t tick) {
+  return rng_k(key, r, stream, tick);
+}
+__device__ __attribute__((noinline)) int64_t entry_value(uint64_t vbase, uint32_t e) {   // rand.Int() (main.go:92)
+  return int64_t(sm64(vbase ^ uint64_t(e)) >> 1);
+}
+
+// Election timer duration min + (rng >> 32) % span (main.go:114, 194). Kept
+// out of line: inlined into every unrolled handler copy, the 64-bit RNG gets
+// speculated ahead of its branches and the general kernels run out of VGPRs.
+__device__ __attribute__((noinline)) int timer_draw(uint64_t key, uint32_t r, uint32_t stream, int64_t tick, int mn,
+                                                    int span) {
+  const uint64_t h = rng_k(key, r, stream, uint64_t(tick));
+  return mn + int(uint32_t(h >> 32) % uint32_t(span));
+}
+
 // --------------------------------------------------------------- CRC32C --
 // EXT (config C5): CRC32C (Castagnoli, reflected) of an entry's payload =
 // Term (4 B LE) || Value (8 B LE), slice-by-4 then slice-by-8 over the
@@ -164,6 +182,23 @@ __device__ __forceinline__ void put(int (&a)[R], int c, int v) {
 #pragma unroll
   for (int i = 0; i < R; ++i) a[i] = (c == i) ? v : a[i];
 }
+// Per-replica array of one lane kept in LDS (general kernels): column
+// `threadIdx.x` of a [R][256] int slab, so that consecutive lanes hit
+// consecutive banks and a runtime replica index is one ds_read/ds_write
+// instead of an R-way select chain in registers.
+template <int R>
+struct LArr {
+  int* p;
+  __device__ __forceinline__ int& operator[](int i) const { return p[i * 256]; }
+};
+template <int R>
+__device__ __forceinline__ int sel(const LArr<R>& a, int c) { return a[c]; }
+template <int R>
+__device__ __forceinline__ void put(LArr<R>& a, int c, int v) { a[c] = v; }
+// LDS ints one Group needs per lane (6 arrays of R)
+template <int R>
+constexpr int group_lds_ints() { return 6 * R; }
+
 template <int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (N > 0) {
@@ -184,8 +219,9 @@ struct AEResp { int term, match, ok; };  // AppendEntriesResponse (main.go:298-3
 // Raft-paper mode (same tick model and layout, see the r_* methods).
 template <int R, int SEM = SEM_REF>
 struct Group {
-  int term[R], last[R], commit[R], dl[R], dur[R];
-  int hw[R];            // RAFT: high-water mark of each log (REF: unused)
+  // term, last, commit, dl (deadline), dur (timer duration), hw (RAFT:
+  // high-water mark of each log; REF: unused) live in LDS (bind())
+  LArr<R> term, last, commit, dl, dur, hw;
   uint32_t roles;       // 2 bits per replica
   uint32_t votes;       // 4 bits per replica: REF Voted (0/1), RAFT votedFor+1
   uint32_t known;       // deadline register valid
@@ -221,6 +257,12 @@ struct Group {
   __device__ __forceinline__ bool dropped(int a, int b) const { return ((iso >> a) | (iso >> b)) & 1u; }
 
   // ---------------------------------------------------------- load/store --
+  // lds: a block's [6][R][256] int slab (shared by the lanes, column = lane)
+  __device__ __forceinline__ void bind(int* lds) {
+    int* b = lds + threadIdx.x;
+    term.p = b; last.p = b + R * 256; commit.p = b + 2 * R * 256;
+    dl.p = b + 3 * R * 256; dur.p = b + 4 * R * 256; hw.p = b + 5 * R * 256;
+  }
   __device__ __forceinline__ void begin(const DevPlanes& P, const Trace& T, uint32_t g_) {
     g = g_;
     key = group_key(T.seed, P.gbase + g);
@@ -322,7 +364,7 @@ struct Group {
   // EXT: is the AppendEntries delivered to replica p this tick corrupted?
   __device__ __forceinline__ int corrupted(const DevPlanes& P, int p) const {
     if (!P.crc_on || !P.corrupt_p) return 0;
-    return (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(tick)) & 0xFFFF) < P.corrupt_p;
+    return (rng_k_call(key, uint32_t(p), ST_CORRUPT, uint64_t(tick)) & 0xFFFF) < P.corrupt_p;
   }
   // Timer of replica r (lazy: only read from HBM when a timeout check needs it).
   template <int Rp>
@@ -336,9 +378,8 @@ struct Group {
 
   // ------------------------------------------------------------ timers --
   __device__ __forceinline__ int draw(const Trace& T, int r, bool cand) const {
-    const uint64_t h = rng_k(key, uint32_t(r), cand ? ST_TIMER_C : ST_TIMER_F, uint64_t(tick));
-    const uint32_t span = uint32_t(cand ? T.c_span : T.f_span);
-    return (cand ? T.c_min : T.f_min) + int(uint32_t(h >> 32) % span);
+    return cand ? timer_draw(key, uint32_t(r), ST_TIMER_C, tick, T.c_min, T.c_span)
+                : timer_draw(key, uint32_t(r), ST_TIMER_F, tick, T.f_min, T.f_span);
   }
   // FollowerRun entry: d = rand.Intn(20)+10, timer started (main.go:113-115).
   template <int Rp>
@@ -909,7 +950,7 @@ struct TickSrc {
     c = 0;
     if (leader == cache_leader && idx >= cache_from) {
       t = cache_term;
-      v = int64_t(sm64(cache_vbase ^ uint64_t(uint32_t(idx - cache_from))) >> 1);
+      v = entry_value(cache_vbase, uint32_t(idx - cache_from));
       if (crc_on) c = crc_entry(tab, t, v);   // the leader's stamp of its own fresh entry
     } else {
       const uint64_t rb = uint64_t(leader) * K * Gp;

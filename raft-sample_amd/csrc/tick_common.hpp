@@ -51,7 +51,7 @@ __device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, c
     static_for<R>([&](auto RI) {
       constexpr int r = decltype(RI)::value;
       if (G.role(r) != ROLE_L || !G.alive()) return;
-      const uint64_t vb = rng_k(G.key, r, ST_VALUE, uint64_t(G.tick));
+      const uint64_t vb = rng_k_call(G.key, r, ST_VALUE, uint64_t(G.tick));
       const int l = G.last[r];
       const int room = I32MAX - l;
       const int n_ok = int(E) <= room ? int(E) : room;
@@ -60,7 +60,7 @@ __device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, c
       }
       const int e0 = n_ok > int(P.K) ? n_ok - int(P.K) : 0;   // only the last K stay in the ring
       for (int e = e0; e < n_ok; ++e) {
-        const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+        const int64_t v = entry_value(vb, uint32_t(e));
         G.ring_term(P, r, l + 1 + e) = G.term[r];
         G.ring_value(P, r, l + 1 + e) = v;
         if (P.crc_on) G.ring_crc(P, r, l + 1 + e) = crc_entry(P.crc_tab, G.term[r], v);
