@@ -622,6 +622,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   HIPCHK(hipMemsetAsync(e->wcount, 0, 2 * sizeof(uint32_t), e->stream));
   const Trace T0 = make_trace(e, first_tick);
   uint32_t window = 0;
+  int64_t win_first = first_tick;   // first tick of the current general-kernel window
   hipEvent_t ra = nullptr, rb = nullptr;
   if (e->prof == 2) {
     ra = next_event(e);
@@ -645,9 +646,10 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
                             e->stream, a, b));
     // deferred groups catch up every slow_every ticks and at the end of the call
     if ((i + 1) % e->slow_every == 0 || i + 1 == nticks) {
-      HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, t, stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
+      HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t, stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
                               e->wcount + ((window + 1) & 1), e->stream));
       ++window;
+      win_first = t + 1;
     }
   }
   if (e->prof == 2) {

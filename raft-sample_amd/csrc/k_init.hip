@@ -121,10 +121,10 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
   if ((threadIdx.x & 63) == 0 && x) atomicAdd(total, x);
 }
 
-hipError_t launch_tick_slow_ref(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
+hipError_t launch_tick_slow_ref(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t win_first, int64_t last_tick,
                                 unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
                                 const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
-hipError_t launch_tick_slow_raft(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
+hipError_t launch_tick_slow_raft(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t win_first, int64_t last_tick,
                                  unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
                                  const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
 hipError_t launch_ops_ref(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n, const int32_t* et,
@@ -132,12 +132,12 @@ hipError_t launch_ops_ref(int R, const DevPlanes& P, const Trace& T, const DevOp
 hipError_t launch_ops_raft(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n, const int32_t* et,
                            const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s);
 
-hipError_t launch_tick_slow(int R, int sem, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t last_tick,
+hipError_t launch_tick_slow(int R, int sem, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t win_first, int64_t last_tick,
                             unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
                             const uint32_t* work_count, uint32_t* next_count, hipStream_t s) {
   return sem == SEM_RAFT
-             ? launch_tick_slow_raft(R, P, T0, first_tick, last_tick, stats, work, work_tick, work_count, next_count, s)
-             : launch_tick_slow_ref(R, P, T0, first_tick, last_tick, stats, work, work_tick, work_count, next_count, s);
+             ? launch_tick_slow_raft(R, P, T0, first_tick, win_first, last_tick, stats, work, work_tick, work_count, next_count, s)
+             : launch_tick_slow_ref(R, P, T0, first_tick, win_first, last_tick, stats, work, work_tick, work_count, next_count, s);
 }
 hipError_t launch_ops(int R, int sem, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
                       const int32_t* et, const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s) {

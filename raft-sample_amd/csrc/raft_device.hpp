@@ -281,6 +281,17 @@ struct Group {
     fault = (m >> 4) & 0xF;
     hbt = HB_NONE;
   }
+  // Per-tick reset of a group whose state stays resident across ticks
+  // (general kernel catch-up): clock, counters, this tick's entry cache.
+  __device__ __forceinline__ void next_tick(const Trace& T) {
+    tick = T.tick;
+    now = T.now;
+    iso = 0;
+#pragma unroll
+    for (int s = 0; s < NSTAT; ++s) st[s] = 0;
+    cache_leader = -1;
+    cache_from = 0; cache_term = 0; cache_vbase = 0;
+  }
   // Effective timer start: followers/candidates also count the last
   // steady-state heartbeat (hb), which resets every follower at once.
   __device__ __forceinline__ int eff_start(int ts, int r) const { return role(r) == ROLE_L ? ts : max(ts, hbt); }
