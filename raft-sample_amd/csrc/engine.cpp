@@ -74,9 +74,9 @@ uint32_t host_entry_crc(int32_t term, int64_t value) {
            T[768 + (hi & 255)] ^ T[512 + ((hi >> 8) & 255)] ^ T[256 + ((hi >> 16) & 255)] ^ T[hi >> 24]);
 }
 
-// Device ring layout (raft_device.hpp ring_slot_off): [R][Gp/64][K][64].
-inline uint64_t ring_index(uint64_t r, uint64_t g, uint64_t s, uint64_t K, uint64_t Gp) {
-  return r * K * Gp + ((g >> 6) * K + s) * 64 + (g & 63);
+// Device ring layout (raft_device.hpp ring_tile / ring_in_tile): [Gp/64][K][64][R].
+inline uint64_t ring_index(uint64_t r, uint64_t g, uint64_t s, uint64_t K, uint64_t R) {
+  return (((g >> 6) * K + s) * 64 + (g & 63)) * R + r;
 }
 
 bool fits32(int64_t v) { return v >= -int64_t(I32) - 1 && v <= int64_t(I32); }
@@ -296,9 +296,10 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
       (c.isolate_min_ticks < 1 || c.isolate_max_ticks > 32 || c.isolate_min_ticks > c.isolate_max_ticks))
     return fail(RAFT_EINVAL, "isolation length must satisfy 1 <= min <= max <= 32");
   const uint64_t Gp = (c.groups + 255) & ~uint64_t(255);
-  // device addressing uses 32-bit byte offsets inside one replica's ring
-  if (Gp * c.ring_depth * 8 > (uint64_t(1) << 32))
-    return fail(RAFT_EINVAL, "groups x ring_depth too large for one engine (need groups*ring_depth <= 2^29)");
+  // device addressing: 64-bit plane/tile bases, 32-bit lane offsets (group
+  // index < 2^32 within a plane, K*64*R entries within a ring tile)
+  if (c.groups >= (uint64_t(1) << 31))
+    return fail(RAFT_EINVAL, "too many groups for one engine (need groups < 2^31)");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RAFT_ENODEV, "no HIP device");
   if (c.device < 0 || c.device >= ndev) return fail(RAFT_ENODEV, "device %d out of range", c.device);
@@ -498,7 +499,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
           v->next[c * R + p] = nx;
         }
       if (logs && last[d] > 0) {
-        const int32_t want = lt[ring_index(r, g, uint64_t((last[d] - 1) & int64_t(K - 1)), K, Gp)];
+        const int32_t want = lt[ring_index(r, g, uint64_t((last[d] - 1) & int64_t(K - 1)), K, R)];
         if (ltm[d] != want)
           return fail(RAFT_EINVAL, "internal: last-entry term cache of group %llu replica %llu is %d, ring says %d",
                       (unsigned long long)g, (unsigned long long)r, ltm[d], want);
@@ -509,7 +510,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
           // slot s holds the largest index i <= l with (i-1) mod K == s
           int64_t idx = l >= 1 ? l - ((l - 1 - int64_t(s)) & int64_t(K - 1)) : 0;
           const bool live = idx >= 1 && idx <= l && idx > int64_t(hwm) - int64_t(K);
-          const uint64_t o = ring_index(r, g, s, K, Gp);
+          const uint64_t o = ring_index(r, g, s, K, R);
           if (v->log_term) v->log_term[c * K + s] = live ? lt[o] : 0;
           if (v->log_value) v->log_value[c * K + s] = live ? lv[o] : 0;
           if (v->log_crc) v->log_crc[c * K + s] = (live && crcs) ? lcrc[o] : 0u;
@@ -581,10 +582,10 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
         hw[d] = h;
       }
       for (uint64_t s = 0; s < K; ++s) {
-        lt[ring_index(r, g, s, K, Gp)] = v->log_term[c * K + s];
-        lv[ring_index(r, g, s, K, Gp)] = v->log_value[c * K + s];
+        lt[ring_index(r, g, s, K, R)] = v->log_term[c * K + s];
+        lv[ring_index(r, g, s, K, R)] = v->log_value[c * K + s];
         if (e->cfg.payload_crc)
-          lcrc[ring_index(r, g, s, K, Gp)] = v->log_crc ? v->log_crc[c * K + s]
+          lcrc[ring_index(r, g, s, K, R)] = v->log_crc ? v->log_crc[c * K + s]
                                                   : host_entry_crc(v->log_term[c * K + s], v->log_value[c * K + s]);
       }
       if (v->last[c] > 0) ltm[d] = v->log_term[c * K + uint64_t((v->last[c] - 1) & int64_t(K - 1))];

@@ -45,6 +45,11 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
   }
   int sv[4] = {0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups
   bool bail = false;
+  const int n = int(T.client_entries());   // entries per leader this tick (wave-uniform)
+  // this lane's ring writes, issued after the per-group code (wave-converged)
+  uint32_t wr = 0;      // replicas that append this tick's entries (leader + accepting followers)
+  int w_term = 0, w_idx = 0;   // their term and first index - 1 (the leader's LastApplied)
+  uint64_t w_vb = 0;    // value stream base of this tick's entries
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
     const int c = meta & 0xF;
@@ -77,7 +82,6 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         }
       }
     }
-    const int n = int(T.client_entries());
     uint64_t key = 0;
     if (go && (T.iso_p || n)) key = group_key(T.seed, P.gbase + g);
     if (go && T.iso_p) bail |= isolation_mask<R>(key, T) != 0;
@@ -200,33 +204,109 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       // RAFT: MSYNC also makes NextIndex (= match+1) and the high-water marks (= last) implicit
       const int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
       if (nm != meta) at(P.gmeta, g) = uint16_t(nm);
-      // this tick's entries: leader log + every follower that accepted
+      // this tick's entries go to the leader log + every follower that accepted
       if (n) {
-        const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
-        const uint64_t cb = uint64_t(c) * P.K * P.Gp;
-        uint32_t cs = 0;
-        if constexpr (CRC) cs = crc_term_state(tab, Lt);
-        for (int e = 0; e < n; ++e) {
-          const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
-          const uint32_t o = ring_slot_off(g, P.K, uint32_t((Ll + e) & int(P.kmask)));
-          uint32_t stamp = 0;
-          if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
-          st<WT>(P.log_term + cb, o, Lt);
-          st<WT>(P.log_value + cb, o, v);
-          if constexpr (CRC) st<WT>(P.log_crc + cb, o, stamp);
+        bool same = true;   // every writer appends at Ll+1 (REF: a follower's log may run past its MatchIndex)
 #pragma unroll
-          for (int p = 0; p < R; ++p) {
-            if (p == c || !((okm >> p) & 1u)) continue;
-            const uint32_t op = ring_slot_off(g, P.K, uint32_t((last[p] - n + e) & int(P.kmask)));
-            const uint64_t pb = uint64_t(p) * P.K * P.Gp;
-            st<WT>(P.log_term + pb, op, Lt);
-            st<WT>(P.log_value + pb, op, v);
-            if constexpr (CRC) st<WT>(P.log_crc + pb, op, stamp);
+        for (int p = 0; p < R; ++p)
+          if (((okm >> p) & 1u) && last[p] - n != Ll) same = false;
+        const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+        if (same) {
+          wr = okm | (1u << c);
+          w_term = Lt;
+          w_idx = Ll;
+          w_vb = vb;
+        } else {   // rare: write here, each replica at its own LastApplied+1+e
+          const uint64_t tb = ring_tile(g, P.K, R);
+          uint32_t cs = 0;
+          if constexpr (CRC) cs = crc_term_state(tab, Lt);
+          for (int e = 0; e < n; ++e) {
+            const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+            uint32_t stamp = 0;
+            if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+#pragma unroll
+            for (int p = 0; p < R; ++p) {
+              if (p != c && !((okm >> p) & 1u)) continue;
+              const int i0 = p == c ? Ll : last[p] - n;
+              const uint32_t o = ring_in_tile(g, R, uint32_t((i0 + e) & int(P.kmask)), uint32_t(p));
+              st<WT>(P.log_term + tb, o, Lt);
+              st<WT>(P.log_value + tb, o, v);
+              if constexpr (CRC) st<WT>(P.log_crc + tb, o, stamp);
+            }
           }
         }
       }
     }
     if (bail) at(P.gmeta, g) = uint16_t(meta | M_DEFER);
+  }
+  // ---- this tick's log entries into the rings (all lanes of the wave) ----
+  // Ring row of one slot = 64 lanes x R replicas, contiguous. When every
+  // writing lane of the wave appends at the same slot (logs in step: the
+  // steady state), the wave writes whole rows cooperatively: store k covers
+  // row elements k*64 + lane, i.e. (group lane (k*64+lane)/R, replica
+  // (k*64+lane)%R), whose term/value/stamp come from that group's lane by
+  // shuffle — R fully contiguous stores per plane and entry. Otherwise
+  // (drifted logs) each lane writes its own R-contiguous segment.
+  if (n) {
+    const uint64_t wball = __ballot(wr != 0);
+    if (wball) {
+      const int lane = threadIdx.x & 63;
+      // the tile base is wave-uniform (blocks are whole waves of consecutive groups)
+      const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g), P.K, R);
+      int32_t* const rt = P.log_term + tb;
+      int64_t* const rv = P.log_value + tb;
+      uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
+      const int s0 = __shfl(w_idx, int(__builtin_ctzll(wball)));
+      const bool aligned = __all(wr == 0 || ((w_idx - s0) & int(P.kmask)) == 0);
+      uint32_t cs = 0;
+      if constexpr (CRC) cs = crc_term_state(tab, w_term);
+      if (aligned) {
+        int k_term[R];
+        uint32_t k_on[R];
+        int k_src[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const int j = k * 64 + lane;
+          const int src = j / R, rr = j - src * R;
+          k_src[k] = src;
+          k_term[k] = __shfl(w_term, src);
+          k_on[k] = (uint32_t(__shfl(int(wr), src)) >> rr) & 1u;
+        }
+        for (int e = 0; e < n; ++e) {
+          const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
+          uint32_t stamp = 0;
+          if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+          const uint32_t row = uint32_t((s0 + e) & int(P.kmask)) * 64u * R;
+          const int vlo = int(uint32_t(uint64_t(v))), vhi = int(uint32_t(uint64_t(v) >> 32));
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const int lo = __shfl(vlo, k_src[k]), hi = __shfl(vhi, k_src[k]);
+            uint32_t sk = 0;
+            if constexpr (CRC) sk = uint32_t(__shfl(int(stamp), k_src[k]));
+            if (k_on[k]) {
+              const uint32_t o = row + uint32_t(k * 64 + lane);
+              st<WT>(rt, o, k_term[k]);
+              st<WT>(rv, o, int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo)));
+              if constexpr (CRC) st<WT>(rc, o, sk);
+            }
+          }
+        }
+      } else if (wr) {
+        for (int e = 0; e < n; ++e) {
+          const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
+          uint32_t stamp = 0;
+          if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+          const uint32_t o = ring_in_tile(g, R, uint32_t((w_idx + e) & int(P.kmask)), 0u);
+#pragma unroll
+          for (int p = 0; p < R; ++p) {
+            if (!((wr >> p) & 1u)) continue;
+            st<WT>(rt, o + p, w_term);
+            st<WT>(rv, o + p, v);
+            if constexpr (CRC) st<WT>(rc, o + p, stamp);
+          }
+        }
+      }
+    }
   }
   // groups that need the general path go to the dense worklist: block-local
   // prefix over the wave ballots, one atomic per block that defers anything

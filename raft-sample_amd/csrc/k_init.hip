@@ -102,10 +102,10 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
         }
         h = dg_mix(h, lo32(m) | (lo32(nx) << 32));
       }
-      const uint64_t rb = uint64_t(r) * P.K * P.Gp;
+      const uint64_t rb = ring_tile(g, P.K, R);
 #pragma unroll 1
       for (int idx = hwm > int(P.K) ? hwm - int(P.K) + 1 : 1; idx <= l; ++idx) {
-        const uint32_t o = ring_slot_off(g, P.K, uint32_t((idx - 1) & int(P.kmask)));
+        const uint32_t o = ring_in_tile(g, R, uint32_t((idx - 1) & int(P.kmask)), uint32_t(r));
         h = dg_mix(h, lo32(at(P.log_term + rb, o)) | (lo32(idx) << 32));
         h = dg_mix(h, uint64_t(at(P.log_value + rb, o)));
         h = dg_mix(h, P.crc_on ? uint64_t(at(P.log_crc + rb, o)) : 0ull);

@@ -72,14 +72,21 @@ struct DevPlanes {
   uint32_t kmask;
 };
 
-// Ring layout: each replica's ring is tiled by waves of 64 groups,
-// [R][Gp/64][K][64]: entry slot s of group g sits at ((g/64)*K + s)*64 + g%64.
-// Groups whose logs are in step (steady state) write one contiguous 256-B
-// term row / 512-B value row per wave and entry; groups whose log lengths
-// have drifted apart (churn) still stay inside one K*64-entry tile per wave
-// instead of scattering over K slabs of Gp entries (TLB misses).
-__device__ __forceinline__ uint32_t ring_slot_off(uint32_t g, uint32_t K, uint32_t slot) {
-  return ((g >> 6) * K + slot) * 64u + (g & 63u);
+// Ring layout: the log rings of all R replicas are tiled by waves of 64
+// groups, [Gp/64][K][64][R] (replica innermost): entry slot s of replica r
+// of group g sits at element ((g/64)*K + s)*64*R + (g%64)*R + r.
+// * steady groups (logs in step, the same slot across a wave) write one
+//   contiguous 64*R*4-B term row / 64*R*8-B value row per wave and entry;
+// * groups whose log lengths drifted apart (churn) still write the R copies
+//   of an entry next to each other (R*4 + R*8 contiguous bytes per lane
+//   instead of 2R separate lines), and a wave stays inside one K*64*R tile.
+// The tile base is 64-bit (wave-uniform in the fast kernel), the offset
+// inside a tile 32-bit (K*64*R <= 2^21).
+__device__ __forceinline__ uint64_t ring_tile(uint32_t g, uint32_t K, uint32_t R) {
+  return uint64_t(g >> 6) * (K * 64u * R);
+}
+__device__ __forceinline__ uint32_t ring_in_tile(uint32_t g, uint32_t R, uint32_t slot, uint32_t r) {
+  return (slot * 64u + (g & 63u)) * R + r;
 }
 
 // Addressing: every access is a wave-uniform base (SGPRs: plane + replica
@@ -360,17 +367,17 @@ struct Group {
   }
 
   // Log ring of replica r: entry idx (1-based) at slot (idx-1) mod K.
-  __device__ __forceinline__ uint32_t ring_off(const DevPlanes& P, int idx) const {
-    return ring_slot_off(g, P.K, uint32_t((idx - 1) & int(P.kmask)));
+  __device__ __forceinline__ uint32_t ring_off(const DevPlanes& P, int r, int idx) const {
+    return ring_in_tile(g, R, uint32_t((idx - 1) & int(P.kmask)), uint32_t(r));
   }
   __device__ __forceinline__ int32_t& ring_term(const DevPlanes& P, int r, int idx) const {
-    return at(P.log_term + uint64_t(r) * P.K * P.Gp, ring_off(P, idx));
+    return at(P.log_term + ring_tile(g, P.K, R), ring_off(P, r, idx));
   }
   __device__ __forceinline__ int64_t& ring_value(const DevPlanes& P, int r, int idx) const {
-    return at(P.log_value + uint64_t(r) * P.K * P.Gp, ring_off(P, idx));
+    return at(P.log_value + ring_tile(g, P.K, R), ring_off(P, r, idx));
   }
   __device__ __forceinline__ uint32_t& ring_crc(const DevPlanes& P, int r, int idx) const {
-    return at(P.log_crc + uint64_t(r) * P.K * P.Gp, ring_off(P, idx));
+    return at(P.log_crc + ring_tile(g, P.K, R), ring_off(P, r, idx));
   }
   // EXT: is the AppendEntries delivered to replica p this tick corrupted?
   __device__ __forceinline__ int corrupted(const DevPlanes& P, int p) const {
@@ -951,7 +958,7 @@ struct TickSrc {
   const uint32_t* lc;
   const uint32_t* tab;
   uint32_t crc_on;
-  uint64_t Gp;
+  uint32_t R;          // replicas (ring layout)
   uint32_t g, K, kmask;
   int leader, from;
   int cache_leader, cache_from, cache_term;
@@ -964,11 +971,11 @@ struct TickSrc {
       v = entry_value(cache_vbase, uint32_t(idx - cache_from));
       if (crc_on) c = crc_entry(tab, t, v);   // the leader's stamp of its own fresh entry
     } else {
-      const uint64_t rb = uint64_t(leader) * K * Gp;
-      const uint32_t o = ring_slot_off(g, K, uint32_t((idx - 1) & int(kmask)));
-      t = at(lt + rb, o);
-      v = at(lv + rb, o);
-      if (crc_on) c = at(lc + rb, o);
+      const uint64_t tb = ring_tile(g, K, R);
+      const uint32_t o = ring_in_tile(g, R, uint32_t((idx - 1) & int(kmask)), uint32_t(leader));
+      t = at(lt + tb, o);
+      v = at(lv + tb, o);
+      if (crc_on) c = at(lc + tb, o);
     }
   }
 };
