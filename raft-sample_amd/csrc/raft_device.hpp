@@ -202,9 +202,9 @@ template <int R>
 __device__ __forceinline__ int sel(const LArr<R>& a, int c) { return a[c]; }
 template <int R>
 __device__ __forceinline__ void put(LArr<R>& a, int c, int v) { a[c] = v; }
-// LDS ints one Group needs per lane (6 arrays of R)
+// LDS ints one Group needs per lane (9 arrays of R)
 template <int R>
-constexpr int group_lds_ints() { return 6 * R; }
+constexpr int group_lds_ints() { return 9 * R; }
 
 template <int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -229,6 +229,12 @@ struct Group {
   // term, last, commit, dl (deadline), dur (timer duration), hw (RAFT:
   // high-water mark of each log; REF: unused) live in LDS (bind())
   LArr<R> term, last, commit, dl, dur, hw;
+  // resident copies of the primary leader's MatchIndex / NextIndex rows and
+  // of every replica's last-entry term (lmatch / lnext / lterm planes):
+  // loaded once (rows lazily), written back once by store()
+  LArr<R> pm, pn, ltm;
+  uint32_t rows_m, rows_n;   // pm / pn hold the plane rows
+  uint32_t d_pm, d_pn, d_lt;
   uint32_t roles;       // 2 bits per replica
   uint32_t votes;       // 4 bits per replica: REF Voted (0/1), RAFT votedFor+1
   uint32_t known;       // deadline register valid
@@ -269,6 +275,7 @@ struct Group {
     int* b = lds + threadIdx.x;
     term.p = b; last.p = b + R * 256; commit.p = b + 2 * R * 256;
     dl.p = b + 3 * R * 256; dur.p = b + 4 * R * 256; hw.p = b + 5 * R * 256;
+    pm.p = b + 6 * R * 256; pn.p = b + 7 * R * 256; ltm.p = b + 8 * R * 256;
   }
   __device__ __forceinline__ void begin(const DevPlanes& P, const Trace& T, uint32_t g_) {
     g = g_;
@@ -276,6 +283,8 @@ struct Group {
     tick = T.tick;
     now = T.now;
     d_term = d_last = d_commit = d_dl = d_rs = d_hw = 0;
+    d_pm = d_pn = d_lt = 0;
+    rows_m = rows_n = 0;
     known = 0;
     iso = 0;
 #pragma unroll
@@ -315,6 +324,7 @@ struct Group {
       votes |= ((x >> 2) & 15u) << (4 * r);
       dur[r] = int(x >> 6);
       hw[r] = (SEM == SEM_RAFT) ? at(prow(P.hwm, r, P.Gp), g) : 0;
+      ltm[r] = at(prow(P.lterm, r, P.Gp), g);
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) dl[r] = with_deadlines ? eff_start(at(prow(P.tstart, r, P.Gp), g), r) + dur[r] : 0;
@@ -322,11 +332,14 @@ struct Group {
     // materialise the rows the fast kernel kept implicit: MatchIndex = LastApplied
     // (RAFT also NextIndex = LastApplied+1 and high-water mark = LastApplied)
     if ((meta0 & M_MSYNC) && primary < R) {
+      const uint32_t peers = ((1u << R) - 1u) & ~(1u << primary);
+      rows_m = 1; d_pm = peers;
+      if constexpr (SEM == SEM_RAFT) { rows_n = 1; d_pn = peers; }
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p != primary) {
-          at(prow(P.lmatch, p, P.Gp), g) = last[p];
-          if constexpr (SEM == SEM_RAFT) at(prow(P.lnext, p, P.Gp), g) = last[p] + 1;
+          pm[p] = last[p];
+          if constexpr (SEM == SEM_RAFT) pn[p] = last[p] + 1;
         }
         if constexpr (SEM == SEM_RAFT) {
           if (hw[p] != last[p]) { hw[p] = last[p]; d_hw |= 1u << p; }
@@ -334,7 +347,7 @@ struct Group {
       }
     }
   }
-  __device__ __forceinline__ void store(const DevPlanes& P) const {
+  __device__ __forceinline__ void store(const DevPlanes& P) const {   // also flushes the resident rows
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if ((d_term >> r) & 1u) at(prow(P.term, r, P.Gp), g) = term[r];
@@ -345,6 +358,9 @@ struct Group {
         at(prow(P.rs, r, P.Gp), g) =
             uint16_t(((roles >> (2 * r)) & 3u) | (((votes >> (4 * r)) & 15u) << 2) | (uint32_t(dur[r]) << 6));
       if (SEM == SEM_RAFT && ((d_hw >> r) & 1u)) at(prow(P.hwm, r, P.Gp), g) = hw[r];
+      if ((d_lt >> r) & 1u) at(prow(P.lterm, r, P.Gp), g) = ltm[r];
+      if ((d_pm >> r) & 1u) at(prow(P.lmatch, r, P.Gp), g) = pm[r];
+      if (SEM == SEM_RAFT && ((d_pn >> r) & 1u)) at(prow(P.lnext, r, P.Gp), g) = pn[r];
     }
     // The primary leader stepped down while another replica leads: move that
     // leader's rows into the coalesced primary planes so the group can take
@@ -423,6 +439,9 @@ struct Group {
     known |= 1u << Rp;
     d_dl |= 1u << Rp;
   }
+  __device__ __forceinline__ void set_lterm(int r, int t) {   // Log[len-1].Term cache
+    if (ltm[r] != t) { ltm[r] = t; d_lt |= 1u << r; }
+  }
   template <int Rp>
   __device__ __forceinline__ void set_term(int t) {
     if (term[Rp] != t) { term[Rp] = t; d_term |= 1u << Rp; }
@@ -467,7 +486,7 @@ struct Group {
     if (q.n) {
       last[Rp] = nl;
       d_last |= 1u << Rp;
-      at(prow(P.lterm, Rp, P.Gp), g) = tl;
+      set_lterm(Rp, tl);
     }
     if (q.lc > commit[Rp]) {                                  // 151-152: min(LC, len(Log)+1)
       const int64_t cap = int64_t(nl) + 1;
@@ -561,7 +580,9 @@ struct Group {
         primary = c;
 #pragma unroll
         for (int p = 0; p < R; ++p)
-          if (p != c) at(prow(P.lmatch, p, P.Gp), g) = 0;
+          if (p != c) pm[p] = 0;
+        rows_m = 1;
+        d_pm |= ((1u << R) - 1u) & ~(1u << c);
       } else {
 #pragma unroll
         for (int p = 0; p < R; ++p)
@@ -591,20 +612,32 @@ struct Group {
 
   // MatchIndex row of leader c: the primary leader's row lives in the
   // coalesced lmatch planes, any other concurrent leader's in xmatch.
-  __device__ __forceinline__ void load_match(const DevPlanes& P, int c, int (&m)[R]) const {
+  __device__ __forceinline__ void load_match(const DevPlanes& P, int c, int (&m)[R]) {
     if (primary == c) {
+      if (!rows_m) {
 #pragma unroll
-      for (int p = 0; p < R; ++p) m[p] = (p != c) ? at(prow(P.lmatch, p, P.Gp), g) : 0;
+        for (int p = 0; p < R; ++p) pm[p] = at(prow(P.lmatch, p, P.Gp), g);
+        rows_m = 1;
+      }
+#pragma unroll
+      for (int p = 0; p < R; ++p) m[p] = (p != c) ? pm[p] : 0;
     } else {
 #pragma unroll
       for (int p = 0; p < R; ++p) m[p] = (p != c) ? at(prow(P.xmatch, c * R + p, P.Gp), g) : 0;
     }
   }
-  __device__ __forceinline__ void store_match(const DevPlanes& P, int c, const int (&m)[R], uint32_t dirty) const {
+  __device__ __forceinline__ void store_match(const DevPlanes& P, int c, const int (&m)[R], uint32_t dirty) {
     if (primary == c) {
+      dirty &= ~(1u << c);
+      if (!rows_m && dirty != (((1u << R) - 1u) & ~(1u << c))) {   // partial update: fetch the row first
+#pragma unroll
+        for (int p = 0; p < R; ++p) pm[p] = at(prow(P.lmatch, p, P.Gp), g);
+      }
+      rows_m = 1;
 #pragma unroll
       for (int p = 0; p < R; ++p)
-        if (p != c && ((dirty >> p) & 1u)) at(prow(P.lmatch, p, P.Gp), g) = m[p];
+        if ((dirty >> p) & 1u) pm[p] = m[p];
+      d_pm |= dirty;
     } else {
 #pragma unroll
       for (int p = 0; p < R; ++p)
@@ -669,7 +702,7 @@ struct Group {
     ring_term(P, c, l + 1) = t;
     ring_value(P, c, l + 1) = v;
     if (P.crc_on) ring_crc(P, c, l + 1) = crc_entry(P.crc_tab, t, v);
-    at(P.lterm + uint64_t(c) * P.Gp, g) = t;
+    set_lterm(c, t);
     put(last, c, l + 1);
     d_last |= 1u << c;
     if (SEM == SEM_RAFT && l + 1 > sel(hw, c)) { put(hw, c, l + 1); d_hw |= 1u << c; }
@@ -716,7 +749,7 @@ struct Group {
     }
   }
   __device__ __forceinline__ int lterm_of(const DevPlanes& P, int r, int l) const {
-    return l > 0 ? at(P.lterm + uint64_t(r) * P.Gp, g) : 0;
+    return l > 0 ? ltm[r] : 0;
   }
   template <int Rp>
   __device__ __forceinline__ void r_grew(int nl) {   // the log reached length nl
@@ -795,7 +828,7 @@ struct Group {
       }
       const int nl = q.prev_idx + q.n;
       if (nl != l) { last[Rp] = nl; d_last |= 1u << Rp; }
-      at(prow(P.lterm, Rp, P.Gp), g) = tl;
+      set_lterm(Rp, tl);
       r_grew<Rp>(nl);
     }
     const int last_new = q.prev_idx + q.n;
@@ -835,20 +868,32 @@ struct Group {
     return 0;
   }
 
-  __device__ __forceinline__ void load_next(const DevPlanes& P, int c, int (&nx)[R]) const {
+  __device__ __forceinline__ void load_next(const DevPlanes& P, int c, int (&nx)[R]) {
     if (primary == c) {
+      if (!rows_n) {
 #pragma unroll
-      for (int p = 0; p < R; ++p) nx[p] = (p != c) ? at(prow(P.lnext, p, P.Gp), g) : 0;
+        for (int p = 0; p < R; ++p) pn[p] = at(prow(P.lnext, p, P.Gp), g);
+        rows_n = 1;
+      }
+#pragma unroll
+      for (int p = 0; p < R; ++p) nx[p] = (p != c) ? pn[p] : 0;
     } else {
 #pragma unroll
       for (int p = 0; p < R; ++p) nx[p] = (p != c) ? at(prow(P.xnext, c * R + p, P.Gp), g) : 0;
     }
   }
-  __device__ __forceinline__ void store_next(const DevPlanes& P, int c, const int (&nx)[R], uint32_t dirty) const {
+  __device__ __forceinline__ void store_next(const DevPlanes& P, int c, const int (&nx)[R], uint32_t dirty) {
     if (primary == c) {
+      dirty &= ~(1u << c);
+      if (!rows_n && dirty != (((1u << R) - 1u) & ~(1u << c))) {
+#pragma unroll
+        for (int p = 0; p < R; ++p) pn[p] = at(prow(P.lnext, p, P.Gp), g);
+      }
+      rows_n = 1;
 #pragma unroll
       for (int p = 0; p < R; ++p)
-        if (p != c && ((dirty >> p) & 1u)) at(prow(P.lnext, p, P.Gp), g) = nx[p];
+        if ((dirty >> p) & 1u) pn[p] = nx[p];
+      d_pn |= dirty;
     } else {
 #pragma unroll
       for (int p = 0; p < R; ++p)

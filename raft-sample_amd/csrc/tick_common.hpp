@@ -68,7 +68,7 @@ __device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, c
       if (n_ok) {
         G.last[r] = l + n_ok;
         G.d_last |= 1u << r;
-        at(prow(P.lterm, r, P.Gp), G.g) = G.term[r];
+        G.set_lterm(r, G.term[r]);
         if constexpr (SEM == SEM_RAFT) G.template r_grew<r>(l + n_ok);
       }
       if (n_ok < int(E)) G.raise(F_OVERFLOW);
