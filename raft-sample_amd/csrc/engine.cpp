@@ -323,6 +323,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.lmatch), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.xmatch), R * R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.gmeta), Gp * 2);
+  A(reinterpret_cast<void**>(&e->P.grot), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.lterm), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->work), Gp * 4);
   A(reinterpret_cast<void**>(&e->work_tick), Gp * 4);
@@ -373,6 +374,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(e->P.gmeta), uint16_t(NO_PRIMARY), Gp,
                                            e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.lterm, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.grot, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, 256, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_value, 0, R * K * Gp * 8, e->stream) : z;
@@ -439,7 +441,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
   const bool raft = e->cfg.semantics == RAFT_SEM_RAFT;
   std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt, ln, xn, hw;
-  std::vector<uint16_t> rs, meta;
+  std::vector<uint16_t> rs, meta, rot;
   std::vector<int64_t> lv;
   std::vector<uint32_t> lcrc;
   int rc = RAFT_OK;
@@ -458,6 +460,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   const bool logs = v->log_term || v->log_value || v->log_crc;
   std::vector<int32_t> ltm;
   if (!rc && logs) rc = d2h(e, ltm, e->P.lterm, R * Gp);
+  if (!rc && logs) rc = d2h(e, rot, e->P.grot, Gp);
   if (!rc && logs) rc = d2h(e, lt, e->P.log_term, R * K * Gp);
   if (!rc && logs) rc = d2h(e, lv, e->P.log_value, R * K * Gp);
   const bool crcs = v->log_crc && e->cfg.payload_crc;
@@ -499,7 +502,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
           v->next[c * R + p] = nx;
         }
       if (logs && last[d] > 0) {
-        const int32_t want = lt[ring_index(r, g, uint64_t((last[d] - 1) & int64_t(K - 1)), K, R)];
+        const int32_t want = lt[ring_index(r, g, uint64_t((last[d] - 1 + rot[g]) & int64_t(K - 1)), K, R)];
         if (ltm[d] != want)
           return fail(RAFT_EINVAL, "internal: last-entry term cache of group %llu replica %llu is %d, ring says %d",
                       (unsigned long long)g, (unsigned long long)r, ltm[d], want);
@@ -510,7 +513,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
           // slot s holds the largest index i <= l with (i-1) mod K == s
           int64_t idx = l >= 1 ? l - ((l - 1 - int64_t(s)) & int64_t(K - 1)) : 0;
           const bool live = idx >= 1 && idx <= l && idx > int64_t(hwm) - int64_t(K);
-          const uint64_t o = ring_index(r, g, s, K, R);
+          const uint64_t o = ring_index(r, g, (s + rot[g]) & (K - 1), K, R);   // physical slot
           if (v->log_term) v->log_term[c * K + s] = live ? lt[o] : 0;
           if (v->log_value) v->log_value[c * K + s] = live ? lv[o] : 0;
           if (v->log_crc) v->log_crc[c * K + s] = (live && crcs) ? lcrc[o] : 0u;
@@ -601,6 +604,8 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.lmatch, lm);
   if (!rc) rc = h2d(e, e->P.xmatch, xm);
   if (!rc) rc = h2d(e, e->P.gmeta, meta);
+  const std::vector<uint16_t> rot(Gp, 0);   // loaded rings: logical slot = physical slot
+  if (!rc) rc = h2d(e, e->P.grot, rot);
   if (!rc) rc = h2d(e, e->P.lterm, ltm);
   if (!rc && raft) rc = h2d(e, e->P.lnext, ln);
   if (!rc && raft) rc = h2d(e, e->P.xnext, xn);

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
   const int n = int(T.client_entries());   // entries per leader this tick (wave-uniform)
   // this lane's ring writes, issued after the per-group code (wave-converged)
   uint32_t wr = 0;      // replicas that append this tick's entries (leader + accepting followers)
-  int w_term = 0, w_idx = 0;   // their term and first index - 1 (the leader's LastApplied)
+  int w_term = 0, w_ph = 0;    // their term and the ring slot of the first entry
   uint64_t w_vb = 0;    // value stream base of this tick's entries
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
@@ -211,10 +211,11 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         for (int p = 0; p < R; ++p)
           if (((okm >> p) & 1u) && last[p] - n != Ll) same = false;
         const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+        const int rot = at(P.grot, g);   // ring rotation: index i at slot (i-1+rot) mod K
         if (same) {
           wr = okm | (1u << c);
           w_term = Lt;
-          w_idx = Ll;
+          w_ph = (Ll + rot) & int(P.kmask);
           w_vb = vb;
         } else {   // rare: write here, each replica at its own LastApplied+1+e
           const uint64_t tb = ring_tile(g, P.K, R);
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
             for (int p = 0; p < R; ++p) {
               if (p != c && !((okm >> p) & 1u)) continue;
               const int i0 = p == c ? Ll : last[p] - n;
-              const uint32_t o = ring_in_tile(g, R, uint32_t((i0 + e) & int(P.kmask)), uint32_t(p));
+              const uint32_t o = ring_in_tile(g, R, uint32_t((i0 + e + rot) & int(P.kmask)), uint32_t(p));
               st<WT>(P.log_term + tb, o, Lt);
               st<WT>(P.log_value + tb, o, v);
               if constexpr (CRC) st<WT>(P.log_crc + tb, o, stamp);
@@ -240,13 +241,15 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     if (bail) at(P.gmeta, g) = uint16_t(meta | M_DEFER);
   }
   // ---- this tick's log entries into the rings (all lanes of the wave) ----
-  // Ring row of one slot = 64 lanes x R replicas, contiguous. When every
-  // writing lane of the wave appends at the same slot (logs in step: the
-  // steady state), the wave writes whole rows cooperatively: store k covers
-  // row elements k*64 + lane, i.e. (group lane (k*64+lane)/R, replica
-  // (k*64+lane)%R), whose term/value/stamp come from that group's lane by
-  // shuffle — R fully contiguous stores per plane and entry. Otherwise
-  // (drifted logs) each lane writes its own R-contiguous segment.
+  // Ring row of one slot = 64 lanes x R replicas, contiguous. The lanes of
+  // the wave that append at the wave's common slot s0 (logs in step: the
+  // steady state; groups that drifted apart under churn do not) write whole
+  // rows cooperatively: store k covers row elements k*64 + lane, i.e. (group
+  // lane (k*64+lane)/R, replica (k*64+lane)%R), whose term/value/stamp come
+  // from that group's lane by shuffle — R contiguous stores per plane and
+  // entry. Every other writing lane stores its own R-contiguous segment.
+  // s0: the global phase entries_before(tick) (groups rotated at their first
+  // entry, init_steady) or the first writer's slot, whichever more lanes share.
   if (n) {
     const uint64_t wball = __ballot(wr != 0);
     if (wball) {
@@ -256,21 +259,25 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       int32_t* const rt = P.log_term + tb;
       int64_t* const rv = P.log_value + tb;
       uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
-      const int s0 = __shfl(w_idx, int(__builtin_ctzll(wball)));
-      const bool aligned = __all(wr == 0 || ((w_idx - s0) & int(P.kmask)) == 0);
+      const int sa = __shfl(w_ph, int(__builtin_ctzll(wball)));
+      const int sb = int(T.entries_before(T.tick) & P.kmask);
+      const int na = __popcll(__ballot(wr != 0 && w_ph == sa)), nb = __popcll(__ballot(wr != 0 && w_ph == sb));
+      const int s0 = nb >= na ? sb : sa;
+      const bool coop = wr != 0 && w_ph == s0;
       uint32_t cs = 0;
       if constexpr (CRC) cs = crc_term_state(tab, w_term);
-      if (aligned) {
+      {
         int k_term[R];
         uint32_t k_on[R];
         int k_src[R];
+        const int cwr = coop ? int(wr) : 0;
 #pragma unroll
         for (int k = 0; k < R; ++k) {
           const int j = k * 64 + lane;
           const int src = j / R, rr = j - src * R;
           k_src[k] = src;
           k_term[k] = __shfl(w_term, src);
-          k_on[k] = (uint32_t(__shfl(int(wr), src)) >> rr) & 1u;
+          k_on[k] = (uint32_t(__shfl(cwr, src)) >> rr) & 1u;
         }
         for (int e = 0; e < n; ++e) {
           const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
@@ -290,19 +297,15 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
               if constexpr (CRC) st<WT>(rc, o, sk);
             }
           }
-        }
-      } else if (wr) {
-        for (int e = 0; e < n; ++e) {
-          const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
-          uint32_t stamp = 0;
-          if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
-          const uint32_t o = ring_in_tile(g, R, uint32_t((w_idx + e) & int(P.kmask)), 0u);
+          if (wr != 0 && !coop) {   // drifted lane: its own segment
+            const uint32_t o = ring_in_tile(g, R, uint32_t((w_ph + e) & int(P.kmask)), 0u);
 #pragma unroll
-          for (int p = 0; p < R; ++p) {
-            if (!((wr >> p) & 1u)) continue;
-            st<WT>(rt, o + p, w_term);
-            st<WT>(rv, o + p, v);
-            if constexpr (CRC) st<WT>(rc, o + p, stamp);
+            for (int p = 0; p < R; ++p) {
+              if (!((wr >> p) & 1u)) continue;
+              st<WT>(rt, o + p, w_term);
+              st<WT>(rv, o + p, v);
+              if constexpr (CRC) st<WT>(rc, o + p, stamp);
+            }
           }
         }
       }

@@ -58,6 +58,7 @@ struct DevPlanes {
   int32_t* xnext;      // RAFT mode: [R][R][Gp] NextIndex rows of further leaders
   int32_t* hwm;        // RAFT mode: [R][Gp] highest LastApplied ever (== last in REF)
   uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
+  uint16_t* grot;      // ring rotation: entry idx of every replica sits at slot (idx-1+rot) mod K
   int32_t* lterm;      // [R][Gp] Log[len-1].Term: cached term of each replica's last entry
   int32_t* log_term;   // Log.Term  ring, [R] x tiles [Gp/64][K][64] (ring_slot_off)
   int64_t* log_value;  // Log.Value ring
@@ -120,6 +121,11 @@ struct Trace {          // per-launch trace parameters (virtual clock + RNG)
   }
   __device__ __forceinline__ uint32_t client_entries() const {
     return (period && (tick % int64_t(period)) == 0) ? entries : 0u;
+  }
+  // Client entries of all ticks before t (ticks >= 0): the ring phase that
+  // keeps every steady group's appends in the same slots (ring_phase()).
+  __device__ __forceinline__ uint64_t entries_before(int64_t t) const {
+    return period && t > 0 ? uint64_t((t + int64_t(period) - 1) / int64_t(period)) * entries : 0u;
   }
 };
 
@@ -234,6 +240,7 @@ struct Group {
   // loaded once (rows lazily), written back once by store()
   LArr<R> pm, pn, ltm;
   uint32_t rows_m, rows_n;   // pm / pn hold the plane rows
+  uint32_t rot, rot0;        // ring rotation (grot) now / as loaded
   uint32_t d_pm, d_pn, d_lt;
   uint32_t roles;       // 2 bits per replica
   uint32_t votes;       // 4 bits per replica: REF Voted (0/1), RAFT votedFor+1
@@ -296,6 +303,7 @@ struct Group {
     primary = m & 0xF;
     fault = (m >> 4) & 0xF;
     hbt = HB_NONE;
+    rot = rot0 = at(P.grot, g);
   }
   // Per-tick reset of a group whose state stays resident across ticks
   // (general kernel catch-up): clock, counters, this tick's entry cache.
@@ -362,6 +370,7 @@ struct Group {
       if ((d_pm >> r) & 1u) at(prow(P.lmatch, r, P.Gp), g) = pm[r];
       if (SEM == SEM_RAFT && ((d_pn >> r) & 1u)) at(prow(P.lnext, r, P.Gp), g) = pn[r];
     }
+    if (rot != rot0) at(P.grot, g) = uint16_t(rot);
     // The primary leader stepped down while another replica leads: move that
     // leader's rows into the coalesced primary planes so the group can take
     // the steady-state kernel again (placement only; no state changes).
@@ -384,7 +393,17 @@ struct Group {
 
   // Log ring of replica r: entry idx (1-based) at slot (idx-1) mod K.
   __device__ __forceinline__ uint32_t ring_off(const DevPlanes& P, int r, int idx) const {
-    return ring_in_tile(g, R, uint32_t((idx - 1) & int(P.kmask)), uint32_t(r));
+    return ring_in_tile(g, R, uint32_t((idx - 1 + int(rot)) & int(P.kmask)), uint32_t(r));
+  }
+  // Every log of the group is empty (RAFT: nothing above LastApplied either):
+  // the ring holds no entry, so its rotation is free. Chosen so that the
+  // entry appended at tick t lands in slot entries_before(t) mod K, the slot
+  // every other steady group appends to at t (coalesced ring rows).
+  __device__ __forceinline__ void align_ring(const DevPlanes& P, const Trace& T) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (last[r] != 0 || (SEM == SEM_RAFT && hw[r] != 0)) return;
+    rot = uint32_t(T.entries_before(T.tick)) & P.kmask;
   }
   __device__ __forceinline__ int32_t& ring_term(const DevPlanes& P, int r, int idx) const {
     return at(P.log_term + ring_tile(g, P.K, R), ring_off(P, r, idx));
@@ -1004,7 +1023,7 @@ struct TickSrc {
   const uint32_t* tab;
   uint32_t crc_on;
   uint32_t R;          // replicas (ring layout)
-  uint32_t g, K, kmask;
+  uint32_t g, K, kmask, rot;
   int leader, from;
   int cache_leader, cache_from, cache_term;
   uint64_t cache_vbase;
@@ -1017,7 +1036,7 @@ struct TickSrc {
       if (crc_on) c = crc_entry(tab, t, v);   // the leader's stamp of its own fresh entry
     } else {
       const uint64_t tb = ring_tile(g, K, R);
-      const uint32_t o = ring_in_tile(g, R, uint32_t((idx - 1) & int(kmask)), uint32_t(leader));
+      const uint32_t o = ring_in_tile(g, R, uint32_t((idx - 1 + int(rot)) & int(kmask)), uint32_t(leader));
       t = at(lt + tb, o);
       v = at(lv + tb, o);
       if (crc_on) c = at(lc + tb, o);

@@ -53,6 +53,7 @@ __device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, c
       if (G.role(r) != ROLE_L || !G.alive()) return;
       const uint64_t vb = rng_k_call(G.key, r, ST_VALUE, uint64_t(G.tick));
       const int l = G.last[r];
+      if (l == 0) G.align_ring(P, T);   // first entry of an empty group: choose the ring phase
       const int room = I32MAX - l;
       const int n_ok = int(E) <= room ? int(E) : room;
       if (G.cache_leader < 0) {
@@ -76,7 +77,7 @@ __device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, c
   }
 
   // 2. rounds in ascending replica id, against the roles as they are now.
-  const TickSrc base{P.log_term, P.log_value, P.log_crc, P.crc_tab, P.crc_on, uint32_t(R), G.g, P.K, P.kmask, 0, 1,
+  const TickSrc base{P.log_term, P.log_value, P.log_crc, P.crc_tab, P.crc_on, uint32_t(R), G.g, P.K, P.kmask, G.rot, 0, 1,
                      G.cache_leader, G.cache_from, G.cache_term, G.cache_vbase};
   auto make_src = [base](int c) {
     TickSrc s = base;
