@@ -458,6 +458,12 @@ struct Group {
     known |= 1u << Rp;
     d_dl |= 1u << Rp;
   }
+  // Log[idx].Term of replica r (1 <= idx <= its LastApplied): the last entry's
+  // term is resident (ltm), so the common prevLogIndex == LastApplied check
+  // costs no dependent HBM read; older entries come from the ring.
+  __device__ __forceinline__ int term_at(const DevPlanes& P, int r, int idx) const {
+    return idx == last[r] ? ltm[r] : ring_term(P, r, idx);
+  }
   __device__ __forceinline__ void set_lterm(int r, int t) {   // Log[len-1].Term cache
     if (ltm[r] != t) { ltm[r] = t; d_lt |= 1u << r; }
   }
@@ -479,7 +485,7 @@ struct Group {
       if (int64_t(l) + q.n < q.prev_idx) return res;          // 137-140
       if (q.prev_idx < 1 || q.prev_idx > l) { raise(F_PANIC_GETLOG); return res; }  // 142 -> 404
       if (q.prev_idx <= l - int(P.K)) { raise(F_RING_EVICTED); return res; }
-      if (ring_term(P, Rp, q.prev_idx) != q.prev_term) return res;                 // 142-145
+      if (term_at(P, Rp, q.prev_idx) != q.prev_term) return res;                   // 142-145
     }
     if (int64_t(l) + q.n > I32MAX) { raise(F_OVERFLOW); return res; }
     // 148-149: append all Logs at the end (no truncation); only the last K
@@ -689,7 +695,7 @@ struct Group {
         } else {                                              // 353-360
           if (nxt < 1 || m[p] > ll) { raise(F_PANIC_GETLOG); return; }
           if (m[p] <= ll - int(P.K)) { raise(F_RING_EVICTED); return; }
-          q.prev_term = ring_term(P, c, m[p]);                // GetLog(MatchIndex).Term
+          q.prev_term = term_at(P, c, m[p]);                  // GetLog(MatchIndex).Term
           q.prev_idx = m[p]; q.n = ll - nxt + 1; from = nxt;
         }
       } else {                                                // 364-371: heartbeat
@@ -810,7 +816,7 @@ struct Group {
     if (q.prev_idx > l) return res;               // log too short: hint = last
     if (q.prev_idx > 0) {
       if (q.prev_idx <= hw[Rp] - K) { raise(F_RING_EVICTED); return res; }
-      if (ring_term(P, Rp, q.prev_idx) != q.prev_term) {     // conflict: back off to the committed prefix
+      if (term_at(P, Rp, q.prev_idx) != q.prev_term) {       // conflict: back off to the committed prefix
         res.match = q.prev_idx - 1 < commit[Rp] ? q.prev_idx - 1 : commit[Rp];
         return res;
       }
@@ -833,7 +839,7 @@ struct Group {
       if (idx <= hw[Rp] - K) { raise(F_RING_EVICTED); return res; }
       int t; int64_t v; uint32_t c;
       src.fetch(j, t, v, c);
-      if (ring_term(P, Rp, idx) != t) break;     // conflict: entries from idx on are replaced
+      if (term_at(P, Rp, idx) != t) break;       // conflict: entries from idx on are replaced
     }
     if (j < q.n) {
       int tl = 0;
@@ -938,7 +944,7 @@ struct Group {
     if (N > cm) {
       if (N < 1 || N > ll) { raise(F_PANIC_GETLOG); return cm; }
       if (N <= lh - int(P.K)) { raise(F_RING_EVICTED); return cm; }
-      if (ring_term(P, c, N) == lt) {
+      if (term_at(P, c, N) == lt) {
         st[S_COMMITTED] += N - cm;
         return N;
       }
@@ -971,7 +977,7 @@ struct Group {
       q.prev_term = 0;
       if (q.prev_idx > 0) {
         if (q.prev_idx <= lh - K) { raise(F_RING_EVICTED); return; }
-        q.prev_term = ring_term(P, c, q.prev_idx);
+        q.prev_term = term_at(P, c, q.prev_idx);
       }
       q.n = ll - q.prev_idx;
       auto src = src0;
