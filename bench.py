@@ -88,10 +88,11 @@ def engine_kwargs(wl, R, G, base, K, E, crc):
     return kw
 
 
-def load_pmc(workload):
-    """HBM traffic per launch from a committed rocprofv3 --pmc summary for
-    this workload (tools/pmc_summary.py), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+def load_pmc(wl_key, workload):
+    """HBM traffic per launch of the steady-state kernel from the committed
+    rocprofv3 --pmc summary of this workload (profiles/pmc_<key>.json, made
+    by tools/pmc_summary.py from FETCH_SIZE / WRITE_SIZE passes), or None."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{wl_key}.json")
     try:
         d = json.load(open(p))
     except (OSError, ValueError):
@@ -198,7 +199,7 @@ def main():
     avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)   # region events / launches: tick kernel + gaps
     achieved = B * G / avg_kernel_s / 1e9
     workload = f"{args.workload}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}"
-    traffic = load_pmc(workload)
+    traffic = load_pmc(args.workload, workload)
     result = {
         "metric": "Raft group-steps/sec at 1M 5-replica groups, 1-8 GPUs; % of HBM peak",
         "value": value,

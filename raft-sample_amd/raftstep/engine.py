@@ -12,7 +12,7 @@ import numpy as np
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libraftstep.so"))
+LIB_PATH = os.environ.get("RAFTSTEP_LIB") or os.path.normpath(os.path.join(_HERE, "..", "lib", "libraftstep.so"))   # env: A/B of another build
 _lib = None
 
 
