@@ -101,6 +101,7 @@ struct raft_engine {
   int force_general = 0;        // debug: route every group through the general kernel
   uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
   int write_through = 0;        // fast kernel stores with sc1 (write-through) instead of write-back
+  int debug_work = 0;           // RAFTSTEP_DEBUG_WORK: print each general-kernel worklist size
   // handler-batch staging
   void* stage = nullptr;
   size_t stage_cap = 0;
@@ -360,6 +361,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
   if (const char* se = getenv("RAFTSTEP_SLOW_EVERY")) e->slow_every = std::max(1, atoi(se));
   if (const char* wt = getenv("RAFTSTEP_WRITE_THROUGH")) e->write_through = atoi(wt) != 0;
+  if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
   // zero everything once so that padding / unused rows are deterministic
   for (void* p : e->allocs) (void)p;
   hipError_t z = hipSuccess;
@@ -652,6 +654,12 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
                             e->stream, a, b));
     // deferred groups catch up every slow_every ticks and at the end of the call
     if ((i + 1) % e->slow_every == 0 || i + 1 == nticks) {
+      if (e->debug_work) {   // diagnostics: worklist size of each general-kernel launch (synchronising)
+        uint32_t nw = 0;
+        HIPCHK(hipMemcpyAsync(&nw, cnt, 4, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        fprintf(stderr, "raftstep: general kernel ticks %lld..%lld worklist %u\n", (long long)win_first, (long long)t, nw);
+      }
       HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t, stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
                               e->wcount + ((window + 1) & 1), e->stream));
       ++window;
