@@ -28,6 +28,13 @@ __device__ __forceinline__ void st(T* base, uint32_t idx, T v) {
   else at(base, idx) = v;
 }
 
+// A ONECAND group is taken only when a replica is isolated this tick (its
+// role, which must be the candidate, is checked once the rs row is read).
+template <bool RAFT>
+__device__ __forceinline__ bool xi_ok(int meta, int xi) {
+  return (meta & M_STEADY) || (RAFT && (meta & M_ONECAND) && xi >= 0);
+}
+
 template <int R, bool WT, bool CRC, int SEM>
 __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, unsigned long long* stats,
                                                         uint32_t* work, int32_t* work_tick, uint32_t* work_count,
@@ -43,7 +50,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     dst[threadIdx.x + 256] = src[threadIdx.x + 256];
     __syncthreads();
   }
-  int sv[4] = {0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups
+  int sv[5] = {0, 0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups, term bumps
   bool bail = false;
   const int n = int(T.client_entries());   // entries per leader this tick (wave-uniform)
   // this lane's ring writes, issued after the per-group code (wave-converged)
@@ -54,7 +61,8 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     const int meta = at(P.gmeta, g);
     const int c = meta & 0xF;
     const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
-    bail = !skip && (force_slow || !(meta & M_STEADY));
+    // RAFT also takes ONECAND groups (their candidate must be isolated this tick, checked below)
+    bail = !skip && (force_slow || !(meta & (RAFT ? (M_STEADY | M_ONECAND) : M_STEADY)));
     int term[R], last[R], commit[R], lt[R], m[R];
     const bool go = !skip && !bail;
     if (go) {
@@ -84,16 +92,46 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     }
     uint64_t key = 0;
     if (go && (T.iso_p || n)) key = group_key(T.seed, P.gbase + g);
-    if (go && T.iso_p) bail |= isolation_mask<R>(key, T) != 0;
+    // RAFT: one isolated replica xi (not the leader) is handled here: it
+    // receives nothing and sends nothing (its AppendEntries is dropped, its
+    // vote requests too), so the rest of the group ticks as usual and xi only
+    // runs its own election timer. Its lagging MatchIndex stays implicit
+    // (MSYNC: MatchIndex[xi] == LastApplied[xi], both unchanged).
+    int xi = -1;
+    if (go && T.iso_p) {
+      const uint32_t im = isolation_mask<R>(key, T);
+      if (RAFT && R >= 3 && im && (im & (im - 1u)) == 0u && int(__builtin_ctz(im)) != c) xi = int(__builtin_ctz(im));
+      else bail |= im != 0u;
+    }
+    if (go && !xi_ok<RAFT>(meta, xi)) bail = true;   // ONECAND needs its candidate isolated (role checked below)
     // leader view
     const int Lt = sel(term, c), Ll = sel(last, c), Lc = sel(commit, c), Llt = sel(lt, c);
     if (go && !bail) bail = int64_t(Ll) + n > I32MAX || n >= int(P.K);
     if (go) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
+        if (p == xi) { bail |= m[p] != last[p] || m[p] > Ll; continue; }   // MSYNC stays exact for xi
         bail |= (p != c) && m[p] != Ll;
         // RAFT: a follower with extra entries or another term takes the general path
         if constexpr (RAFT) bail |= (p != c) && (last[p] != Ll || term[p] != Lt);
+      }
+    }
+    // the isolated replica's own state: role, vote, timer (eff. start = max(tstart, hb))
+    int x_rs = 0, x_term = 0, x_fire = 0, x_dur = 0;
+    if constexpr (RAFT) {
+      if (go && !bail && xi >= 0) {
+        x_rs = at(prow(P.rs, xi, P.Gp), g);
+        x_term = sel(term, xi);
+        const int role = x_rs & 3;
+        // STEADY: xi is a follower; ONECAND: xi is the group's one candidate
+        if (role != ((meta & M_STEADY) ? ROLE_F : ROLE_C)) bail = true;
+        const int dl = max(at(prow(P.tstart, xi, P.Gp), g), at(P.hb, g)) + (x_rs >> 6);
+        if (dl <= T.now) {   // timer.C: Term++, vote for itself, new candidate timer (Raft §5.2)
+          if (x_term >= I32MAX) bail = true;
+          x_fire = 1;
+          x_dur = T.c_min + int(uint32_t(rng_k(key, uint32_t(xi), ST_TIMER_C, uint64_t(T.tick)) >> 32) %
+                                uint32_t(T.c_span));
+        }
       }
     }
     // one AppendEntries shape for every peer (NextIndex == Ll+1)
@@ -109,7 +147,8 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         uint32_t cm = 0;   // followers whose message is corrupted this tick
 #pragma unroll
         for (int p = 0; p < R; ++p)
-          if (p != c && P.corrupt_p && (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(T.tick)) & 0xFFFF) < P.corrupt_p)
+          if (p != c && p != xi && P.corrupt_p &&
+              (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(T.tick)) & 0xFFFF) < P.corrupt_p)
             cm |= 1u << p;
         const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
         const uint32_t cs = crc_term_state(tab, Lt);
@@ -118,7 +157,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
           const uint32_t stamp = crc_value_final(tab, cs, v);               // leader's stamp
 #pragma unroll
           for (int p = 0; p < R; ++p) {
-            if (p == c) continue;
+            if (p == c || p == xi) continue;
             const int64_t rv = v ^ ((((cm >> p) & 1u) && e == n - 1) ? 1 : 0);  // what p received
             if (crc_value_final(tab, cs, rv) != stamp) crcbad |= 1u << p;
           }
@@ -129,7 +168,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     if (go && !bail) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
-        if (p == c) continue;
+        if (p == c || p == xi) continue;   // xi: dropped (sender sees false, receiver unchanged)
         const int l = last[p];
         bool ok;
         if constexpr (RAFT) {
@@ -166,8 +205,9 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       int cm = Lc;
       bool sync = true;
       if constexpr (RAFT) {
-        // every log now ends at Ll+n: the majority index is Ll+n, committed
-        // only if that entry is of the current term (this tick's entries are)
+        // every log now ends at Ll+n (all but at most one lagging isolated
+        // replica, and R >= 3): the majority index is Ll+n, committed only if
+        // that entry is of the current term (this tick's entries are)
         const int N = Ll + n;
         if (N > Lc && (n > 0 || Llt == Lt)) cm = N;
       } else {
@@ -185,24 +225,34 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       sv[1] = __builtin_popcount(okm);
       sv[2] = (R - 1) - sv[1];
       sv[3] = 1;
+      sv[4] = x_fire;
       // ---- stores (no bail past this point) ----
       if (n) {
         st<WT>(P.last + uint64_t(c) * P.Gp, g, Ll + n);
         if (Llt != Lt) st<WT>(P.lterm + uint64_t(c) * P.Gp, g, Lt);
       }
       if (cm != Lc) st<WT>(P.commit + uint64_t(c) * P.Gp, g, cm);
-      st<WT>(P.hb, g, T.now);                                     // timer.Reset(d) of every follower
+      if (xi < 0) st<WT>(P.hb, g, T.now);                         // timer.Reset(d) of every follower
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == c || !((okm >> p) & 1u)) continue;
+        if (xi >= 0) st<WT>(prow(P.tstart, p, P.Gp), g, T.now);   // xi isolated: reset each receiver, not hb
         if (n) st<WT>(prow(P.last, p, P.Gp), g, last[p]);
         if (!sync && ((mch >> p) & 1u)) st<WT>(prow(P.lmatch, p, P.Gp), g, m[p]);
         if ((cch >> p) & 1u) st<WT>(prow(P.commit, p, P.Gp), g, commit[p]);
         if ((ltch >> p) & 1u) st<WT>(prow(P.lterm, p, P.Gp), g, Lt);
         if (!RAFT && term[p] != Lt) st<WT>(prow(P.term, p, P.Gp), g, Lt);  // main.go:155
       }
+      if constexpr (RAFT) {
+        if (x_fire) {   // the isolated replica became / stays a candidate: Term+1, votedFor itself
+          st<WT>(prow(P.term, xi, P.Gp), g, x_term + 1);
+          st<WT>(prow(P.rs, xi, P.Gp), g, uint16_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
+          st<WT>(prow(P.tstart, xi, P.Gp), g, T.now);
+        }
+      }
       // RAFT: MSYNC also makes NextIndex (= match+1) and the high-water marks (= last) implicit
-      const int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
+      int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
+      if (x_fire) nm = (nm & ~M_STEADY) | M_ONECAND;
       if (nm != meta) at(P.gmeta, g) = uint16_t(nm);
       // this tick's entries go to the leader log + every follower that accepted
       if (n) {
@@ -330,8 +380,14 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     work_tick[off] = int32_t(T.tick);
   }
   if (stats) {
-    const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
-    block_stats<4>(sv, idx, stats);
+    if constexpr (RAFT) {
+      const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
+      block_stats<5>(sv, idx, stats);
+    } else {
+      const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
+      const int v4[4] = {sv[0], sv[1], sv[2], sv[3]};
+      block_stats<4>(v4, idx, stats);
+    }
   }
 }
 

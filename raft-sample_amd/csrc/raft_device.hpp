@@ -37,6 +37,7 @@ constexpr int NO_PRIMARY = 0xF;
 constexpr int M_DEFER = 1 << 8;   // on the worklist with ticks pending; the fast kernel leaves it alone
 constexpr int M_MSYNC = 1 << 9;   // primary's MatchIndex[p] == LastApplied[p] for every peer; lmatch is stale
 constexpr int M_STEADY = 1 << 10; // exactly one leader (the primary), every other replica a follower
+constexpr int M_ONECAND = 1 << 11; // as STEADY, except that exactly one other replica is a candidate
 constexpr int HB_NONE = -2147483647 - 1;
 constexpr int I32MAX = 2147483647;
 constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to cut atomic contention
@@ -385,9 +386,13 @@ struct Group {
       }
       pri = nl;
     }
-    // DEFER and MSYNC are consumed by the general path; STEADY is recomputed
-    const bool steady = pri < R && role(pri) == ROLE_L && (roles & ~(3u << (2 * pri))) == 0u;
-    const int m = pri | (fault << 4) | (steady ? M_STEADY : 0);
+    // DEFER and MSYNC are consumed by the general path; STEADY / ONECAND are recomputed
+    const uint32_t others = roles & ~(3u << (2 * pri));
+    const bool led = pri < R && role(pri) == ROLE_L;
+    const bool steady = led && others == 0u;
+    // exactly one non-follower besides the primary, and it is a candidate (ROLE_C = 1)
+    const bool onecand = led && others != 0u && (others & (others - 1u)) == 0u && (others & 0x5555u) != 0u;
+    const int m = pri | (fault << 4) | (steady ? M_STEADY : 0) | (onecand ? M_ONECAND : 0);
     if (m != meta0) at(P.gmeta, g) = uint16_t(m);
   }
 
