@@ -28,6 +28,28 @@ __device__ __forceinline__ void st(T* base, uint32_t idx, T v) {
   else at(base, idx) = v;
 }
 
+// R copies of one value into R consecutive elements (4-B aligned) with the
+// widest stores: 16-B pieces, then the remainder (a drifted lane's ring
+// segment: 2 store instructions for R=7 terms instead of 7).
+template <int N, typename T>
+__device__ __forceinline__ void fill_seg(T* p, T v) {
+  constexpr int per = int(16 / sizeof(T));   // elements per 16-B piece
+  struct __attribute__((aligned(4))) V16 { T x[per]; };
+  V16 w;
+#pragma unroll
+  for (int i = 0; i < per; ++i) w.x[i] = v;
+#pragma unroll
+  for (int i = 0; i + per <= N; i += per) *reinterpret_cast<V16*>(p + i) = w;
+  constexpr int rem = N % per;
+  if constexpr (rem > 0) {
+    struct __attribute__((aligned(4))) VR { T x[rem]; };
+    VR r;
+#pragma unroll
+    for (int i = 0; i < rem; ++i) r.x[i] = v;
+    *reinterpret_cast<VR*>(p + (N - rem)) = r;
+  }
+}
+
 // A ONECAND group is taken only when a replica is isolated this tick (its
 // role, which must be the candidate, is checked once the rs row is read).
 template <bool RAFT>
@@ -349,12 +371,18 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
           }
           if (wr != 0 && !coop) {   // drifted lane: its own segment
             const uint32_t o = ring_in_tile(g, R, uint32_t((w_ph + e) & int(P.kmask)), 0u);
+            if (!WT && wr == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
+              fill_seg<R>(rt + o, w_term);
+              fill_seg<R>(rv + o, v);
+              if constexpr (CRC) fill_seg<R>(rc + o, stamp);
+            } else {
 #pragma unroll
-            for (int p = 0; p < R; ++p) {
-              if (!((wr >> p) & 1u)) continue;
-              st<WT>(rt, o + p, w_term);
-              st<WT>(rv, o + p, v);
-              if constexpr (CRC) st<WT>(rc, o + p, stamp);
+              for (int p = 0; p < R; ++p) {
+                if (!((wr >> p) & 1u)) continue;
+                st<WT>(rt, o + p, w_term);
+                st<WT>(rv, o + p, v);
+                if constexpr (CRC) st<WT>(rc, o + p, stamp);
+              }
             }
           }
         }
