@@ -86,6 +86,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     // RAFT also takes ONECAND groups (their candidate must be isolated this tick, checked below)
     bail = !skip && (force_slow || !(meta & (RAFT ? (M_STEADY | M_ONECAND) : M_STEADY)));
     int term[R], last[R], commit[R], lt[R], m[R];
+    bool empty = true;   // every log of the group empty before this tick
     const bool go = !skip && !bail;
     if (go) {
 #pragma unroll
@@ -94,6 +95,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         last[r] = at(prow(P.last, r, P.Gp), g);
         commit[r] = at(prow(P.commit, r, P.Gp), g);
         lt[r] = at(prow(P.lterm, r, P.Gp), g);
+        empty &= last[r] == 0;
       }
       if (meta & M_MSYNC) {
 #pragma unroll
@@ -283,7 +285,13 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         for (int p = 0; p < R; ++p)
           if (((okm >> p) & 1u) && last[p] - n != Ll) same = false;
         const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
-        const int rot = at(P.grot, g);   // ring rotation: index i at slot (i-1+rot) mod K
+        // ring rotation: index i at slot (i-1+rot) mod K; an empty group's first
+        // entry goes to the global phase (its logs hold nothing to move)
+        int rot = at(P.grot, g);
+        if (empty) {
+          const int r0 = int(T.entries_before(T.tick) & P.kmask);
+          if (r0 != rot) { rot = r0; at(P.grot, g) = uint16_t(rot); }
+        }
         if (same) {
           wr = okm | (1u << c);
           w_term = Lt;

@@ -356,7 +356,10 @@ struct Group {
       }
     }
   }
-  __device__ __forceinline__ void store(const DevPlanes& P) const {   // also flushes the resident rows
+  // Also flushes the resident rows. next_phase: ring phase of the next tick to
+  // be processed (entries_before(tick+1) mod K), taken by a group whose logs
+  // are still empty (the fast kernel may append its first entry next).
+  __device__ __forceinline__ void store(const DevPlanes& P, uint32_t next_phase) const {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if ((d_term >> r) & 1u) at(prow(P.term, r, P.Gp), g) = term[r];
@@ -371,7 +374,14 @@ struct Group {
       if ((d_pm >> r) & 1u) at(prow(P.lmatch, r, P.Gp), g) = pm[r];
       if (SEM == SEM_RAFT && ((d_pn >> r) & 1u)) at(prow(P.lnext, r, P.Gp), g) = pn[r];
     }
-    if (rot != rot0) at(P.grot, g) = uint16_t(rot);
+    {   // logs still empty: pick the phase of the next tick's first entry (the fast kernel may append it)
+      bool empty = true;
+#pragma unroll
+      for (int r = 0; r < R; ++r) empty &= last[r] == 0 && (SEM != SEM_RAFT || hw[r] == 0);
+      uint32_t rt = rot;
+      if (empty && !fault) rt = next_phase & P.kmask;
+      if (rt != rot0) at(P.grot, g) = uint16_t(rt);
+    }
     // The primary leader stepped down while another replica leads: move that
     // leader's rows into the coalesced primary planes so the group can take
     // the steady-state kernel again (placement only; no state changes).
