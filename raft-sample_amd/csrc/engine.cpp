@@ -87,6 +87,7 @@ struct raft_engine {
   raft_config cfg{};
   int R = 0;
   uint64_t Gp = 0;
+  uint64_t KP = 0;   // physical ring slots per replica (ring_depth or 2x)
   hipStream_t stream = nullptr;
   DevPlanes P{};
   std::vector<void*> allocs;
@@ -314,7 +315,14 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   auto A = [&](void** p, size_t bytes) {
     if (rc == RAFT_OK) rc = dev_alloc(e, p, bytes);
   };
-  const uint64_t R = c.replicas, K = c.ring_depth;
+  const uint64_t R = c.replicas;
+  // physical ring slots: 2K where groups can drift out of the global ring
+  // phase (EXT isolation churn), so that their rotation can be switched in
+  // place (raft_device.hpp ring_slot); RAFTSTEP_RING_PHYS=1|2 overrides
+  uint64_t phys = c.isolate_per_65536 > 0 ? 2 : 1;
+  if (const char* rp = getenv("RAFTSTEP_RING_PHYS")) phys = atoi(rp) == 2 ? 2 : 1;
+  const uint64_t K = c.ring_depth * phys;
+  e->KP = K;
   A(reinterpret_cast<void**>(&e->P.term), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.last), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.commit), R * Gp * 4);
@@ -325,6 +333,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.xmatch), R * R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.gmeta), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.grot), Gp * 2);
+  A(reinterpret_cast<void**>(&e->P.grota), Gp * 2);
+  A(reinterpret_cast<void**>(&e->P.gsb), Gp * 4);
   A(reinterpret_cast<void**>(&e->P.lterm), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->work), Gp * 4);
   A(reinterpret_cast<void**>(&e->work_tick), Gp * 4);
@@ -355,7 +365,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->P.G = c.groups;
   e->P.gbase = c.group_base;
   e->P.K = c.ring_depth;
-  e->P.kmask = c.ring_depth - 1;
+  e->P.KP = uint32_t(K);
+  e->P.kmask = uint32_t(K) - 1;
   e->P.crc_on = c.payload_crc;
   e->P.corrupt_p = c.corrupt_per_65536;
   if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
@@ -377,6 +388,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
                                            e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.lterm, 0, R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grot, 0, Gp * 2, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.grota, 0, Gp * 2, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.gsb, 0, Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, 256, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_value, 0, R * K * Gp * 8, e->stream) : z;
@@ -443,7 +456,8 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
   const bool raft = e->cfg.semantics == RAFT_SEM_RAFT;
   std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt, ln, xn, hw;
-  std::vector<uint16_t> rs, meta, rot;
+  std::vector<uint16_t> rs, meta, rot, rota;
+  std::vector<int32_t> sb;
   std::vector<int64_t> lv;
   std::vector<uint32_t> lcrc;
   int rc = RAFT_OK;
@@ -462,11 +476,14 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   const bool logs = v->log_term || v->log_value || v->log_crc;
   std::vector<int32_t> ltm;
   if (!rc && logs) rc = d2h(e, ltm, e->P.lterm, R * Gp);
+  const uint64_t KP = e->KP;
   if (!rc && logs) rc = d2h(e, rot, e->P.grot, Gp);
-  if (!rc && logs) rc = d2h(e, lt, e->P.log_term, R * K * Gp);
-  if (!rc && logs) rc = d2h(e, lv, e->P.log_value, R * K * Gp);
+  if (!rc && logs) rc = d2h(e, rota, e->P.grota, Gp);
+  if (!rc && logs) rc = d2h(e, sb, e->P.gsb, Gp);
+  if (!rc && logs) rc = d2h(e, lt, e->P.log_term, R * KP * Gp);
+  if (!rc && logs) rc = d2h(e, lv, e->P.log_value, R * KP * Gp);
   const bool crcs = v->log_crc && e->cfg.payload_crc;
-  if (!rc && crcs) rc = d2h(e, lcrc, e->P.log_crc, R * K * Gp);
+  if (!rc && crcs) rc = d2h(e, lcrc, e->P.log_crc, R * KP * Gp);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(e->stream));
   for (uint64_t g = 0; g < G; ++g) {
@@ -503,8 +520,12 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
           }
           v->next[c * R + p] = nx;
         }
+      // physical slot of entry idx (raft_device.hpp ring_slot)
+      auto pslot = [&](int64_t idx) {
+        return uint64_t((idx - 1 + (idx >= sb[g] ? rot[g] : rota[g])) & int64_t(KP - 1));
+      };
       if (logs && last[d] > 0) {
-        const int32_t want = lt[ring_index(r, g, uint64_t((last[d] - 1 + rot[g]) & int64_t(K - 1)), K, R)];
+        const int32_t want = lt[ring_index(r, g, pslot(last[d]), KP, R)];
         if (ltm[d] != want)
           return fail(RAFT_EINVAL, "internal: last-entry term cache of group %llu replica %llu is %d, ring says %d",
                       (unsigned long long)g, (unsigned long long)r, ltm[d], want);
@@ -515,7 +536,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
           // slot s holds the largest index i <= l with (i-1) mod K == s
           int64_t idx = l >= 1 ? l - ((l - 1 - int64_t(s)) & int64_t(K - 1)) : 0;
           const bool live = idx >= 1 && idx <= l && idx > int64_t(hwm) - int64_t(K);
-          const uint64_t o = ring_index(r, g, (s + rot[g]) & (K - 1), K, R);   // physical slot
+          const uint64_t o = live ? ring_index(r, g, pslot(idx), KP, R) : 0;
           if (v->log_term) v->log_term[c * K + s] = live ? lt[o] : 0;
           if (v->log_value) v->log_value[c * K + s] = live ? lv[o] : 0;
           if (v->log_crc) v->log_crc[c * K + s] = (live && crcs) ? lcrc[o] : 0u;
@@ -533,13 +554,14 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
     return fail(RAFT_EINVAL, "raft_load_state needs every field of the view");
   HIPCHK(hipSetDevice(e->cfg.device));
   const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
+  const uint64_t KP = e->KP;
   std::vector<int32_t> term(R * Gp, 0), last(R * Gp, 0), commit(R * Gp, 0), ts(R * Gp, 0), lm(R * Gp, 0),
-      xm(R * R * Gp, 0), lt(R * K * Gp, 0), hb(Gp, HB_NONE);
+      xm(R * R * Gp, 0), lt(R * KP * Gp, 0), hb(Gp, HB_NONE);
   std::vector<uint16_t> rs(R * Gp, 0);
   std::vector<uint16_t> meta(Gp, uint16_t(NO_PRIMARY));
-  std::vector<int64_t> lv(R * K * Gp, 0);
+  std::vector<int64_t> lv(R * KP * Gp, 0);
   std::vector<int32_t> ltm(R * Gp, 0);
-  std::vector<uint32_t> lcrc(e->cfg.payload_crc ? R * K * Gp : 0, 0);
+  std::vector<uint32_t> lcrc(e->cfg.payload_crc ? R * KP * Gp : 0, 0);
   const bool raft = e->cfg.semantics == RAFT_SEM_RAFT;
   std::vector<int32_t> ln(raft ? R * Gp : 0, 0), xn(raft ? R * R * Gp : 0, 0), hw(raft ? R * Gp : 0, 0);
   const int max_vote = raft ? int(R) : 1;   // REF Voted bool; RAFT votedFor + 1
@@ -586,12 +608,22 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
                       (unsigned long long)g, (unsigned long long)r);
         hw[d] = h;
       }
+      // view slot s = (idx-1) mod K; loaded rings use rotation 0 (physical slot (idx-1) mod KP).
+      // With KP == K every slot is copied as is; with KP = 2K only the entries the view
+      // holds for indices <= LastApplied (the others can never be read).
+      const int64_t l = v->last[c];
       for (uint64_t s = 0; s < K; ++s) {
-        lt[ring_index(r, g, s, K, R)] = v->log_term[c * K + s];
-        lv[ring_index(r, g, s, K, R)] = v->log_value[c * K + s];
+        uint64_t ps = s;
+        if (KP != K) {
+          const int64_t idx = l >= 1 ? l - ((l - 1 - int64_t(s)) & int64_t(K - 1)) : 0;
+          if (idx < 1) continue;
+          ps = uint64_t(idx - 1) & (KP - 1);
+        }
+        const uint64_t o = ring_index(r, g, ps, KP, R);
+        lt[o] = v->log_term[c * K + s];
+        lv[o] = v->log_value[c * K + s];
         if (e->cfg.payload_crc)
-          lcrc[ring_index(r, g, s, K, R)] = v->log_crc ? v->log_crc[c * K + s]
-                                                  : host_entry_crc(v->log_term[c * K + s], v->log_value[c * K + s]);
+          lcrc[o] = v->log_crc ? v->log_crc[c * K + s] : host_entry_crc(v->log_term[c * K + s], v->log_value[c * K + s]);
       }
       if (v->last[c] > 0) ltm[d] = v->log_term[c * K + uint64_t((v->last[c] - 1) & int64_t(K - 1))];
     }
@@ -606,8 +638,11 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.lmatch, lm);
   if (!rc) rc = h2d(e, e->P.xmatch, xm);
   if (!rc) rc = h2d(e, e->P.gmeta, meta);
-  const std::vector<uint16_t> rot(Gp, 0);   // loaded rings: logical slot = physical slot
+  const std::vector<uint16_t> rot(Gp, 0);   // loaded rings: rotation 0, one segment
+  const std::vector<int32_t> sb0(Gp, 0);
   if (!rc) rc = h2d(e, e->P.grot, rot);
+  if (!rc) rc = h2d(e, e->P.grota, rot);
+  if (!rc) rc = h2d(e, e->P.gsb, sb0);
   if (!rc) rc = h2d(e, e->P.lterm, ltm);
   if (!rc && raft) rc = h2d(e, e->P.lnext, ln);
   if (!rc && raft) rc = h2d(e, e->P.xnext, xn);

@@ -297,8 +297,31 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
           w_term = Lt;
           w_ph = (Ll + rot) & int(P.kmask);
           w_vb = vb;
+          // out of the global phase (logs stood still while leaderless):
+          // switch the ring segment in place when that is safe (ring_slot)
+          const int ph = int(T.entries_before(T.tick) & P.kmask);
+          const uint32_t d = uint32_t(ph - w_ph) & P.kmask;
+          if (P.KP > P.K && d != 0u && d <= P.K && Ll > 0) {
+            int lo = Ll, hi = Ll;   // log lengths before this tick (== high-water marks on this path)
+#pragma unroll
+            for (int p = 0; p < R; ++p) {
+              const int pre = (p != c && ((okm >> p) & 1u)) ? last[p] - n : last[p];
+              lo = min(lo, pre);
+              hi = max(hi, pre);
+            }
+            const int sbo = at(P.gsb, g);
+            if (hi <= Ll && (sbo <= 1 || sbo <= lo - int(P.K) + 1)) {
+              at(P.grota, g) = uint16_t(rot);
+              at(P.gsb, g) = Ll + 1;
+              rot = (rot + int(d)) & int(P.kmask);
+              at(P.grot, g) = uint16_t(rot);
+              w_ph = ph;
+            }
+          }
         } else {   // rare: write here, each replica at its own LastApplied+1+e
-          const uint64_t tb = ring_tile(g, P.K, R);
+          const uint64_t tb = ring_tile(g, P.KP, R);
+          const uint32_t rota = at(P.grota, g);
+          const int sb = at(P.gsb, g);
           uint32_t cs = 0;
           if constexpr (CRC) cs = crc_term_state(tab, Lt);
           for (int e = 0; e < n; ++e) {
@@ -309,7 +332,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
             for (int p = 0; p < R; ++p) {
               if (p != c && !((okm >> p) & 1u)) continue;
               const int i0 = p == c ? Ll : last[p] - n;
-              const uint32_t o = ring_in_tile(g, R, uint32_t((i0 + e + rot) & int(P.kmask)), uint32_t(p));
+              const uint32_t o = ring_in_tile(g, R, ring_slot(i0 + e + 1, uint32_t(rot), rota, sb, P.kmask), uint32_t(p));
               st<WT>(P.log_term + tb, o, Lt);
               st<WT>(P.log_value + tb, o, v);
               if constexpr (CRC) st<WT>(P.log_crc + tb, o, stamp);
@@ -335,7 +358,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     if (wball) {
       const int lane = threadIdx.x & 63;
       // the tile base is wave-uniform (blocks are whole waves of consecutive groups)
-      const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g), P.K, R);
+      const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g), P.KP, R);
       int32_t* const rt = P.log_term + tb;
       int64_t* const rv = P.log_value + tb;
       uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;

@@ -23,6 +23,8 @@ __global__ __launch_bounds__(256) void init_new_kernel(DevPlanes P, Trace T) {
   P.hb[g] = HB_NONE;
   P.gmeta[g] = uint16_t(NO_PRIMARY);
   P.grot[g] = 0;   // empty logs: the phase is chosen at the first append
+  P.grota[g] = 0;
+  P.gsb[g] = 0;
 }
 
 // Post-election state (KAT-1 generalised).
@@ -55,6 +57,8 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
   P.hb[g] = HB_NONE;
   P.gmeta[g] = uint16_t(L | (P.hwm ? 0 : M_MSYNC) | M_STEADY);
   P.grot[g] = uint16_t(T.entries_before(T.tick + 1) & P.kmask);   // entry 1 lands in the global phase
+  P.grota[g] = 0;
+  P.gsb[g] = 0;
 }
 
 // State digest (raft_state_digest): one lane per group derives the canonical
@@ -104,11 +108,12 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
         }
         h = dg_mix(h, lo32(m) | (lo32(nx) << 32));
       }
-      const uint64_t rb = ring_tile(g, P.K, R);
-      const int rot = at(P.grot, g);
+      const uint64_t rb = ring_tile(g, P.KP, R);
+      const uint32_t rot = at(P.grot, g), rota = at(P.grota, g);
+      const int sb = at(P.gsb, g);
 #pragma unroll 1
       for (int idx = hwm > int(P.K) ? hwm - int(P.K) + 1 : 1; idx <= l; ++idx) {
-        const uint32_t o = ring_in_tile(g, R, uint32_t((idx - 1 + rot) & int(P.kmask)), uint32_t(r));
+        const uint32_t o = ring_in_tile(g, R, ring_slot(idx, rot, rota, sb, P.kmask), uint32_t(r));
         h = dg_mix(h, lo32(at(P.log_term + rb, o)) | (lo32(idx) << 32));
         h = dg_mix(h, uint64_t(at(P.log_value + rb, o)));
         h = dg_mix(h, P.crc_on ? uint64_t(at(P.log_crc + rb, o)) : 0ull);

@@ -42,9 +42,8 @@ constexpr int HB_NONE = -2147483647 - 1;
 constexpr int I32MAX = 2147483647;
 constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to cut atomic contention
 
-// Device layout. Per-replica scalar planes are [R][Gp]; the per-replica log
-// ring is [R][K][Gp] (slot-major, so a wave of groups in lock-step writes
-// one 256-B term segment and one 512-B value segment per entry).
+// Device layout. Per-replica scalar planes are [R][Gp]; the log rings are
+// wave tiles [Gp/64][KP][64][R] (see ring_tile below).
 struct DevPlanes {
   int32_t* term;       // Node.Term                 (main.go:19)
   int32_t* last;       // Node.LastApplied=len(Log) (main.go:25)
@@ -59,9 +58,11 @@ struct DevPlanes {
   int32_t* xnext;      // RAFT mode: [R][R][Gp] NextIndex rows of further leaders
   int32_t* hwm;        // RAFT mode: [R][Gp] highest LastApplied ever (== last in REF)
   uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
-  uint16_t* grot;      // ring rotation: entry idx of every replica sits at slot (idx-1+rot) mod K
+  uint16_t* grot;      // ring rotation of the current segment: entry idx >= gsb sits at slot (idx-1+grot) mod KP
+  uint16_t* grota;     // rotation of the previous segment (entries idx < gsb)
+  int32_t* gsb;        // first index of the current segment (0: one segment)
   int32_t* lterm;      // [R][Gp] Log[len-1].Term: cached term of each replica's last entry
-  int32_t* log_term;   // Log.Term  ring, [R] x tiles [Gp/64][K][64] (ring_slot_off)
+  int32_t* log_term;   // Log.Term  ring, tiles [Gp/64][KP][64][R] (ring_tile / ring_in_tile)
   int64_t* log_value;  // Log.Value ring
   uint32_t* log_crc;   // EXT: CRC32C stamp ring (payload_crc only)
   const uint32_t* crc_tab;  // 8 x 256 slice-by-8 CRC32C tables
@@ -70,20 +71,35 @@ struct DevPlanes {
   uint64_t Gp;         // plane pitch (groups, padded)
   uint64_t G;          // groups on this engine
   uint64_t gbase;      // global id of local group 0
-  uint32_t K;          // ring depth (power of two)
-  uint32_t kmask;
+  uint32_t K;          // ring depth (power of two): the last K entries of every log stay readable
+  uint32_t KP;         // physical ring slots per replica: K, or 2K when segment switches are on
+  uint32_t kmask;      // KP - 1 (physical slot mask)
 };
 
+// Ring phase segments. A group whose logs stop growing for L ticks (no
+// leader under churn) comes back out of phase with the global slot
+// entries_before(t) mod KP that every steady wave writes, and would write
+// partial ring lines from then on. With KP = 2K its rotation can instead be
+// switched without moving a single entry: entries idx >= gsb use the new
+// rotation, older ones the previous one (grota). Safe when the jump
+// d = new - old rotation is in [1, K] (the new segment's slots then only
+// reach an old slot once the entry there is more than K behind every log
+// that writes it), no log holds an entry at or above gsb yet, and the
+// previous segment holds no readable entry (the last K of any log).
+__device__ __forceinline__ uint32_t ring_slot(int idx, uint32_t rot, uint32_t rota, int sb, uint32_t kmask) {
+  return uint32_t(idx - 1 + int(idx >= sb ? rot : rota)) & kmask;
+}
+
 // Ring layout: the log rings of all R replicas are tiled by waves of 64
-// groups, [Gp/64][K][64][R] (replica innermost): entry slot s of replica r
+// groups, [Gp/64][KP][64][R] (replica innermost): entry slot s of replica r
 // of group g sits at element ((g/64)*K + s)*64*R + (g%64)*R + r.
 // * steady groups (logs in step, the same slot across a wave) write one
 //   contiguous 64*R*4-B term row / 64*R*8-B value row per wave and entry;
 // * groups whose log lengths drifted apart (churn) still write the R copies
 //   of an entry next to each other (R*4 + R*8 contiguous bytes per lane
-//   instead of 2R separate lines), and a wave stays inside one K*64*R tile.
+//   instead of 2R separate lines), and a wave stays inside one KP*64*R tile.
 // The tile base is 64-bit (wave-uniform in the fast kernel), the offset
-// inside a tile 32-bit (K*64*R <= 2^21).
+// inside a tile 32-bit (KP*64*R <= 2^22).
 __device__ __forceinline__ uint64_t ring_tile(uint32_t g, uint32_t K, uint32_t R) {
   return uint64_t(g >> 6) * (K * 64u * R);
 }
@@ -242,6 +258,8 @@ struct Group {
   LArr<R> pm, pn, ltm;
   uint32_t rows_m, rows_n;   // pm / pn hold the plane rows
   uint32_t rot, rot0;        // ring rotation (grot) now / as loaded
+  uint32_t rota, rota0;      // previous segment's rotation (grota) now / as loaded
+  int sb, sb0;               // segment boundary (gsb) now / as loaded
   uint32_t d_pm, d_pn, d_lt;
   uint32_t roles;       // 2 bits per replica
   uint32_t votes;       // 4 bits per replica: REF Voted (0/1), RAFT votedFor+1
@@ -305,6 +323,8 @@ struct Group {
     fault = (m >> 4) & 0xF;
     hbt = HB_NONE;
     rot = rot0 = at(P.grot, g);
+    rota = rota0 = at(P.grota, g);
+    sb = sb0 = at(P.gsb, g);
   }
   // Per-tick reset of a group whose state stays resident across ticks
   // (general kernel catch-up): clock, counters, this tick's entry cache.
@@ -379,8 +399,11 @@ struct Group {
 #pragma unroll
       for (int r = 0; r < R; ++r) empty &= last[r] == 0 && (SEM != SEM_RAFT || hw[r] == 0);
       uint32_t rt = rot;
-      if (empty && !fault) rt = next_phase & P.kmask;
+      int sbn = sb;
+      if (empty && !fault) { rt = next_phase & P.kmask; sbn = 0; }
       if (rt != rot0) at(P.grot, g) = uint16_t(rt);
+      if (sbn != sb0) at(P.gsb, g) = sbn;
+      if (rota != rota0) at(P.grota, g) = uint16_t(rota);
     }
     // The primary leader stepped down while another replica leads: move that
     // leader's rows into the coalesced primary planes so the group can take
@@ -408,7 +431,7 @@ struct Group {
 
   // Log ring of replica r: entry idx (1-based) at slot (idx-1) mod K.
   __device__ __forceinline__ uint32_t ring_off(const DevPlanes& P, int r, int idx) const {
-    return ring_in_tile(g, R, uint32_t((idx - 1 + int(rot)) & int(P.kmask)), uint32_t(r));
+    return ring_in_tile(g, R, ring_slot(idx, rot, rota, sb, P.kmask), uint32_t(r));
   }
   // Every log of the group is empty (RAFT: nothing above LastApplied either):
   // the ring holds no entry, so its rotation is free. Chosen so that the
@@ -419,15 +442,16 @@ struct Group {
     for (int r = 0; r < R; ++r)
       if (last[r] != 0 || (SEM == SEM_RAFT && hw[r] != 0)) return;
     rot = uint32_t(T.entries_before(T.tick)) & P.kmask;
+    sb = 0;
   }
   __device__ __forceinline__ int32_t& ring_term(const DevPlanes& P, int r, int idx) const {
-    return at(P.log_term + ring_tile(g, P.K, R), ring_off(P, r, idx));
+    return at(P.log_term + ring_tile(g, P.KP, R), ring_off(P, r, idx));
   }
   __device__ __forceinline__ int64_t& ring_value(const DevPlanes& P, int r, int idx) const {
-    return at(P.log_value + ring_tile(g, P.K, R), ring_off(P, r, idx));
+    return at(P.log_value + ring_tile(g, P.KP, R), ring_off(P, r, idx));
   }
   __device__ __forceinline__ uint32_t& ring_crc(const DevPlanes& P, int r, int idx) const {
-    return at(P.log_crc + ring_tile(g, P.K, R), ring_off(P, r, idx));
+    return at(P.log_crc + ring_tile(g, P.KP, R), ring_off(P, r, idx));
   }
   // EXT: is the AppendEntries delivered to replica p this tick corrupted?
   __device__ __forceinline__ int corrupted(const DevPlanes& P, int p) const {
@@ -1056,7 +1080,8 @@ struct TickSrc {
   const uint32_t* tab;
   uint32_t crc_on;
   uint32_t R;          // replicas (ring layout)
-  uint32_t g, K, kmask, rot;
+  uint32_t g, KP, kmask, rot, rota;
+  int sb;
   int leader, from;
   int cache_leader, cache_from, cache_term;
   uint64_t cache_vbase;
@@ -1068,8 +1093,8 @@ struct TickSrc {
       v = entry_value(cache_vbase, uint32_t(idx - cache_from));
       if (crc_on) c = crc_entry(tab, t, v);   // the leader's stamp of its own fresh entry
     } else {
-      const uint64_t tb = ring_tile(g, K, R);
-      const uint32_t o = ring_in_tile(g, R, uint32_t((idx - 1 + int(rot)) & int(kmask)), uint32_t(leader));
+      const uint64_t tb = ring_tile(g, KP, R);
+      const uint32_t o = ring_in_tile(g, R, ring_slot(idx, rot, rota, sb, kmask), uint32_t(leader));
       t = at(lt + tb, o);
       v = at(lv + tb, o);
       if (crc_on) c = at(lc + tb, o);
