@@ -373,6 +373,16 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* se = getenv("RAFTSTEP_SLOW_EVERY")) e->slow_every = std::max(1, atoi(se));
   if (const char* wt = getenv("RAFTSTEP_WRITE_THROUGH")) e->write_through = atoi(wt) != 0;
   if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
+  if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
+    if (rc == RAFT_OK) rc = dev_alloc(e, reinterpret_cast<void**>(&e->P.dbg), 16 * 8);
+    if (rc == RAFT_OK && hipMemset(e->P.dbg, 0, 16 * 8) != hipSuccess) rc = fail(RAFT_EHIP, "hipMemset failed");
+    if (rc != RAFT_OK) {
+      std::string keep = g_err;
+      raft_engine_destroy(e);
+      g_err = keep;
+      return rc;
+    }
+  }
   // zero everything once so that padding / unused rows are deterministic
   for (void* p : e->allocs) (void)p;
   hipError_t z = hipSuccess;
@@ -704,6 +714,17 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (e->prof == 2) {
     HIPCHK(hipEventRecord(rb, e->stream));
     e->prof_n += nticks;
+  }
+  if (e->P.dbg) {   // diagnostics: fast-kernel lane classes summed over this call's ticks (synchronising)
+    unsigned long long d[16];
+    HIPCHK(hipMemcpyAsync(d, e->P.dbg, sizeof d, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemsetAsync(e->P.dbg, 0, sizeof d, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    fprintf(stderr,
+            "raftstep: ticks %lld..%lld lanes %llu skip %llu bail %llu iso %llu drift<=K %llu drift>K %llu switch %llu "
+            "blk_hi %llu blk_seg %llu coop %llu drifted %llu\n",
+            (long long)first_tick, (long long)(first_tick + nticks - 1), d[10], d[0], d[1], d[2], d[3], d[4], d[5], d[6],
+            d[7], d[8], d[9]);
   }
   if (stats && e->comm)
     RCCLCHK(ncclAllReduce(e->hist, e->hist, size_t(nticks) * STAT_SLOTS * NSTAT, ncclUint64, ncclSum, e->comm,

@@ -79,6 +79,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
   uint32_t wr = 0;      // replicas that append this tick's entries (leader + accepting followers)
   int w_term = 0, w_ph = 0;    // their term and the ring slot of the first entry
   uint64_t w_vb = 0;    // value stream base of this tick's entries
+  uint32_t df = 0;      // diagnostics: lane class bits (P.dbg)
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
     const int c = meta & 0xF;
@@ -88,6 +89,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     int term[R], last[R], commit[R], lt[R], m[R];
     bool empty = true;   // every log of the group empty before this tick
     const bool go = !skip && !bail;
+    df |= skip ? 1u : 0u;
     if (go) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -126,6 +128,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       const uint32_t im = isolation_mask<R>(key, T);
       if (RAFT && R >= 3 && im && (im & (im - 1u)) == 0u && int(__builtin_ctz(im)) != c) xi = int(__builtin_ctz(im));
       else bail |= im != 0u;
+      if (im) df |= 4u;
     }
     if (go && !xi_ok<RAFT>(meta, xi)) bail = true;   // ONECAND needs its candidate isolated (role checked below)
     // leader view
@@ -301,6 +304,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
           // switch the ring segment in place when that is safe (ring_slot)
           const int ph = int(T.entries_before(T.tick) & P.kmask);
           const uint32_t d = uint32_t(ph - w_ph) & P.kmask;
+          if (d != 0u) df |= d <= P.K ? 8u : 16u;
           if (P.KP > P.K && d != 0u && d <= P.K && Ll > 0) {
             int lo = Ll, hi = Ll;   // log lengths before this tick (== high-water marks on this path)
 #pragma unroll
@@ -310,7 +314,10 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
               hi = max(hi, pre);
             }
             const int sbo = at(P.gsb, g);
+            df |= hi > Ll ? 64u : 0u;
+            df |= (sbo <= 1 || sbo <= lo - int(P.K) + 1) ? 0u : 128u;
             if (hi <= Ll && (sbo <= 1 || sbo <= lo - int(P.K) + 1)) {
+              df |= 32u;
               at(P.grota, g) = uint16_t(rot);
               at(P.gsb, g) = Ll + 1;
               rot = (rot + int(d)) & int(P.kmask);
@@ -367,6 +374,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       const int na = __popcll(__ballot(wr != 0 && w_ph == sa)), nb = __popcll(__ballot(wr != 0 && w_ph == sb));
       const int s0 = nb >= na ? sb : sa;
       const bool coop = wr != 0 && w_ph == s0;
+      df |= coop ? 256u : (wr != 0 ? 512u : 0u);
       uint32_t cs = 0;
       if constexpr (CRC) cs = crc_term_state(tab, w_term);
       {
@@ -418,6 +426,15 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
           }
         }
       }
+    }
+  }
+  if (P.dbg) {   // diagnostics: lanes per class, one atomic per wave and class
+    df |= bail ? 2u : 0u;
+    df |= (g < P.G) ? 1024u : 0u;
+#pragma unroll 1
+    for (int k = 0; k < 11; ++k) {
+      const uint64_t b = __ballot((df >> k) & 1u);
+      if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
     }
   }
   // groups that need the general path go to the dense worklist: block-local

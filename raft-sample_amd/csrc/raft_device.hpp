@@ -74,6 +74,7 @@ struct DevPlanes {
   uint32_t K;          // ring depth (power of two): the last K entries of every log stay readable
   uint32_t KP;         // physical ring slots per replica: K, or 2K when segment switches are on
   uint32_t kmask;      // KP - 1 (physical slot mask)
+  unsigned long long* dbg;  // diagnostics (RAFTSTEP_DEBUG_FAST): fast-kernel lane class counters, else null
 };
 
 // Ring phase segments. A group whose logs stop growing for L ticks (no
