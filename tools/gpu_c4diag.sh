@@ -1,11 +1,14 @@
 #!/bin/bash
-# C4 diagnostics: general-kernel worklist size per launch and fast-kernel lane
-# classes (both synchronising, so not a timing run), then a plain C4 bench line.
+# Parity suite, then C4 diagnostics: general-kernel worklist size per launch
+# and fast-kernel lane classes with deferral reasons (both synchronising, so
+# not timing runs), then plain C2 and C4 bench lines.
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
-RAFTSTEP_DEBUG_WORK=1 timeout -k 10 200 python3 -u bench.py --workload C4 --steps 64 --warmup 16 --no-cpu-baseline > $OUT/c4_work.log 2>&1 \
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 \
+&& RAFTSTEP_DEBUG_WORK=1 timeout -k 10 200 python3 -u bench.py --workload C4 --steps 64 --warmup 16 --no-cpu-baseline > $OUT/c4_work.log 2>&1 \
 && RAFTSTEP_DEBUG_FAST=1 timeout -k 10 200 python3 -u bench.py --workload C4 --steps 64 --warmup 16 --no-cpu-baseline > $OUT/c4_fast.log 2>&1 \
+&& timeout -k 10 200 python3 -u bench.py --steps 200 --warmup 20 --no-cpu-baseline > $OUT/c2_bench.log 2>&1 \
 && timeout -k 10 200 python3 -u bench.py --workload C4 --steps 100 --warmup 16 --no-cpu-baseline > $OUT/c4_bench.log 2>&1
