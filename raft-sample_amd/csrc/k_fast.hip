@@ -80,6 +80,13 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
   int w_term = 0, w_ph = 0;    // their term and the ring slot of the first entry
   uint64_t w_vb = 0;    // value stream base of this tick's entries
   uint32_t df = 0;      // diagnostics: lane class bits (P.dbg)
+  // deferral-reason bits 11-15 only in a diagnostics build (make DIAG=1),
+  // so the product kernel carries no extra instructions for them
+#ifdef RAFTSTEP_DIAG_REASONS
+#define DIAG_REASON(x) x
+#else
+#define DIAG_REASON(x)
+#endif
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
     const int c = meta & 0xF;
@@ -90,7 +97,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     bool empty = true;   // every log of the group empty before this tick
     const bool go = !skip && !bail;
     df |= skip ? 1u : 0u;
-    df |= bail ? 2048u : 0u;   // diagnostics: deferral reason "group not steady"
+    DIAG_REASON(df |= bail ? 2048u : 0u;);   // diagnostics: deferral reason "group not steady"
     if (go) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -117,7 +124,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         }
       }
     }
-    if (bail && !(df & 2048u)) df |= 16384u;   // reason: explicit RAFT rows out of step
+    DIAG_REASON(if (bail && !(df & 2048u)) df |= 16384u;);   // reason: explicit RAFT rows out of step
     uint64_t key = 0;
     if (go && (T.iso_p || n)) key = group_key(T.seed, P.gbase + g);
     // RAFT: one isolated replica xi (not the leader) is handled here: it
@@ -132,7 +139,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       else bail |= im != 0u;
       if (im) df |= 4u;
     }
-    if (bail && !(df & (2048u | 16384u))) df |= 4096u;   // reason: leader or >1 replica isolated
+    DIAG_REASON(if (bail && !(df & (2048u | 16384u))) df |= 4096u;);   // reason: leader or >1 replica isolated
     if (go && !xi_ok<RAFT>(meta, xi)) bail = true;   // ONECAND needs its candidate isolated (role checked below)
     // leader view
     const int Lt = sel(term, c), Ll = sel(last, c), Lc = sel(commit, c), Llt = sel(lt, c);
@@ -146,7 +153,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         if constexpr (RAFT) bail |= (p != c) && (last[p] != Ll || term[p] != Lt);
       }
     }
-    if (bail && !(df & (2048u | 4096u | 16384u))) df |= 8192u;   // reason: a follower's log or term not in step
+    DIAG_REASON(if (bail && !(df & (2048u | 4096u | 16384u))) df |= 8192u;);   // reason: a follower's log or term not in step
     // the isolated replica's own state: role, vote, timer (eff. start = max(tstart, hb))
     int x_rs = 0, x_term = 0, x_fire = 0, x_dur = 0;
     if constexpr (RAFT) {
@@ -435,8 +442,8 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
   if (P.dbg) {   // diagnostics: lanes per class, one atomic per wave and class
     df |= bail ? 2u : 0u;
     df |= (g < P.G) ? 1024u : 0u;
-    if (bail && !(df & (2048u | 4096u | 8192u | 16384u))) df |= 32768u;   // reason: anything later
-    if (!bail) df &= ~(2048u | 4096u | 8192u | 16384u);
+    DIAG_REASON(if (bail && !(df & (2048u | 4096u | 8192u | 16384u))) df |= 32768u;);   // reason: anything later
+    DIAG_REASON(if (!bail) df &= ~(2048u | 4096u | 8192u | 16384u););
 #pragma unroll 1
     for (int k = 0; k < 16; ++k) {
       const uint64_t b = __ballot((df >> k) & 1u);
