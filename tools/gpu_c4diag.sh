@@ -1,7 +1,10 @@
 #!/bin/bash
 # Parity suite, then C4 diagnostics: general-kernel worklist size per launch
 # and fast-kernel lane classes with deferral reasons (both synchronising, so
-# not timing runs), then plain C2 and C4 bench lines.
+# not timing runs), then plain C2 and C4 bench lines. The reason counters are
+# compiled only into a diagnostics build: on the CPU side first run
+#   touch raft-sample_amd/csrc/k_fast.hip && make -C raft-sample_amd/csrc DIAG=1
+# (and rebuild without DIAG=1 afterwards); a product build prints zeros there.
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
