@@ -8,17 +8,27 @@ launch per tick, state read from and written back to HBM every tick.
 
 Workload at N=1: SURVEY config C2 — 2^20 independent 5-replica groups,
 steady-state AppendEntries + commitIndex, one client entry per tick, seeded
-synthetic trace. For N>1 each rank owns 2^20 groups (weak scaling; groups
-shard by id, no data-path collective); the per-tick statistics are summed
-across GPUs with RCCL inside the engine.
+synthetic trace. For N>1 the default is SURVEY config C3: each rank owns
+2^21 groups (16M over 8 GPUs; weak scaling; groups shard by id, no
+data-path collective); the per-tick statistics are reduced on the device and
+summed across GPUs with RCCL on a side stream inside the engine.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Protocol: W untimed warm-up ticks, then the timed region of
+exactly K ticks (barrier + synchronize on both sides, max over ranks) is
+repeated --repeats times (default 5) and the median is reported. The
+roofline's `achieved` uses the steady-state kernel's own average duration,
+measured by HIP events attached to each of its dispatches (profile mode 1)
+in a separate, untimed pass of K ticks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2|C3|C4|C4REF|C5]
 """
 import argparse
 import json
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "raft-sample_amd"))
@@ -36,18 +46,25 @@ def algorithmic_bytes(R, E, crc=False):
 
 # SURVEY.md §8(d) workloads runnable by this bench (per GPU)
 WORKLOADS = {
-    "C2": dict(groups=1 << 20, entries=1, ring_depth=32, crc=0,
+    "C2": dict(groups=1 << 20, entries=1, ring_depth=32, crc=0, seed=0x5EED0002,
                desc="steady-state AppendEntries+commit"),
-    "C3": dict(groups=1 << 21, entries=1, ring_depth=32, crc=0,
+    "C3": dict(groups=1 << 21, entries=1, ring_depth=32, crc=0, seed=0x5EED0003,
                desc="steady-state AppendEntries+commit, 2^21 groups per GPU (16M over 8 GPUs)"),
-    "C5": dict(groups=1 << 20, entries=64, ring_depth=128, crc=1,
+    "C5": dict(groups=1 << 20, entries=64, ring_depth=128, crc=1, seed=0x5EED0005,
                desc="64-entry AppendEntries batches with per-entry CRC32C stamp+verify"),
-    # C4: NewNode start, seeded isolation churn (one replica of a group cut
-    # off for 8-32 ticks w.p. 1/8 per 32-tick epoch ~ 1/256 per tick), RAFT
-    # semantics (REF faults on a new leader's first contact, SURVEY KAT-11)
+    # C4: NewNode start, seeded isolation churn: per 32-tick epoch w.p. 1/8
+    # (~1/256 per tick) one replica of a group is cut off for 8-32 ticks;
+    # RAFT semantics (REF faults on a new leader's first contact, SURVEY KAT-11)
     "C4": dict(groups=1 << 22, replicas=7, entries=1, ring_depth=128, crc=0, init="new", semantics=1, settle=48,
-               iso=(8192, 8, 32),
+               iso=(8192, 8, 32), seed=0x5EED0004,
                desc="NewNode start, isolation churn (elections, term bumps, truncation), RAFT semantics"),
+    # C4REF: the same trace in REF semantics (main.go bit for bit): the first
+    # contact of a new leader panics (GetLog, main.go:142 -> 404) and the
+    # group freezes, so this line reports throughput over the prefix and the
+    # fault counts (SURVEY §8(d) "REF parity on prefix + fault codes")
+    "C4REF": dict(groups=1 << 22, replicas=7, entries=1, ring_depth=128, crc=0, init="new", semantics=0, settle=48,
+                  iso=(8192, 8, 32), seed=0x5EED0004, allow_faults=True,
+                  desc="NewNode start, isolation churn, REF semantics (prefix; groups freeze on their first fault)"),
 }
 
 
@@ -76,30 +93,42 @@ def cpu_baseline(args, wl, R, E, K, crc):
     dt = time.perf_counter() - t0
     o.close()
     return {"value": G * T / dt, "unit": "group-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{G} groups x {T} ticks, R={R}, E={E}, crc={crc}, {start}, "
+            "sample": f"G scaled down to {G} groups (GPU line: {wl['groups']}) x {T} ticks, R={R}, E={E}, "
+                      f"crc={crc}, {start}; oracle/raft_oracle.c (C restatement of main.go's handlers), "
                       f"{threads} pthreads over contiguous group ranges ({dt:.2f} s)"}
 
 
 def engine_kwargs(wl, R, G, base, K, E, crc):
     kw = dict(replicas=R, groups=G, group_base=base, ring_depth=K, entries_per_tick=E, client_period=1,
-              payload_crc=crc, seed=wl.get("seed", 0x5EED0002), semantics=wl.get("semantics", 0))
+              payload_crc=crc, seed=wl["seed"], semantics=wl.get("semantics", 0))
     if "iso" in wl:
         kw.update(isolate_per_65536=wl["iso"][0], isolate_min_ticks=wl["iso"][1], isolate_max_ticks=wl["iso"][2])
     return kw
 
 
-def load_pmc(wl_key, workload):
+def load_pmc(workload):
     """HBM traffic per launch of the steady-state kernel from the committed
-    rocprofv3 --pmc summary of this workload (profiles/pmc_<key>.json, made
-    by tools/pmc_summary.py from FETCH_SIZE / WRITE_SIZE passes), or None."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{wl_key}.json")
-    try:
-        d = json.load(open(p))
-    except (OSError, ValueError):
-        return None
-    if d.get("workload") != workload:
-        return None
-    return d.get("hbm_bytes_per_launch")
+    rocprofv3 --pmc summary of exactly this workload (profiles/pmc_*.json,
+    made by tools/pmc_summary.py from FETCH_SIZE / WRITE_SIZE passes), and
+    where it came from; (None, None) if no pass covers it."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            src = f"{os.path.relpath(p, ROOT)} (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of this workload, " \
+                  f"calibrated by tools/pmc_calib; not measured in this run" + \
+                  (f"; build {d['commit']}" if d.get("commit") else "") + ")"
+            return d["hbm_bytes_per_launch"], src
+    return None, None
+
+
+def median(xs):
+    xs = sorted(xs)
+    n = len(xs)
+    return xs[n // 2] if n % 2 else 0.5 * (xs[n // 2 - 1] + xs[n // 2])
 
 
 def main():
@@ -107,7 +136,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--repeats", type=int, default=5, help="timed regions of --steps ticks; the median is reported")
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: C2 at --gpus 1, C3 (2^21 groups per GPU) at --gpus > 1")
     ap.add_argument("--groups-per-gpu", type=int, default=None)
     ap.add_argument("--replicas", type=int, default=None)
     ap.add_argument("--entries", type=int, default=None)
@@ -123,6 +154,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    wl_key = args.workload or ("C2" if world == 1 else "C3")
 
     import torch
     dist = None
@@ -141,14 +173,15 @@ def main():
 
     from raftstep import Engine, STAT_NAMES
 
-    wl = WORKLOADS[args.workload]
+    wl = WORKLOADS[wl_key]
     R = args.replicas or wl.get("replicas", R_DEFAULT)
     G = args.groups_per_gpu or wl["groups"]
     E = args.entries or wl["entries"]
     K = args.ring_depth or wl["ring_depth"]
     crc = wl["crc"]
     churn = wl.get("init") == "new"
-    eng = Engine(device=local, **engine_kwargs(wl, R, G, rank * G, K, E, crc))
+    base = rank * G
+    eng = Engine(device=local, **engine_kwargs(wl, R, G, base, K, E, crc))
     if dist is not None and not same_dev:
         from raftstep import dist as rdist
         eng.comm_init(world, rank, rdist.exchange_comm_id(dist, rank, Engine.comm_unique_id))
@@ -169,37 +202,61 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    eng.profile(2)   # one HIP event pair on the engine stream around the timed ticks
-    barrier()
-    t0 = time.perf_counter()
-    stats = eng.tick(tick, args.steps, stats=True)   # K fused tick launches + per-tick stats (+RCCL sum)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms, launches = eng.profile_read()
+    # timed regions: exactly K fused ticks each (+ the per-tick stats, reduced
+    # on the device and, at N>1, all-reduced by RCCL on the engine's side stream)
+    times, stats = [], np.zeros(len(STAT_NAMES), np.int64)
+    eng.profile(2)   # one HIP event pair on the engine stream around each timed call
+    for _ in range(max(1, args.repeats)):
+        barrier()
+        t0 = time.perf_counter()
+        s = eng.tick(tick, args.steps, stats=True)
+        barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            from raftstep import dist as rdist
+            el = rdist.max_over_ranks(dist, el, device=None if same_dev else "cuda")
+            if same_dev:   # no engine communicator: sum the stats through torch.distributed
+                s = np.array(rdist.sum_over_ranks(dist, s), np.int64)
+        times.append(el)
+        stats += s
+        tick += args.steps
+    region_ms, region_launches = eng.profile_read()
+    # untimed pass: the steady-state kernel's own duration, events attached to each dispatch
+    eng.profile(1)
+    eng.tick(tick, args.steps, stats=False)
+    kernel_ms, kernel_launches = eng.profile_read()
     eng.profile(0)
-    if dist is not None:
-        from raftstep import dist as rdist
-        elapsed = rdist.max_over_ranks(dist, elapsed, device=None if same_dev else "cuda")
-        if same_dev:   # no engine communicator: sum the stats through torch.distributed
-            stats = rdist.sum_over_ranks(dist, stats)
+    nranks, _, allreduces = eng.comm_info()
 
+    elapsed = median(times)
+    reps = len(times)
     total_steps = G * world * args.steps
     value = total_steps / elapsed
-    # correctness guard on the timed run: the steady state commits exactly one
+    # correctness guard on the timed runs: the steady state commits exactly one
     # entry per group per tick and never faults; under churn nothing faults
-    # and most groups have a leader
-    expect_commit = G * world * args.steps * E
-    faults = stats[STAT_NAMES.index("faults")]
+    # and most groups have a leader (REF prefix: faults are the point)
+    expect_commit = G * world * args.steps * E * reps
+    faults = int(stats[STAT_NAMES.index("faults")])
     if churn:
-        ok = faults == 0 and stats[STAT_NAMES.index("leader_groups")] > 0.5 * G * world * args.steps
+        ok = (wl.get("allow_faults") or faults == 0) and \
+            (wl.get("allow_faults") or stats[STAT_NAMES.index("leader_groups")] > 0.5 * G * world * args.steps * reps)
     else:
         ok = stats[STAT_NAMES.index("committed")] == expect_commit and faults == 0
 
     B = algorithmic_bytes(R, E, crc)
-    avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)   # region events / launches: tick kernel + gaps
+    avg_kernel_s = kernel_ms / 1e3 / max(kernel_launches, 1)    # steady-state kernel, kernel-exact
+    avg_region_s = region_ms / 1e3 / max(region_launches, 1)    # all launches of a tick + gaps
     achieved = B * G / avg_kernel_s / 1e9
-    workload = f"{args.workload}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}"
-    traffic = load_pmc(args.workload, workload)
+    workload = f"{wl_key}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}"
+    traffic, traffic_src = load_pmc(workload)
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "frac_measured": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
+            "traffic_source": traffic_src,
+            "bytes_per_group_step": B, "units_per_launch": G,
+            "kernel": "tick_fast_kernel", "avg_kernel_us": avg_kernel_s * 1e6, "kernel_launches": kernel_launches,
+            "avg_region_us_per_tick": avg_region_s * 1e6,
+            "achieved_region": B * G / avg_region_s / 1e9}
     result = {
         "metric": "Raft group-steps/sec at 1M 5-replica groups, 1-8 GPUs; % of HBM peak",
         "value": value,
@@ -213,17 +270,25 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (seeded splitmix64 trace; %s, SURVEY.md §8(d) %s)"
-                % ("NewNode start + isolation churn" if churn else "post-election steady state", args.workload),
+                % ("NewNode start + isolation churn" if churn else "post-election steady state", wl_key),
         "config": {"workload": workload, "groups_per_gpu": G, "groups_total": G * world, "replicas": R,
                    "entries_per_tick": E, "ring_depth": K, "payload_crc32c": bool(crc), "leader": args.leader,
+                   "seed": hex(wl["seed"]),
                    "semantics": "RAFT (EXT, Raft paper)" if wl.get("semantics") else "REF (main.go)",
                    "parallelism": f"group-sharded x{world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "bytes_per_group_step": B, "avg_kernel_us": avg_kernel_s * 1e6, "launches": launches},
+        "timing": {"repeats": reps, "median_s": elapsed, "repeat_ms_per_step": [t * 1e3 / args.steps for t in times]},
+        "roofline": roof,
         "stats": dict(zip(STAT_NAMES, [int(x) for x in stats])),
         "stats_check": bool(ok),
     }
+    if world > 1:
+        from raftstep import dist as rdist
+        ranks = [None] * world
+        dist.all_gather_object(ranks, {"rank": rank, "group_base": base, "groups": G, "rccl_nranks": nranks,
+                                       "stat_allreduces": allreduces})
+        result["multi_gpu"] = {"rccl_nranks": nranks if not same_dev else None,
+                               "engine_communicator": not same_dev,
+                               "per_rank": ranks}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, wl, R, E, K, crc)
     elif rank == 0:
@@ -235,7 +300,7 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     if not ok:
-        raise SystemExit("bench: steady-state statistics check failed")
+        raise SystemExit("bench: statistics check failed")
 
 
 if __name__ == "__main__":

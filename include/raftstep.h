@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RAFT_ABI_VERSION 3u
+#define RAFT_ABI_VERSION 4u
 #define RAFT_MAX_REPLICAS 8u
 
 /* Node.State (main.go:51-57). */
@@ -103,7 +103,9 @@ typedef struct raft_config {
   int32_t device;              /* HIP device ordinal */
   uint32_t payload_crc;        /* EXT (config C5): stamp every entry with CRC32C(term||value), followers verify */
   uint32_t corrupt_per_65536;  /* EXT: probability that an AppendEntries' last entry arrives with a flipped bit */
-  uint32_t reserved[6];
+  uint32_t isolate_leader;     /* EXT: 1 = an isolation window cuts off the group's leader at the window's first
+                                  tick (the lowest-id Leader then; no leader: nobody), 0 = a hashed replica */
+  uint32_t reserved[5];
 } raft_config;
 
 /* Canonical host view of engine state, group-major:
@@ -184,6 +186,10 @@ int raft_checkpoint_load(raft_engine* e, const char* path);
  *      at once by the new candidate's vote round (main.go:171-177, 248-251).
  * `out` (may be NULL) receives the stats summed over the ticks. */
 int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_stats* out);
+/* Per-tick statistics of the last raft_tick call that asked for stats: record
+ * t (0 <= t < nticks of that call) holds tick first_tick+t, summed over groups
+ * and, with a communicator, over GPUs (the 64-B record the all-reduce carries). */
+int raft_tick_records(raft_engine* e, uint32_t nticks, raft_tick_stats* per_tick);
 int raft_sync(raft_engine* e);
 
 /* ---- message-level handlers (drop-in for the select cases) --------------
@@ -259,11 +265,19 @@ int raft_group_ops_batch(raft_engine* e, int64_t now_tick, const raft_group_op* 
 
 /* ---- multi-GPU statistics (RCCL over xGMI) -------------------------------
  * Groups shard by id (config.group_base); the only collective is the sum of
- * tick statistics. Rank 0 creates the id and distributes it out of band. */
+ * tick statistics: after each general-kernel window raft_tick reduces the
+ * window's per-tick records on the device (NSTAT int64 = 64 B per tick) and
+ * all-reduces them on a second HIP stream, ordered by an event, so the sum
+ * overlaps the following ticks. Rank 0 creates the id and distributes it out
+ * of band. */
 int raft_comm_unique_id(uint8_t id_out[128]);
 int raft_comm_init(raft_engine* e, int nranks, int rank, const uint8_t id[128]);
 /* All-reduce `stats` (in/out) over the communicator (sum); no-op without one. */
 int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats);
+/* Ranks of the attached communicator as RCCL reports them (ncclCommCount /
+ * ncclCommUserRank; 1 / 0 without one) and the number of per-window stats
+ * all-reduces raft_tick has issued on the engine's comm stream so far. */
+int raft_comm_info(raft_engine* e, int32_t* nranks, int32_t* rank, uint64_t* allreduces);
 
 /* ---- instrumentation -----------------------------------------------------
  * mode 1: every steady-state tick kernel is timed by events attached to its

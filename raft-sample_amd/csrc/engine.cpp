@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/raftstep.h"
@@ -92,9 +93,14 @@ struct raft_engine {
   DevPlanes P{};
   std::vector<void*> allocs;
   uint64_t device_bytes = 0;
-  // per-tick statistics: [cap][STAT_SLOTS][NSTAT] u64
+  // per-tick statistics: atomic targets [cap][STAT_SLOTS][NSTAT] u64 (kept
+  // zero between calls by the reduce kernel) and the reduced per-tick records
+  // [cap][NSTAT] (the 64 B per tick that RCCL sums across GPUs)
   unsigned long long* hist = nullptr;
+  unsigned long long* tstat = nullptr;
   uint32_t hist_cap = 0;
+  unsigned long long* cstat = nullptr;   // raft_comm_allreduce_stats staging
+  uint32_t wpar = 0;            // parity of the next worklist window (its counter was zeroed by the last general kernel)
   // worklist of groups the steady-state kernel hands to the general kernel
   uint32_t* work = nullptr;     // deferred group ids
   int32_t* work_tick = nullptr; // tick each one was deferred at
@@ -113,9 +119,13 @@ struct raft_engine {
   size_t ev_used = 0;
   double prof_ms = 0.0;
   uint64_t prof_n = 0;
-  // RCCL
+  // RCCL: the per-tick stats all-reduce runs on its own stream, ordered after
+  // each window's reduce kernel by an event, so it overlaps the next ticks
   ncclComm_t comm = nullptr;
+  hipStream_t comm_stream = nullptr;
+  std::vector<hipEvent_t> comm_ev;
   int nranks = 1, rank = 0;
+  uint64_t allreduces = 0;      // ncclAllReduce calls issued (diagnostics)
 };
 
 namespace {
@@ -171,13 +181,17 @@ int ensure_stage(raft_engine* e, size_t bytes) {
 
 int ensure_hist(raft_engine* e, uint32_t n) {
   if (n <= e->hist_cap) return RAFT_OK;
-  if (e->hist) {
-    HIPCHK(hipStreamSynchronize(e->stream));
-    HIPCHK(hipFree(e->hist));
-    e->hist = nullptr;
-  }
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (e->comm_stream) HIPCHK(hipStreamSynchronize(e->comm_stream));
+  if (e->hist) HIPCHK(hipFree(e->hist));
+  if (e->tstat) HIPCHK(hipFree(e->tstat));
+  e->hist = e->tstat = nullptr;
+  e->hist_cap = 0;
   uint32_t cap = std::max<uint32_t>(n, 64);
-  HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->hist), size_t(cap) * STAT_SLOTS * NSTAT * 8));
+  const size_t hb = size_t(cap) * STAT_SLOTS * NSTAT * 8;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->hist), hb));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->tstat), size_t(cap) * NSTAT * 8));
+  HIPCHK(hipMemsetAsync(e->hist, 0, hb, e->stream));   // once; the reduce kernel re-zeroes what it reads
   e->hist_cap = cap;
   return RAFT_OK;
 }
@@ -294,14 +308,16 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (c.isolate_per_65536 > 65536) return fail(RAFT_EINVAL, "isolate_per_65536 must be <= 65536");
   if (c.payload_crc > 1) return fail(RAFT_EINVAL, "payload_crc must be 0 or 1");
   if (c.corrupt_per_65536 > 65536) return fail(RAFT_EINVAL, "corrupt_per_65536 must be <= 65536");
+  if (c.isolate_leader != 0) return fail(RAFT_EINVAL, "isolate_leader is not supported by this build");
   if (c.isolate_per_65536 &&
       (c.isolate_min_ticks < 1 || c.isolate_max_ticks > 32 || c.isolate_min_ticks > c.isolate_max_ticks))
     return fail(RAFT_EINVAL, "isolation length must satisfy 1 <= min <= max <= 32");
   const uint64_t Gp = (c.groups + 255) & ~uint64_t(255);
-  // device addressing: 64-bit plane/tile bases, 32-bit lane offsets (group
-  // index < 2^32 within a plane, K*64*R entries within a ring tile)
-  if (c.groups >= (uint64_t(1) << 31))
-    return fail(RAFT_EINVAL, "too many groups for one engine (need groups < 2^31)");
+  // device addressing (raft_device.hpp at()): 64-bit plane/tile bases, 32-bit
+  // per-lane BYTE offsets, so the widest per-group plane (4-B elements) must
+  // satisfy Gp*4 < 2^32, i.e. Gp <= 2^30 - 256 (ring tiles: KP*64*R*8 < 2^26)
+  if (Gp * 4 > uint64_t(0xFFFFFFFFu))
+    return fail(RAFT_EINVAL, "too many groups for one engine (need groups <= 2^30 - 256)");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RAFT_ENODEV, "no HIP device");
   if (c.device < 0 || c.device >= ndev) return fail(RAFT_ENODEV, "device %d out of range", c.device);
@@ -423,10 +439,15 @@ int raft_engine_destroy(raft_engine* e) {
   if (!e) return RAFT_OK;
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
   if (e->comm) (void)ncclCommDestroy(e->comm);
   for (hipEvent_t x : e->ev) (void)hipEventDestroy(x);
+  for (hipEvent_t x : e->comm_ev) (void)hipEventDestroy(x);
+  if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->hist) (void)hipFree(e->hist);
+  if (e->tstat) (void)hipFree(e->tstat);
+  if (e->cstat) (void)hipFree(e->cstat);
   if (e->stage) (void)hipFree(e->stage);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -665,16 +686,33 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   return RAFT_OK;
 }
 
+// Stats of the window [w0, w1] (indices into this call's ticks) are final
+// once its general kernel has run: reduce them to per-tick records and, with
+// a communicator, sum those across GPUs on the comm stream (ordered by an
+// event, overlapping the following ticks on the engine stream).
+static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1) {
+  const uint32_t n = w1 - w0 + 1;
+  HIPCHK(launch_stats_reduce(e->hist + size_t(w0) * STAT_SLOTS * NSTAT, e->tstat + size_t(w0) * NSTAT, n, e->stream));
+  if (!e->comm) return RAFT_OK;
+  if (e->comm_ev.empty()) {
+    hipEvent_t x;
+    HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+    e->comm_ev.push_back(x);
+  }
+  HIPCHK(hipEventRecord(e->comm_ev[0], e->stream));
+  HIPCHK(hipStreamWaitEvent(e->comm_stream, e->comm_ev[0], 0));
+  RCCLCHK(ncclAllReduce(e->tstat + size_t(w0) * NSTAT, e->tstat + size_t(w0) * NSTAT, size_t(n) * NSTAT, ncclUint64,
+                        ncclSum, e->comm, e->comm_stream));
+  ++e->allreduces;
+  return RAFT_OK;
+}
+
 static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool stats) {
   if (int rc = check_ticks(e, first_tick, nticks)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
-  if (stats) {
+  if (stats)
     if (int rc = ensure_hist(e, nticks)) return rc;
-    HIPCHK(hipMemsetAsync(e->hist, 0, size_t(nticks) * STAT_SLOTS * NSTAT * 8, e->stream));
-  }
-  HIPCHK(hipMemsetAsync(e->wcount, 0, 2 * sizeof(uint32_t), e->stream));
   const Trace T0 = make_trace(e, first_tick);
-  uint32_t window = 0;
   int64_t win_first = first_tick;   // first tick of the current general-kernel window
   hipEvent_t ra = nullptr, rb = nullptr;
   if (e->prof == 2) {
@@ -687,7 +725,9 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     const int64_t t = first_tick + int64_t(i);
     const Trace T = make_trace(e, t);
     unsigned long long* st = stats ? e->hist + size_t(i) * STAT_SLOTS * NSTAT : nullptr;
-    uint32_t* cnt = e->wcount + (window & 1);
+    // worklist counter of this window; zeroed by the previous general kernel
+    // (or at engine creation), so no per-call memset
+    uint32_t* cnt = e->wcount + (e->wpar & 1);
     hipEvent_t a = nullptr, b = nullptr;
     if (e->prof == 1) {
       a = next_event(e);
@@ -706,10 +746,21 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         fprintf(stderr, "raftstep: general kernel ticks %lld..%lld worklist %u\n", (long long)win_first, (long long)t, nw);
       }
       HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t, stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
-                              e->wcount + ((window + 1) & 1), e->stream));
-      ++window;
+                              e->wcount + ((e->wpar + 1) & 1), e->stream));
+      ++e->wpar;
+      if (stats)
+        if (int rc = flush_window_stats(e, uint32_t(win_first - first_tick), i)) return rc;
       win_first = t + 1;
     }
+  }
+  if (stats && e->comm) {   // the engine stream (readback, next call) waits for the last all-reduce
+    if (e->comm_ev.size() < 2) {
+      hipEvent_t x;
+      HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+      e->comm_ev.push_back(x);
+    }
+    HIPCHK(hipEventRecord(e->comm_ev[1], e->comm_stream));
+    HIPCHK(hipStreamWaitEvent(e->stream, e->comm_ev[1], 0));
   }
   if (e->prof == 2) {
     HIPCHK(hipEventRecord(rb, e->stream));
@@ -727,16 +778,6 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
             (long long)first_tick, (long long)(first_tick + nticks - 1), d[10], d[0], d[1], d[2], d[3], d[4], d[5], d[6],
             d[7], d[8], d[9], d[11], d[12], d[13], d[14], d[15]);
   }
-  if (stats && e->comm)
-    RCCLCHK(ncclAllReduce(e->hist, e->hist, size_t(nticks) * STAT_SLOTS * NSTAT, ncclUint64, ncclSum, e->comm,
-                          e->stream));
-  return RAFT_OK;
-}
-
-static int read_hist(raft_engine* e, uint32_t nticks, std::vector<unsigned long long>& h) {
-  h.resize(size_t(nticks) * STAT_SLOTS * NSTAT);
-  HIPCHK(hipMemcpyAsync(h.data(), e->hist, h.size() * 8, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
   return RAFT_OK;
 }
 
@@ -744,11 +785,25 @@ int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_sta
   if (!e) return fail(RAFT_EINVAL, "null engine");
   if (int rc = tick_impl(e, first_tick, nticks, out != nullptr)) return rc;
   if (out) {
-    std::vector<unsigned long long> h;
-    if (int rc = read_hist(e, nticks, h)) return rc;
+    // per-tick records, already summed over slots (and over GPUs)
+    std::vector<unsigned long long> h(size_t(nticks) * NSTAT);
+    HIPCHK(hipMemcpyAsync(h.data(), e->tstat, h.size() * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     std::memset(out, 0, sizeof *out);
     for (size_t i = 0; i < h.size(); ++i) out->v[i % NSTAT] += int64_t(h[i]);
   }
+  return RAFT_OK;
+}
+
+int raft_tick_records(raft_engine* e, uint32_t nticks, raft_tick_stats* per_tick) {
+  if (!e || (nticks && !per_tick)) return fail(RAFT_EINVAL, "null argument");
+  if (nticks > e->hist_cap || !e->tstat) return fail(RAFT_ERANGE, "only %u per-tick records are held", e->hist_cap);
+  HIPCHK(hipSetDevice(e->cfg.device));
+  std::vector<unsigned long long> h(size_t(nticks) * NSTAT);
+  HIPCHK(hipMemcpyAsync(h.data(), e->tstat, h.size() * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  for (uint32_t t = 0; t < nticks; ++t)
+    for (int s = 0; s < NSTAT; ++s) per_tick[t].v[s] = int64_t(h[size_t(t) * NSTAT + s]);
   return RAFT_OK;
 }
 
@@ -773,7 +828,8 @@ int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_re
     if (q.to >= e->cfg.replicas) return fail(RAFT_EINVAL, "req %zu: receiver out of range", i);
     if (!fits32(q.term) || !fits32(q.prev_log_index) || !fits32(q.prev_log_term) || !fits32(q.leader_commit))
       return fail(RAFT_EINVAL, "req %zu: term/index outside the int32 range of the engine", i);
-    if (q.n_entries > uint64_t(I32) || q.entries_offset + q.n_entries > n_entries_total || (q.n_entries && !entries))
+    if (q.n_entries > uint64_t(I32) || q.entries_offset > n_entries_total ||
+        q.n_entries > n_entries_total - q.entries_offset || (q.n_entries && !entries))
       return fail(RAFT_EINVAL, "req %zu: entries out of range", i);
     DevOp& o = ops[i];
     std::memset(&o, 0, sizeof o);
@@ -782,14 +838,18 @@ int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_re
     o.prev_term = int32_t(q.prev_log_term); o.lc = int32_t(q.leader_commit);
     o.n = uint32_t(q.n_entries);
     o.off = et.size();
-    // only the last K entries of a request can land in the ring
+    o.voff = ev.size();
+    // only the last K entries of a request can land in the ring: their values
+    // and stamps are staged; every term is (RAFT compares terms before it
+    // truncates, HostSrc)
     const uint64_t K = e->cfg.ring_depth;
     const uint64_t j0 = q.n_entries > K ? q.n_entries - K : 0;
+    o.skip = uint32_t(j0);
     for (uint64_t j = 0; j < q.n_entries; ++j) {
       const raft_log_entry& le = entries[q.entries_offset + j];
       if (!fits32(le.term)) return fail(RAFT_EINVAL, "req %zu: entry term outside int32", i);
-      if (j < j0) { et.push_back(0); ev.push_back(0); ec.push_back(0); continue; }
       et.push_back(int32_t(le.term));
+      if (j < j0) continue;
       ev.push_back(le.value);
       ec.push_back(e->cfg.payload_crc ? host_entry_crc(int32_t(le.term), le.value) : 0u);  // stamped on ingest
     }
@@ -874,9 +934,23 @@ int raft_comm_init(raft_engine* e, int nranks, int rank, const uint8_t id[128]) 
   HIPCHK(hipSetDevice(e->cfg.device));
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
+  if (!e->comm_stream) HIPCHK(hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
   RCCLCHK(ncclCommInitRank(&e->comm, nranks, uid, rank));
   e->nranks = nranks;
   e->rank = rank;
+  return RAFT_OK;
+}
+
+int raft_comm_info(raft_engine* e, int32_t* nranks, int32_t* rank, uint64_t* allreduces) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  int n = 1, r = 0;
+  if (e->comm) {
+    RCCLCHK(ncclCommCount(e->comm, &n));
+    RCCLCHK(ncclCommUserRank(e->comm, &r));
+  }
+  if (nranks) *nranks = n;
+  if (rank) *rank = r;
+  if (allreduces) *allreduces = e->allreduces;
   return RAFT_OK;
 }
 
@@ -884,12 +958,12 @@ int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats) {
   if (!e || !stats) return fail(RAFT_EINVAL, "null argument");
   if (!e->comm) return RAFT_OK;
   HIPCHK(hipSetDevice(e->cfg.device));
-  if (int rc = ensure_hist(e, 1)) return rc;
+  if (!e->cstat) HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->cstat), NSTAT * 8));
   std::vector<unsigned long long> h(NSTAT);
   for (int s = 0; s < NSTAT; ++s) h[s] = (unsigned long long)stats->v[s];
-  HIPCHK(hipMemcpyAsync(e->hist, h.data(), NSTAT * 8, hipMemcpyHostToDevice, e->stream));
-  RCCLCHK(ncclAllReduce(e->hist, e->hist, NSTAT, ncclUint64, ncclSum, e->comm, e->stream));
-  HIPCHK(hipMemcpyAsync(h.data(), e->hist, NSTAT * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(e->cstat, h.data(), NSTAT * 8, hipMemcpyHostToDevice, e->stream));
+  RCCLCHK(ncclAllReduce(e->cstat, e->cstat, NSTAT, ncclUint64, ncclSum, e->comm, e->stream));
+  HIPCHK(hipMemcpyAsync(h.data(), e->cstat, NSTAT * 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   for (int s = 0; s < NSTAT; ++s) stats->v[s] = int64_t(h[s]);
   return RAFT_OK;
@@ -1049,9 +1123,12 @@ int raft_checkpoint_save(raft_engine* e, const char* path) {
     *fields[i].ptr = bufs[i].data();
   }
   if (int rc = raft_store_state(e, &v)) return rc;
+  // written to <path>.tmp, flushed to disk, then renamed over <path>: a crash
+  // mid-write leaves the previous checkpoint intact
+  const std::string tmp = std::string(path) + ".tmp";
   File f;
-  f.f = fopen(path, "wb");
-  if (!f.f) return fail(RAFT_EINVAL, "cannot open %s for writing", path);
+  f.f = fopen(tmp.c_str(), "wb");
+  if (!f.f) return fail(RAFT_EINVAL, "cannot open %s for writing", tmp.c_str());
   uint32_t crc = 0;
   auto put = [&](const void* p, size_t n) {
     crc = crc32c_update(crc, static_cast<const uint8_t*>(p), n);
@@ -1071,8 +1148,17 @@ int raft_checkpoint_save(raft_engine* e, const char* path) {
     ok = put(&fh, sizeof fh) && put(bufs[i].data(), bufs[i].size());
   }
   ok = ok && fwrite(&crc, 1, 4, f.f) == 4;
-  ok = ok && fflush(f.f) == 0;
-  if (!ok) return fail(RAFT_EINVAL, "short write to %s", path);
+  ok = ok && fflush(f.f) == 0 && fsync(fileno(f.f)) == 0;
+  ok = fclose(f.f) == 0 && ok;
+  f.f = nullptr;
+  if (!ok) {
+    std::remove(tmp.c_str());
+    return fail(RAFT_EINVAL, "short write to %s", tmp.c_str());
+  }
+  if (std::rename(tmp.c_str(), path) != 0) {
+    std::remove(tmp.c_str());
+    return fail(RAFT_EINVAL, "cannot rename %s to %s", tmp.c_str(), path);
+  }
   return RAFT_OK;
 }
 
@@ -1096,6 +1182,28 @@ int raft_checkpoint_load(raft_engine* e, const char* path) {
       h.cfg.semantics != e->cfg.semantics || h.cfg.payload_crc != e->cfg.payload_crc)
     return fail(RAFT_EINVAL, "%s: checkpoint of R=%u G=%llu K=%u sem=%u crc=%u does not fit this engine", path,
                 h.cfg.replicas, (unsigned long long)h.cfg.groups, h.cfg.ring_depth, h.cfg.semantics, h.cfg.payload_crc);
+  // the trace (client values, timer draws, isolation, corruption) is keyed by
+  // the seed and the GLOBAL group id: resuming on another shard or another
+  // trace would silently continue on a different RNG stream
+  {
+    const raft_config& a = h.cfg;
+    const raft_config& b = e->cfg;
+    const char* bad = nullptr;
+    if (a.group_base != b.group_base) bad = "group_base";
+    else if (a.seed != b.seed) bad = "seed";
+    else if (a.tick_seconds != b.tick_seconds) bad = "tick_seconds";
+    else if (a.follower_timeout_min != b.follower_timeout_min || a.follower_timeout_span != b.follower_timeout_span)
+      bad = "follower timeout range";
+    else if (a.candidate_timeout_min != b.candidate_timeout_min || a.candidate_timeout_span != b.candidate_timeout_span)
+      bad = "candidate timeout range";
+    else if (a.client_period != b.client_period) bad = "client_period";
+    else if (a.entries_per_tick != b.entries_per_tick) bad = "entries_per_tick";
+    else if (a.isolate_per_65536 != b.isolate_per_65536 || a.isolate_min_ticks != b.isolate_min_ticks ||
+             a.isolate_max_ticks != b.isolate_max_ticks || a.isolate_leader != b.isolate_leader)
+      bad = "isolation parameters";
+    else if (a.corrupt_per_65536 != b.corrupt_per_65536) bad = "corrupt_per_65536";
+    if (bad) return fail(RAFT_EINVAL, "%s: checkpoint %s differs from this engine's (trace would diverge)", path, bad);
+  }
   raft_state_view v{};
   auto fields = view_fields(v, G, R, K);
   if (h.nfields != fields.size()) return fail(RAFT_EINVAL, "%s: %u fields, expected %zu", path, h.nfields, fields.size());

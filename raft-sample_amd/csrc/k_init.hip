@@ -129,6 +129,37 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
   if ((threadIdx.x & 63) == 0 && x) atomicAdd(total, x);
 }
 
+// Per-tick statistics: the STAT_SLOTS x NSTAT atomic slots of each tick in
+// [0, nt) are summed into out[t][NSTAT] (the 64-B record the multi-GPU
+// all-reduce carries) and zeroed for the next raft_tick call, so the atomic
+// targets never need a memset on the critical path. One 64-lane block per
+// tick; lane = slot.
+__global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hist, unsigned long long* out) {
+  static_assert(STAT_SLOTS == 64, "one lane per slot");
+  unsigned long long* h = hist + size_t(blockIdx.x) * STAT_SLOTS * NSTAT + threadIdx.x * NSTAT;
+  unsigned long long v[NSTAT];
+#pragma unroll
+  for (int s = 0; s < NSTAT; ++s) {
+    v[s] = h[s];
+    h[s] = 0ull;
+  }
+#pragma unroll
+  for (int s = 0; s < NSTAT; ++s)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[s] += __shfl_xor(v[s], o);
+  if (threadIdx.x < NSTAT) {
+    unsigned long long x = 0;
+#pragma unroll
+    for (int s = 0; s < NSTAT; ++s) x = (int(threadIdx.x) == s) ? v[s] : x;
+    out[size_t(blockIdx.x) * NSTAT + threadIdx.x] = x;
+  }
+}
+hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s) {
+  if (!nticks) return hipSuccess;
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3(nticks), dim3(64), 0, s, hist, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_tick_slow_ref(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t win_first, int64_t last_tick,
                                 unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
                                 const uint32_t* work_count, uint32_t* next_count, hipStream_t s);

@@ -29,8 +29,9 @@ struct DevOp {
   int64_t arg;        // CLIENT_APPEND value
   int32_t term, prev_idx, prev_term, lc;  // AE / VR request fields
   uint32_t n;         // AE: len(Logs)
-  uint32_t pad;
-  uint64_t off;       // AE: offset into the entry arrays
+  uint32_t skip;      // AE: values/stamps of Logs[0..skip) are not staged (only the last K can land in the ring)
+  uint64_t off;       // AE: offset of Logs[0] in the term array
+  uint64_t voff;      // AE: offset of Logs[skip] in the value / stamp arrays
 };
 struct DevRes {
   int32_t status, fault, ok, term;
@@ -52,6 +53,9 @@ hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_
 // Per-group state digest (same definition as oracle_state_digest) + wrapping sum.
 hipError_t launch_digest(int R, const DevPlanes& P, int raft, uint64_t* per_group, unsigned long long* total,
                          hipStream_t s);
+// Sums the STAT_SLOTS slots of nticks consecutive per-tick records of `hist`
+// into out[nticks][NSTAT] and zeroes those slots.
+hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s);
 hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s);
 
 }  // namespace raftstep

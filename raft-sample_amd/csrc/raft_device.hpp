@@ -111,8 +111,10 @@ __device__ __forceinline__ uint32_t ring_in_tile(uint32_t g, uint32_t R, uint32_
 // Addressing: every access is a wave-uniform base (SGPRs: plane + replica
 // row, or replica ring) plus a 32-bit per-lane byte offset, so the compiler
 // emits global_load/store with an SGPR base and ONE shared VGPR offset
-// instead of a 64-bit VGPR address per (plane, replica). The engine
-// guarantees every offset fits 32 bits (Gp*4 and K*Gp*8 < 2^32).
+// instead of a 64-bit VGPR address per (plane, replica). The byte offset
+// idx*sizeof(T) must fit 32 bits: raft_engine_create rejects Gp*4 >= 2^32
+// (per-group planes hold at most 4-B elements; ring offsets are taken inside
+// a KP*64*R tile, < 2^26 bytes).
 template <typename T>
 __device__ __forceinline__ T* prow(T* plane, int r, uint64_t Gp) {
   return plane + uint64_t(r) * Gp;
@@ -1104,17 +1106,21 @@ struct TickSrc {
 };
 
 // Entry source of a host-supplied AppendEntriesRequest (handler batch API);
-// host payloads are stamped on ingest.
+// host payloads are stamped on ingest. Every term is staged; values and
+// stamps only for Logs[skip..n), the last K (all that can land in the ring).
 struct HostSrc {
   const int32_t* et;
   const int64_t* ev;
   const uint32_t* ec;
-  uint64_t off;
+  uint64_t off, voff;
+  uint32_t skip;
   int from;
   __device__ __forceinline__ void fetch(int j, int& t, int64_t& v, uint32_t& c) const {
     t = et[off + uint64_t(j)];
-    v = ev[off + uint64_t(j)];
-    c = ec[off + uint64_t(j)];
+    if (uint32_t(j) < skip) { v = 0; c = 0; return; }
+    const uint64_t k = voff + uint64_t(uint32_t(j) - skip);
+    v = ev[k];
+    c = ec[k];
   }
 };
 

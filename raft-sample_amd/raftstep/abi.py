@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-RAFT_ABI_VERSION = 3
+RAFT_ABI_VERSION = 4
 RAFT_MAX_REPLICAS = 8
 
 FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
@@ -40,7 +40,8 @@ class Config(C.Structure):
         ("isolate_max_ticks", C.c_uint32),
         ("device", C.c_int32),
         ("payload_crc", C.c_uint32), ("corrupt_per_65536", C.c_uint32),
-        ("reserved", C.c_uint32 * 6),
+        ("isolate_leader", C.c_uint32),
+        ("reserved", C.c_uint32 * 5),
     ]
 
 
@@ -63,6 +64,7 @@ def default_config(**kw):
     c.device = 0
     c.payload_crc = 0
     c.corrupt_per_65536 = 0
+    c.isolate_leader = 0
     for k, v in kw.items():
         if not hasattr(c, k):
             raise TypeError(f"unknown config field {k!r}")
@@ -103,6 +105,32 @@ def state_shapes(groups, replicas, ring_depth):
 
 def empty_state(groups, replicas, ring_depth):
     return {k: np.zeros(s, d) for k, (s, d) in state_shapes(groups, replicas, ring_depth).items()}
+
+
+OPTIONAL_ON_LOAD = ("log_crc", "next", "hwm")   # raft_load_state: NULL derives them (raftstep.h)
+
+
+def coerce_state(state, groups, replicas, ring_depth):
+    """Canonical view arrays for raft_load_state: each field converted to its
+    C type and checked against its shape (a wrong dtype would be read as
+    garbage, a short array past its end); optional fields may be absent."""
+    out = {}
+    for k, (shape, dt) in state_shapes(groups, replicas, ring_depth).items():
+        a = state.get(k)
+        if a is None:
+            if k in OPTIONAL_ON_LOAD:
+                continue
+            raise KeyError(f"state field {k!r} is required")
+        a = np.asarray(a)
+        if a.dtype.kind not in "iub":
+            raise TypeError(f"state field {k!r}: integer array expected, got {a.dtype}")
+        if a.shape != shape:
+            raise ValueError(f"state field {k!r}: shape {a.shape}, expected {shape}")
+        c = np.ascontiguousarray(a, dtype=dt)
+        if not np.array_equal(c, a):
+            raise ValueError(f"state field {k!r}: values do not fit {np.dtype(dt).name}")
+        out[k] = c
+    return out
 
 
 def make_view(state):
@@ -147,6 +175,8 @@ SIGNATURES = {
     "raft_store_state": (C.c_int, [P, P]),
     "raft_tick": (C.c_int, [P, C.c_int64, C.c_uint32, P]),
     "raft_sync": (C.c_int, [P]),
+    "raft_tick_records": (C.c_int, [P, C.c_uint32, P]),
+    "raft_comm_info": (C.c_int, [P, P, P, P]),
     "raft_append_entries_batch": (C.c_int, [P, C.c_int64, P, C.c_size_t, P, C.c_size_t, P]),
     "raft_request_vote_batch": (C.c_int, [P, C.c_int64, P, C.c_size_t, P]),
     "raft_group_ops_batch": (C.c_int, [P, C.c_int64, P, C.c_size_t, P]),

@@ -13,6 +13,8 @@ def shard(groups_total, world, rank):
     """Contiguous balanced range of global group ids owned by `rank`."""
     if not 0 <= rank < world:
         raise ValueError("rank out of range")
+    if groups_total < world:   # raft_engine_create rejects an empty shard
+        raise ValueError(f"{groups_total} groups cannot be sharded over {world} ranks (need groups_total >= world)")
     lo = groups_total * rank // world
     hi = groups_total * (rank + 1) // world
     return lo, hi - lo

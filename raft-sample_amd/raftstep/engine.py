@@ -103,7 +103,7 @@ class Engine:
         return st
 
     def load_state(self, st):
-        st = {k: np.ascontiguousarray(st[k]) for k in abi.STATE_FIELDS}
+        st = abi.coerce_state(st, self.cfg.groups, self.cfg.replicas, self.cfg.ring_depth)
         v = abi.make_view(st)
         _check(self.lib.raft_load_state(self.h, C.byref(v)))
 
@@ -137,6 +137,13 @@ class Engine:
             return np.array(s.v, dtype=np.int64)
         _check(self.lib.raft_tick(self.h, first_tick, nticks, None))
         return None
+
+    def tick_records(self, nticks):
+        """Per-tick stats [nticks][8] of the last tick(stats=True) call (device-reduced,
+        summed over GPUs with a communicator)."""
+        recs = (abi.TickStats * nticks)()
+        _check(self.lib.raft_tick_records(self.h, nticks, recs))
+        return np.array([list(r.v) for r in recs], dtype=np.int64).reshape(nticks, abi.NSTATS)
 
     def sync(self):
         _check(self.lib.raft_sync(self.h))
@@ -173,6 +180,12 @@ class Engine:
     def comm_init(self, nranks, rank, uid):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         _check(self.lib.raft_comm_init(self.h, nranks, rank, buf))
+
+    def comm_info(self):
+        """(nranks, rank, allreduces issued) as RCCL reports them (1, 0, n without a communicator)."""
+        n, r, k = C.c_int32(), C.c_int32(), C.c_uint64()
+        _check(self.lib.raft_comm_info(self.h, C.byref(n), C.byref(r), C.byref(k)))
+        return n.value, r.value, k.value
 
     def allreduce_stats(self, stats):
         s = abi.TickStats()

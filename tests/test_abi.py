@@ -6,6 +6,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 from raftstep import abi, engine
@@ -72,3 +73,53 @@ def test_missing_library_fails_loudly(tmp_path):
         engine.load_library(str(tmp_path / "nope.so"))
     engine._lib = None
     engine.load_library()
+
+
+@pytest.mark.parametrize("field,value,msg", [
+    ("groups", (1 << 30) - 255, "too many groups"),   # Gp*4 would wrap the 32-bit byte offsets
+    ("groups", 0, "groups must be"),
+    ("replicas", 9, "replicas"),
+    ("ring_depth", 24, "power of two"),
+    ("isolate_leader", 2, "isolate_leader"),
+])
+def test_engine_create_rejects_bad_configs_before_touching_a_gpu(field, value, msg):
+    """Config validation runs before any HIP call, so it is checkable here."""
+    lib = engine.load_library()
+    c = abi.default_config(**{field: value})
+    h = C.c_void_p()
+    rc = lib.raft_engine_create(C.byref(c), C.byref(h))
+    assert rc == abi.RAFT_EINVAL and not h.value
+    assert msg in lib.raft_last_error().decode()
+
+
+def test_largest_engine_size_is_accepted_by_validation():
+    """groups = 2^30 - 256 passes the size checks (then fails only for lack of a device here)."""
+    lib = engine.load_library()
+    c = abi.default_config(groups=(1 << 30) - 256)
+    h = C.c_void_p()
+    rc = lib.raft_engine_create(C.byref(c), C.byref(h))
+    assert rc != abi.RAFT_EINVAL or "too many groups" not in lib.raft_last_error().decode()
+
+
+def test_coerce_state_checks_dtype_shape_and_optional_fields():
+    G, R, K = 3, 5, 8
+    st = abi.empty_state(G, R, K)
+    st["term"] = st["term"].astype(np.int64) + 7          # int64 after numpy arithmetic: converted, not misread
+    out = abi.coerce_state(st, G, R, K)
+    assert out["term"].dtype == np.int32 and (out["term"] == 7).all()
+    for k in abi.OPTIONAL_ON_LOAD:                          # optional fields may be absent
+        del st[k]
+    out = abi.coerce_state(st, G, R, K)
+    assert not set(abi.OPTIONAL_ON_LOAD) & set(out)
+    bad = dict(st, last=np.zeros((G, R - 1), np.int32))     # short array: refused, never read past its end
+    with pytest.raises(ValueError, match="shape"):
+        abi.coerce_state(bad, G, R, K)
+    bad = dict(st, term=np.full((G, R), 1 << 40))           # does not fit int32
+    with pytest.raises(ValueError, match="fit"):
+        abi.coerce_state(bad, G, R, K)
+    bad = dict(st, commit=np.zeros((G, R), np.float32))
+    with pytest.raises(TypeError):
+        abi.coerce_state(bad, G, R, K)
+    missing = {k: v for k, v in st.items() if k != "fault"}
+    with pytest.raises(KeyError):
+        abi.coerce_state(missing, G, R, K)

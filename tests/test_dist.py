@@ -68,7 +68,15 @@ def test_sharded_equals_single_process(tmp_path, oracle_mod):
     assert ref_stats[1] > 0  # elections happened
 
 
-@pytest.mark.parametrize("total,world", [(10, 3), (1 << 20, 8), (7, 7), (5, 8)])
+def test_shard_rejects_empty_shards():
+    """groups_total < world would leave a rank with 0 groups, which
+    raft_engine_create rejects: shard() says so up front."""
+    from raftstep import dist as rdist
+    with pytest.raises(ValueError, match="cannot be sharded"):
+        rdist.shard(5, 8, 0)
+
+
+@pytest.mark.parametrize("total,world", [(10, 3), (1 << 20, 8), (7, 7), (1 << 24, 8)])
 def test_shard_ranges_cover_exactly(total, world):
     from raftstep import dist as rdist
     spans = [rdist.shard(total, world, r) for r in range(world)]

@@ -67,17 +67,19 @@ def test_device_digest_matches_oracle(name):
 
 
 def test_full_size_c2_digest_parity():
-    """BASELINE config C2 at full size: 2^20 groups x R=5, steady state,
-    every group's state after 24 ticks equal to the oracle's (through the
-    per-group digest; the whole canonical view would be ~1 GB)."""
+    """BASELINE config C2 at full size: 2^20 groups x R=5, K=32, steady state,
+    every group's state equal to the oracle's (through the per-group digest;
+    the whole canonical view would be ~1 GB) after 24 ticks and again after
+    48, past the wrap of the 32-slot ring."""
     kw = dict(replicas=5, groups=1 << 20, ring_depth=32, client_period=1, seed=0x5EED0002)
     e, o = both(**kw)
     e.init_steady(0, 0)
     o.init_steady(0, 0)
-    se = e.tick(1, 24)
-    so = o.tick(1, 24, threads=THREADS)
-    assert list(se) == list(so)
-    assert_same_digest(e, o, "C2 full size after 24 ticks")
+    for t, k in ((1, 24), (25, 24)):
+        se = e.tick(t, k)
+        so = o.tick(t, k, threads=THREADS)
+        assert list(se) == list(so)
+        assert_same_digest(e, o, f"C2 full size after tick {t + k - 1}")
 
 
 def test_full_size_c4_shape_digest_parity():
@@ -91,6 +93,23 @@ def test_full_size_c4_shape_digest_parity():
     for t, k in ((0, 48), (48, 16)):
         assert list(e.tick(t, k)) == list(o.tick(t, k, threads=THREADS)), f"stats [{t}, {t + k})"
     assert_same_digest(e, o, "C4 shape full size after 64 ticks")
+
+
+def test_full_size_c4_shape_digest_parity_past_ring_wrap():
+    """C4's shape (R=7, NewNode start, isolation churn, RAFT) on 2^20 groups
+    with K=64 for 160 ticks: past the wrap of the 2K = 128 physical ring slots
+    (KP = 2K under isolation churn), so ring phase-segment switches and slot
+    reuse happen at full size; digest parity at three points."""
+    kw = dict(replicas=7, groups=1 << 20, ring_depth=64, client_period=1, seed=0x5EED0004,
+              semantics=abi.SEM_RAFT, isolate_per_65536=8192, isolate_min_ticks=8, isolate_max_ticks=32)
+    e, o = both(**kw)
+    e.init_new_nodes(0)
+    o.init_new_nodes(0)
+    t = 0
+    for k in (48, 56, 56):
+        assert list(e.tick(t, k)) == list(o.tick(t, k, threads=THREADS)), f"stats [{t}, {t + k})"
+        t += k
+        assert_same_digest(e, o, f"C4 shape K=64 full size after tick {t - 1}")
 
 
 def test_nodelog_matches_oracle():
@@ -153,6 +172,20 @@ def test_checkpoint_rejects_corruption_and_mismatch(tmp_path):
         short = tmp_path / "short.bin"
         short.write_bytes(bytes(data[:400]))
         Engine(**kw).load_checkpoint(short)
+    # the Python reader verifies the trailer too
+    with pytest.raises(ValueError, match="CRC32C"):
+        checkpoint.read(bad)
+    # another shard's or another trace's checkpoint would resume on a different RNG stream
+    with pytest.raises(RaftError, match="group_base"):
+        Engine(**dict(kw, group_base=100)).load_checkpoint(path)
+    with pytest.raises(RaftError, match="seed"):
+        Engine(**dict(kw, seed=2)).load_checkpoint(path)
+    with pytest.raises(RaftError, match="client_period"):
+        Engine(**dict(kw, client_period=1)).load_checkpoint(path)
+    # saving goes through <path>.tmp + rename: no temporary is left behind
+    a.save_checkpoint(path)
+    assert not (tmp_path / "ck.bin.tmp").exists()
+    assert Engine(**kw).load_checkpoint(path) is None
 
 
 @pytest.mark.parametrize("sem", [abi.SEM_REF, abi.SEM_RAFT])

@@ -17,6 +17,40 @@ def test_rccl_single_rank_stats():
     sa, sb = a.tick(1, 10), b.tick(1, 10)
     assert list(sa) == list(sb) == [50000, 0, 0, 200000, 0, 0, 0, 50000]
     assert list(a.allreduce_stats(sa)) == list(sa)
+    assert a.comm_info()[:2] == (1, 0) and b.comm_info() == (1, 0, 0)
+
+
+@pytest.mark.parametrize("slow_every", ["1", "3", "8"])
+def test_side_stream_stats_sum_equals_host_sum(monkeypatch, slow_every):
+    """each general-kernel window's per-tick records are reduced
+    on the device to int64[8] and all-reduced by RCCL on the comm stream.
+    With a single-rank communicator the side-stream sum must equal the
+    records of an engine without one, record by record, and their host-side
+    sum must equal raft_tick's total; one all-reduce per window."""
+    from raftstep import Engine
+    monkeypatch.setenv("RAFTSTEP_SLOW_EVERY", slow_every)
+    kw = dict(replicas=5, groups=3000, client_period=1, seed=0x5EED0003, isolate_per_65536=12000)
+    a, b = Engine(**kw), Engine(**kw)
+    a.comm_init(1, 0, Engine.comm_unique_id())
+    for e in (a, b):
+        e.init_new_nodes(0)
+    n = 40
+    sa, sb = a.tick(0, n), b.tick(0, n)
+    ra, rb = a.tick_records(n), b.tick_records(n)
+    assert (ra == rb).all()
+    assert list(ra.sum(axis=0)) == list(sa) == list(sb)
+    assert ra[:, 1].sum() > 0 and (ra[:, 7] > 0).any()   # elections happened, leaders exist
+    import oracle
+    o = oracle.Oracle(**kw)
+    o.init_new_nodes(0)
+    for t in range(n):   # every per-tick record equals the oracle's stats of that tick
+        assert list(o.tick(t, 1)) == list(ra[t]), f"tick {t}"
+    se = int(slow_every)
+    assert a.comm_info() == (1, 0, (n + se - 1) // se)
+    # a second call starts from clean atomic slots (the reduce kernel re-zeroes them)
+    sa2, sb2 = a.tick(n, 7), b.tick(n, 7)
+    assert list(sa2) == list(sb2)
+    assert list(a.tick_records(7).sum(axis=0)) == list(sa2)
 
 
 def test_group_base_shards_are_invariant():
