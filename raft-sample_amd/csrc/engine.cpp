@@ -106,6 +106,7 @@ struct raft_engine {
   int32_t* work_tick = nullptr; // tick each one was deferred at
   uint32_t* wcount = nullptr;   // [2], indexed by window parity
   int force_general = 0;        // debug: route every group through the general kernel
+  int lane_general = 0;         // RAFTSTEP_GENERAL=lane: one-lane-per-group general kernel (A/B) instead of the segment one
   uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
   int write_through = 0;        // fast kernel stores with sc1 (write-through) instead of write-back
   int debug_work = 0;           // RAFTSTEP_DEBUG_WORK: print each general-kernel worklist size
@@ -386,6 +387,9 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->P.crc_on = c.payload_crc;
   e->P.corrupt_p = c.corrupt_per_65536;
   if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
+  if (const char* gk = getenv("RAFTSTEP_GENERAL")) e->lane_general = std::strcmp(gk, "lane") == 0;
+  // the segment kernel addresses [R][Gp] planes with 32-bit byte offsets (seg_tick.hpp)
+  if (R * Gp * 4 > uint64_t(0xFFFFFFFFu)) e->lane_general = 1;
   if (const char* se = getenv("RAFTSTEP_SLOW_EVERY")) e->slow_every = std::max(1, atoi(se));
   if (const char* wt = getenv("RAFTSTEP_WRITE_THROUGH")) e->write_through = atoi(wt) != 0;
   if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
@@ -745,8 +749,8 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         HIPCHK(hipStreamSynchronize(e->stream));
         fprintf(stderr, "raftstep: general kernel ticks %lld..%lld worklist %u\n", (long long)win_first, (long long)t, nw);
       }
-      HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t, stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
-                              e->wcount + ((e->wpar + 1) & 1), e->stream));
+      HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t, stats ? e->hist : nullptr,
+                              e->work, e->work_tick, cnt, e->wcount + ((e->wpar + 1) & 1), e->lane_general, e->stream));
       ++e->wpar;
       if (stats)
         if (int rc = flush_window_stats(e, uint32_t(win_first - first_tick), i)) return rc;

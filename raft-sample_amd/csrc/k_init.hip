@@ -162,10 +162,10 @@ hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out
 
 hipError_t launch_tick_slow_ref(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t win_first, int64_t last_tick,
                                 unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
-                                const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
+                                const uint32_t* work_count, uint32_t* next_count, int lane_per_group, hipStream_t s);
 hipError_t launch_tick_slow_raft(int R, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t win_first, int64_t last_tick,
                                  unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
-                                 const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
+                                 const uint32_t* work_count, uint32_t* next_count, int lane_per_group, hipStream_t s);
 hipError_t launch_ops_ref(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n, const int32_t* et,
                           const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s);
 hipError_t launch_ops_raft(int R, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n, const int32_t* et,
@@ -173,10 +173,12 @@ hipError_t launch_ops_raft(int R, const DevPlanes& P, const Trace& T, const DevO
 
 hipError_t launch_tick_slow(int R, int sem, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t win_first, int64_t last_tick,
                             unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
-                            const uint32_t* work_count, uint32_t* next_count, hipStream_t s) {
+                            const uint32_t* work_count, uint32_t* next_count, int lane_per_group, hipStream_t s) {
   return sem == SEM_RAFT
-             ? launch_tick_slow_raft(R, P, T0, first_tick, win_first, last_tick, stats, work, work_tick, work_count, next_count, s)
-             : launch_tick_slow_ref(R, P, T0, first_tick, win_first, last_tick, stats, work, work_tick, work_count, next_count, s);
+             ? launch_tick_slow_raft(R, P, T0, first_tick, win_first, last_tick, stats, work, work_tick, work_count, next_count,
+                                     lane_per_group, s)
+             : launch_tick_slow_ref(R, P, T0, first_tick, win_first, last_tick, stats, work, work_tick, work_count, next_count,
+                                    lane_per_group, s);
 }
 hipError_t launch_ops(int R, int sem, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
                       const int32_t* et, const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s) {

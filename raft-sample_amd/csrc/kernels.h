@@ -43,10 +43,12 @@ struct DevRes {
 hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                             int32_t* work_tick, uint32_t* work_count, int force_slow, int write_through, hipStream_t s,
                             hipEvent_t ev_start, hipEvent_t ev_stop);
-// General kernel: catches every worklisted group up to last_tick; zeroes `next_count`.
+// General kernel: catches every worklisted group up to last_tick; zeroes
+// `next_count`. lane_per_group: the one-lane-per-group form (tick_slow_kernel)
+// instead of the replica-parallel one (tick_seg_kernel).
 hipError_t launch_tick_slow(int R, int sem, const DevPlanes& P, const Trace& T0, int64_t first_tick, int64_t win_first, int64_t last_tick,
                             unsigned long long* stats, const uint32_t* work, const int32_t* work_tick,
-                            const uint32_t* work_count, uint32_t* next_count, hipStream_t s);
+                            const uint32_t* work_count, uint32_t* next_count, int lane_per_group, hipStream_t s);
 hipError_t launch_ops(int R, int sem, const DevPlanes& P, const Trace& T, const DevOp* ops, uint32_t n,
                       const int32_t* et, const int64_t* ev, const uint32_t* ec, DevRes* out, hipStream_t s);
 hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_t s);
