@@ -314,11 +314,11 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
       (c.isolate_min_ticks < 1 || c.isolate_max_ticks > 32 || c.isolate_min_ticks > c.isolate_max_ticks))
     return fail(RAFT_EINVAL, "isolation length must satisfy 1 <= min <= max <= 32");
   const uint64_t Gp = (c.groups + 255) & ~uint64_t(255);
-  // device addressing (raft_device.hpp at()): 64-bit plane/tile bases, 32-bit
-  // per-lane BYTE offsets, so the widest per-group plane (4-B elements) must
-  // satisfy Gp*4 < 2^32, i.e. Gp <= 2^30 - 256 (ring tiles: KP*64*R*8 < 2^26)
-  if (Gp * 4 > uint64_t(0xFFFFFFFFu))
-    return fail(RAFT_EINVAL, "too many groups for one engine (need groups <= 2^30 - 256)");
+  // device addressing (raft_device.hpp at(), rix()): 64-bit plane/tile bases,
+  // 32-bit per-lane BYTE offsets, so the group-major per-replica planes (4-B
+  // elements) must satisfy Gp*R*4 < 2^32 (ring tiles: KP*64*R*8 < 2^26)
+  if (Gp * c.replicas * 4 > uint64_t(0xFFFFFFFFu))
+    return fail(RAFT_EINVAL, "too many groups for one engine (need groups * replicas <= 2^30 - 256 * replicas)");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RAFT_ENODEV, "no HIP device");
   if (c.device < 0 || c.device >= ndev) return fail(RAFT_ENODEV, "device %d out of range", c.device);
@@ -388,8 +388,6 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->P.corrupt_p = c.corrupt_per_65536;
   if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
   if (const char* gk = getenv("RAFTSTEP_GENERAL")) e->lane_general = std::strcmp(gk, "lane") == 0;
-  // the segment kernel addresses [R][Gp] planes with 32-bit byte offsets (seg_tick.hpp)
-  if (R * Gp * 4 > uint64_t(0xFFFFFFFFu)) e->lane_general = 1;
   if (const char* se = getenv("RAFTSTEP_SLOW_EVERY")) e->slow_every = std::max(1, atoi(se));
   if (const char* wt = getenv("RAFTSTEP_WRITE_THROUGH")) e->write_through = atoi(wt) != 0;
   if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
@@ -526,7 +524,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
     const bool msync = meta[g] & M_MSYNC;
     if (v->fault) v->fault[g] = uint8_t((meta[g] >> 4) & 0xF);
     for (uint64_t r = 0; r < R; ++r) {
-      const uint64_t d = r * Gp + g, c = g * R + r;
+      const uint64_t d = g * R + r, c = g * R + r;   // per-replica planes are group-major (rix)
       const int role = rs[d] & 3;
       if (v->role) v->role[c] = uint8_t(role);
       if (v->voted) v->voted[c] = uint8_t((rs[d] >> 2) & 15);
@@ -543,15 +541,15 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
         for (uint64_t p = 0; p < R; ++p) {
           int32_t m = 0;
           if (role == ROLE_L && p != r)
-            m = (int(r) == primary) ? (msync ? last[p * Gp + g] : lm[p * Gp + g]) : xm[(r * R + p) * Gp + g];
+            m = (int(r) == primary) ? (msync ? last[g * R + p] : lm[g * R + p]) : xm[(r * R + p) * Gp + g];
           v->match[c * R + p] = m;
         }
       if (v->next)
         for (uint64_t p = 0; p < R; ++p) {
           int32_t nx = 0;
           if (role == ROLE_L && p != r) {
-            if (raft) nx = (int(r) == primary) ? (msync ? last[p * Gp + g] + 1 : ln[p * Gp + g]) : xn[(r * R + p) * Gp + g];
-            else nx = ((int(r) == primary) ? (msync ? last[p * Gp + g] : lm[p * Gp + g]) : xm[(r * R + p) * Gp + g]) + 1;
+            if (raft) nx = (int(r) == primary) ? (msync ? last[g * R + p] + 1 : ln[g * R + p]) : xn[(r * R + p) * Gp + g];
+            else nx = ((int(r) == primary) ? (msync ? last[g * R + p] : lm[g * R + p]) : xm[(r * R + p) * Gp + g]) + 1;
           }
           v->next[c * R + p] = nx;
         }
@@ -616,7 +614,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
       if (int(r) != primary && v->role[g * R + r] != RAFT_FOLLOWER) steady = false;
     meta[g] = uint16_t(primary | (v->fault[g] << 4) | (steady ? M_STEADY : 0));
     for (uint64_t r = 0; r < R; ++r) {
-      const uint64_t d = r * Gp + g, c = g * R + r;
+      const uint64_t d = g * R + r, c = g * R + r;   // per-replica planes are group-major (rix)
       term[d] = v->term[c];
       last[d] = v->last[c];
       commit[d] = v->commit[c];
@@ -629,8 +627,8 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
           // RAFT: NextIndex as given, 0/absent derives match+1 (the oracle's rule)
           const int32_t nx = (v->next && v->next[c * R + p] > 0) ? v->next[c * R + p] : m + 1;
           if (int(r) == primary) {
-            lm[p * Gp + g] = m;
-            if (raft) ln[p * Gp + g] = nx;
+            lm[g * R + p] = m;
+            if (raft) ln[g * R + p] = nx;
           } else {
             xm[(r * R + p) * Gp + g] = m;
             if (raft) xn[(r * R + p) * Gp + g] = nx;
@@ -1029,7 +1027,7 @@ int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap) {
   static const char* names[] = {"follower", "candidate", "leader", "?"};   // State (main.go:51-57)
   std::string out;
   for (uint32_t r = 0; r < e->cfg.replicas; ++r) {
-    const uint64_t d = uint64_t(r) * e->Gp + group;
+    const uint64_t d = group * e->cfg.replicas + r;   // group-major (rix)
     int32_t term = 0, commit = 0, last = 0;
     uint16_t rs = 0;
     HIPCHK(hipMemcpyAsync(&term, e->P.term + d, 4, hipMemcpyDeviceToHost, e->stream));

@@ -50,6 +50,37 @@ __device__ __forceinline__ void fill_seg(T* p, T v) {
   }
 }
 
+// A group's R values of one per-replica plane are contiguous ([Gp][R], rix):
+// a lane moves them with R/4 dwordx4 accesses plus one for the remainder
+// (4-B aligned wide accesses are legal on gfx950) instead of R dword ones,
+// which keeps the wave's requests at ~2 per 128-B line instead of R.
+typedef int32_t row2 __attribute__((ext_vector_type(2), aligned(4)));
+typedef int32_t row3 __attribute__((ext_vector_type(3), aligned(4)));
+typedef int32_t row4 __attribute__((ext_vector_type(4), aligned(4)));
+template <int R>
+__device__ __forceinline__ void load_row(const int32_t* plane, uint32_t g, int (&o)[R]) {
+  const int32_t* q = &at(plane, rix<R>(g, 0));
+#pragma unroll
+  for (int i = 0; i + 4 <= R; i += 4) {
+    const row4 a = *reinterpret_cast<const row4*>(q + i);
+    o[i] = a.x; o[i + 1] = a.y; o[i + 2] = a.z; o[i + 3] = a.w;
+  }
+  constexpr int b = R & ~3, rem = R & 3;
+  if constexpr (rem == 3) { const row3 a = *reinterpret_cast<const row3*>(q + b); o[b] = a.x; o[b + 1] = a.y; o[b + 2] = a.z; }
+  if constexpr (rem == 2) { const row2 a = *reinterpret_cast<const row2*>(q + b); o[b] = a.x; o[b + 1] = a.y; }
+  if constexpr (rem == 1) o[b] = q[b];
+}
+template <int R>
+__device__ __forceinline__ void store_row(int32_t* plane, uint32_t g, const int (&v)[R]) {
+  int32_t* q = &at(plane, rix<R>(g, 0));
+#pragma unroll
+  for (int i = 0; i + 4 <= R; i += 4) *reinterpret_cast<row4*>(q + i) = row4{v[i], v[i + 1], v[i + 2], v[i + 3]};
+  constexpr int b = R & ~3, rem = R & 3;
+  if constexpr (rem == 3) *reinterpret_cast<row3*>(q + b) = row3{v[b], v[b + 1], v[b + 2]};
+  if constexpr (rem == 2) *reinterpret_cast<row2*>(q + b) = row2{v[b], v[b + 1]};
+  if constexpr (rem == 1) q[b] = v[b];
+}
+
 // A ONECAND group is taken only when a replica is isolated this tick (its
 // role, which must be the candidate, is checked once the rs row is read).
 template <bool RAFT>
@@ -99,27 +130,25 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     df |= skip ? 1u : 0u;
     DIAG_REASON(df |= bail ? 2048u : 0u;);   // diagnostics: deferral reason "group not steady"
     if (go) {
+      load_row<R>(P.term, g, term);
+      load_row<R>(P.last, g, last);
+      load_row<R>(P.commit, g, commit);
+      load_row<R>(P.lterm, g, lt);
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        term[r] = at(prow(P.term, r, P.Gp), g);
-        last[r] = at(prow(P.last, r, P.Gp), g);
-        commit[r] = at(prow(P.commit, r, P.Gp), g);
-        lt[r] = at(prow(P.lterm, r, P.Gp), g);
-        empty &= last[r] == 0;
-      }
+      for (int r = 0; r < R; ++r) empty &= last[r] == 0;
       if (meta & M_MSYNC) {
 #pragma unroll
         for (int r = 0; r < R; ++r) m[r] = (r != c) ? last[r] : 0;
       } else {
 #pragma unroll
-        for (int r = 0; r < R; ++r) m[r] = (r != c) ? at(prow(P.lmatch, r, P.Gp), g) : 0;
+        for (int r = 0; r < R; ++r) m[r] = (r != c) ? at(P.lmatch, rix<R>(g, r)) : 0;
         if constexpr (RAFT) {
           // RAFT rows kept explicitly: NextIndex must be MatchIndex+1 and no
           // log may be shorter than its high-water mark (no pending truncation)
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            if (r != c) bail |= at(prow(P.lnext, r, P.Gp), g) != m[r] + 1;
-            bail |= at(prow(P.hwm, r, P.Gp), g) != last[r];
+            if (r != c) bail |= at(P.lnext, rix<R>(g, r)) != m[r] + 1;
+            bail |= at(P.hwm, rix<R>(g, r)) != last[r];
           }
         }
       }
@@ -158,12 +187,12 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     int x_rs = 0, x_term = 0, x_fire = 0, x_dur = 0;
     if constexpr (RAFT) {
       if (go && !bail && xi >= 0) {
-        x_rs = at(prow(P.rs, xi, P.Gp), g);
+        x_rs = at(P.rs, rix<R>(g, xi));
         x_term = sel(term, xi);
         const int role = x_rs & 3;
         // STEADY: xi is a follower; ONECAND: xi is the group's one candidate
         if (role != ((meta & M_STEADY) ? ROLE_F : ROLE_C)) bail = true;
-        const int dl = max(at(prow(P.tstart, xi, P.Gp), g), at(P.hb, g)) + (x_rs >> 6);
+        const int dl = max(at(P.tstart, rix<R>(g, xi)), at(P.hb, g)) + (x_rs >> 6);
         if (dl <= T.now) {   // timer.C: Term++, vote for itself, new candidate timer (Raft §5.2)
           if (x_term >= I32MAX) bail = true;
           x_fire = 1;
@@ -265,27 +294,43 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       sv[3] = 1;
       sv[4] = x_fire;
       // ---- stores (no bail past this point) ----
-      if (n) {
-        st<WT>(P.last + uint64_t(c) * P.Gp, g, Ll + n);
-        if (Llt != Lt) st<WT>(P.lterm + uint64_t(c) * P.Gp, g, Lt);
+      // LastApplied / CommitIndex rows: one wide row store when every replica
+      // changes (the steady state), else the changed elements
+      const uint32_t all = (1u << R) - 1u;
+      const uint32_t peers = all & ~(1u << c);
+      const bool last_row = !WT && n && okm == peers;
+      const bool commit_row = !WT && cm != Lc && cch == peers;
+      if (last_row || commit_row) {
+        int lrow[R], crow[R];
+#pragma unroll
+        for (int p = 0; p < R; ++p) {
+          lrow[p] = p == c ? Ll + n : last[p];
+          crow[p] = p == c ? cm : commit[p];
+        }
+        if (last_row) store_row<R>(P.last, g, lrow);
+        if (commit_row) store_row<R>(P.commit, g, crow);
       }
-      if (cm != Lc) st<WT>(P.commit + uint64_t(c) * P.Gp, g, cm);
+      if (n) {
+        if (!last_row) st<WT>(P.last, rix<R>(g, c), Ll + n);
+        if (Llt != Lt) st<WT>(P.lterm, rix<R>(g, c), Lt);
+      }
+      if (cm != Lc && !commit_row) st<WT>(P.commit, rix<R>(g, c), cm);
       if (xi < 0) st<WT>(P.hb, g, T.now);                         // timer.Reset(d) of every follower
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == c || !((okm >> p) & 1u)) continue;
-        if (xi >= 0) st<WT>(prow(P.tstart, p, P.Gp), g, T.now);   // xi isolated: reset each receiver, not hb
-        if (n) st<WT>(prow(P.last, p, P.Gp), g, last[p]);
-        if (!sync && ((mch >> p) & 1u)) st<WT>(prow(P.lmatch, p, P.Gp), g, m[p]);
-        if ((cch >> p) & 1u) st<WT>(prow(P.commit, p, P.Gp), g, commit[p]);
-        if ((ltch >> p) & 1u) st<WT>(prow(P.lterm, p, P.Gp), g, Lt);
-        if (!RAFT && term[p] != Lt) st<WT>(prow(P.term, p, P.Gp), g, Lt);  // main.go:155
+        if (xi >= 0) st<WT>(P.tstart, rix<R>(g, p), T.now);   // xi isolated: reset each receiver, not hb
+        if (n && !last_row) st<WT>(P.last, rix<R>(g, p), last[p]);
+        if (!sync && ((mch >> p) & 1u)) st<WT>(P.lmatch, rix<R>(g, p), m[p]);
+        if (((cch >> p) & 1u) && !commit_row) st<WT>(P.commit, rix<R>(g, p), commit[p]);
+        if ((ltch >> p) & 1u) st<WT>(P.lterm, rix<R>(g, p), Lt);
+        if (!RAFT && term[p] != Lt) st<WT>(P.term, rix<R>(g, p), Lt);  // main.go:155
       }
       if constexpr (RAFT) {
         if (x_fire) {   // the isolated replica became / stays a candidate: Term+1, votedFor itself
-          st<WT>(prow(P.term, xi, P.Gp), g, x_term + 1);
-          st<WT>(prow(P.rs, xi, P.Gp), g, uint16_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
-          st<WT>(prow(P.tstart, xi, P.Gp), g, T.now);
+          st<WT>(P.term, rix<R>(g, xi), x_term + 1);
+          st<WT>(P.rs, rix<R>(g, xi), uint16_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
+          st<WT>(P.tstart, rix<R>(g, xi), T.now);
         }
       }
       // RAFT: MSYNC also makes NextIndex (= match+1) and the high-water marks (= last) implicit

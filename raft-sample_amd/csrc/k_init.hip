@@ -12,7 +12,7 @@ __global__ __launch_bounds__(256) void init_new_kernel(DevPlanes P, Trace T) {
   const uint64_t key = group_key(T.seed, P.gbase + g);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const uint64_t i = uint64_t(r) * P.Gp + g;
+    const uint64_t i = g * uint64_t(R) + uint64_t(r);   // group-major [Gp][R] (rix)
     const int d = T.f_min + int(uint32_t(rng_k(key, r, ST_TIMER_F, uint64_t(T.tick)) >> 32) % uint32_t(T.f_span));
     P.term[i] = 0; P.last[i] = 0; P.commit[i] = 0;
     P.tstart[i] = T.now;
@@ -37,7 +37,7 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
   const int L = leader >= 0 ? leader % R : int(uint32_t(sm64(T.seed ^ 0x1EADE5ULL ^ sm64(gid)) >> 33) % uint32_t(R));
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const uint64_t i = uint64_t(r) * P.Gp + g;
+    const uint64_t i = g * uint64_t(R) + uint64_t(r);   // group-major [Gp][R] (rix)
     const bool isL = r == L;
     const uint64_t h = rng_k(key, r, isL ? ST_TIMER_C : ST_TIMER_F, uint64_t(T.tick));
     const int d = isL ? T.c_min + int(uint32_t(h >> 32) % uint32_t(T.c_span))
@@ -81,29 +81,29 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
     const int hb = at(P.hb, g);
     int last[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) last[r] = at(prow(P.last, r, P.Gp), g);
+    for (int r = 0; r < R; ++r) last[r] = at(P.last, rix<R>(g, r));
     h = sm64(0x5241465444494721ULL ^ (P.gbase + g));
 #pragma unroll 1
     for (int r = 0; r < R; ++r) {
-      const uint32_t x = at(prow(P.rs, r, P.Gp), g);
+      const uint32_t x = at(P.rs, rix<R>(g, r));
       const int role = int(x & 3u), dur = int(x >> 6);
       const int l = sel(last, r);
-      const int ts = at(prow(P.tstart, r, P.Gp), g);
+      const int ts = at(P.tstart, rix<R>(g, r));
       const int dl = (role == ROLE_L ? ts : max(ts, hb)) + dur;
-      const int hwm = (raft && !msync) ? at(prow(P.hwm, r, P.Gp), g) : l;
+      const int hwm = (raft && !msync) ? at(P.hwm, rix<R>(g, r)) : l;
       h = dg_mix(h, uint64_t(role) | (uint64_t((x >> 2) & 15u) << 8) | (uint64_t(r) << 16));
-      h = dg_mix(h, lo32(at(prow(P.term, r, P.Gp), g)) | (lo32(l) << 32));
-      h = dg_mix(h, lo32(at(prow(P.commit, r, P.Gp), g)) | (lo32(dl) << 32));
+      h = dg_mix(h, lo32(at(P.term, rix<R>(g, r))) | (lo32(l) << 32));
+      h = dg_mix(h, lo32(at(P.commit, rix<R>(g, r))) | (lo32(dl) << 32));
       h = dg_mix(h, lo32(dur) | (lo32(hwm) << 32));
 #pragma unroll 1
       for (int p = 0; p < R; ++p) {
         int m = 0, nx = 0;
         if (role == ROLE_L && p != r) {
           const int lp = sel(last, p);
-          if (r == primary) m = msync ? lp : at(prow(P.lmatch, p, P.Gp), g);
+          if (r == primary) m = msync ? lp : at(P.lmatch, rix<R>(g, p));
           else m = at(prow(P.xmatch, r * R + p, P.Gp), g);
           if (!raft) nx = m + 1;
-          else if (r == primary) nx = msync ? lp + 1 : at(prow(P.lnext, p, P.Gp), g);
+          else if (r == primary) nx = msync ? lp + 1 : at(P.lnext, rix<R>(g, p));
           else nx = at(prow(P.xnext, r * R + p, P.Gp), g);
         }
         h = dg_mix(h, lo32(m) | (lo32(nx) << 32));

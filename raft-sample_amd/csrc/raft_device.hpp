@@ -1,8 +1,8 @@
 // raft_device.hpp — CDNA4 device code of the batched Raft step engine.
 //
 // One lane owns one Raft group for the duration of a launch. The group's R
-// replicas are loaded from struct-of-arrays planes ([R][Gp], one 256-B
-// coalesced wave access per plane) into registers, every message between
+// replicas are loaded from struct-of-arrays planes ([Gp][R]: a wave's 64
+// groups read one contiguous 64*R*4-B span per plane) into registers, every message between
 // replicas is a register hand-off inside the lane, and only changed fields
 // are stored back. Handler semantics follow main.go (eastwd/raft-sample)
 // exactly; each function cites the lines it implements. The CPU oracle in
@@ -42,8 +42,8 @@ constexpr int HB_NONE = -2147483647 - 1;
 constexpr int I32MAX = 2147483647;
 constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to cut atomic contention
 
-// Device layout. Per-replica scalar planes are [R][Gp]; the log rings are
-// wave tiles [Gp/64][KP][64][R] (see ring_tile below).
+// Device layout. Per-replica scalar planes are [Gp][R] (rix below); the
+// log rings are wave tiles [Gp/64][KP][64][R] (see ring_tile below).
 struct DevPlanes {
   int32_t* term;       // Node.Term                 (main.go:19)
   int32_t* last;       // Node.LastApplied=len(Log) (main.go:25)
@@ -52,16 +52,16 @@ struct DevPlanes {
   int32_t* hb;         // [Gp] time of the last steady-state heartbeat that reset every follower
   uint16_t* rs;        // role:2 | vote:4 | timer duration d:10 (main.go:16, 20, 114, 194);
                        // vote = Voted (REF) or votedFor+1 (RAFT, 0 = none)
-  int32_t* lmatch;     // [R][Gp] MatchIndex row of the group's primary leader (main.go:29)
+  int32_t* lmatch;     // [Gp][R] MatchIndex row of the group's primary leader (main.go:29)
   int32_t* xmatch;     // [R][R][Gp] rows of any further concurrent leaders (EXT only)
-  int32_t* lnext;      // RAFT mode: [R][Gp] NextIndex row of the primary leader (REF derives match+1)
+  int32_t* lnext;      // RAFT mode: [Gp][R] NextIndex row of the primary leader (REF derives match+1)
   int32_t* xnext;      // RAFT mode: [R][R][Gp] NextIndex rows of further leaders
-  int32_t* hwm;        // RAFT mode: [R][Gp] highest LastApplied ever (== last in REF)
+  int32_t* hwm;        // RAFT mode: [Gp][R] highest LastApplied ever (== last in REF)
   uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
   uint16_t* grot;      // ring rotation of the current segment: entry idx >= gsb sits at slot (idx-1+grot) mod KP
   uint16_t* grota;     // rotation of the previous segment (entries idx < gsb)
   int32_t* gsb;        // first index of the current segment (0: one segment)
-  int32_t* lterm;      // [R][Gp] Log[len-1].Term: cached term of each replica's last entry
+  int32_t* lterm;      // [Gp][R] Log[len-1].Term: cached term of each replica's last entry
   int32_t* log_term;   // Log.Term  ring, tiles [Gp/64][KP][64][R] (ring_tile / ring_in_tile)
   int64_t* log_value;  // Log.Value ring
   uint32_t* log_crc;   // EXT: CRC32C stamp ring (payload_crc only)
@@ -108,16 +108,25 @@ __device__ __forceinline__ uint32_t ring_in_tile(uint32_t g, uint32_t R, uint32_
   return (slot * 64u + (g & 63u)) * R + r;
 }
 
-// Addressing: every access is a wave-uniform base (SGPRs: plane + replica
-// row, or replica ring) plus a 32-bit per-lane byte offset, so the compiler
-// emits global_load/store with an SGPR base and ONE shared VGPR offset
-// instead of a 64-bit VGPR address per (plane, replica). The byte offset
-// idx*sizeof(T) must fit 32 bits: raft_engine_create rejects Gp*4 >= 2^32
-// (per-group planes hold at most 4-B elements; ring offsets are taken inside
-// a KP*64*R tile, < 2^26 bytes).
+// Addressing: every access is a wave-uniform base (SGPRs: the plane, or a
+// ring tile) plus a 32-bit per-lane byte offset, so the compiler emits
+// global_load/store with an SGPR base and ONE shared VGPR offset instead of
+// a 64-bit VGPR address per (plane, replica). The byte offset idx*sizeof(T)
+// must fit 32 bits: raft_engine_create rejects Gp*R*4 >= 2^32 (per-replica
+// planes hold at most 4-B elements; ring offsets are taken inside a KP*64*R
+// tile, < 2^26 bytes).
 template <typename T>
-__device__ __forceinline__ T* prow(T* plane, int r, uint64_t Gp) {
+__device__ __forceinline__ T* prow(T* plane, int r, uint64_t Gp) {   // [..][Gp] row r (xmatch / xnext)
   return plane + uint64_t(r) * Gp;
+}
+// Per-replica scalar planes are group-major, [Gp][R]: replica r of group g
+// at element g*R + r. A group's R values are contiguous (28 B at R=7: one
+// line for the replica-parallel general kernel instead of R scattered
+// lines), and a lane's loads of one plane share one VGPR offset g*R*4 with
+// immediate offsets r*4. raft_engine_create keeps Gp*R*4 < 2^32.
+template <int R>
+__device__ __forceinline__ uint32_t rix(uint32_t g, int r) {
+  return g * uint32_t(R) + uint32_t(r);
 }
 template <typename T>
 __device__ __forceinline__ T& at(T* base, uint32_t idx) {
@@ -348,18 +357,18 @@ struct Group {
     hbt = at(P.hb, g);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      term[r] = at(prow(P.term, r, P.Gp), g);
-      last[r] = at(prow(P.last, r, P.Gp), g);
-      commit[r] = at(prow(P.commit, r, P.Gp), g);
-      const uint32_t x = at(prow(P.rs, r, P.Gp), g);
+      term[r] = at(P.term, rix<R>(g, r));
+      last[r] = at(P.last, rix<R>(g, r));
+      commit[r] = at(P.commit, rix<R>(g, r));
+      const uint32_t x = at(P.rs, rix<R>(g, r));
       roles |= (x & 3u) << (2 * r);
       votes |= ((x >> 2) & 15u) << (4 * r);
       dur[r] = int(x >> 6);
-      hw[r] = (SEM == SEM_RAFT) ? at(prow(P.hwm, r, P.Gp), g) : 0;
-      ltm[r] = at(prow(P.lterm, r, P.Gp), g);
+      hw[r] = (SEM == SEM_RAFT) ? at(P.hwm, rix<R>(g, r)) : 0;
+      ltm[r] = at(P.lterm, rix<R>(g, r));
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) dl[r] = with_deadlines ? eff_start(at(prow(P.tstart, r, P.Gp), g), r) + dur[r] : 0;
+    for (int r = 0; r < R; ++r) dl[r] = with_deadlines ? eff_start(at(P.tstart, rix<R>(g, r)), r) + dur[r] : 0;
     known = with_deadlines ? (1u << R) - 1u : 0u;
     // materialise the rows the fast kernel kept implicit: MatchIndex = LastApplied
     // (RAFT also NextIndex = LastApplied+1 and high-water mark = LastApplied)
@@ -385,17 +394,17 @@ struct Group {
   __device__ __forceinline__ void store(const DevPlanes& P, uint32_t next_phase) const {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      if ((d_term >> r) & 1u) at(prow(P.term, r, P.Gp), g) = term[r];
-      if ((d_last >> r) & 1u) at(prow(P.last, r, P.Gp), g) = last[r];
-      if ((d_commit >> r) & 1u) at(prow(P.commit, r, P.Gp), g) = commit[r];
-      if ((d_dl >> r) & 1u) at(prow(P.tstart, r, P.Gp), g) = dl[r] - dur[r];
+      if ((d_term >> r) & 1u) at(P.term, rix<R>(g, r)) = term[r];
+      if ((d_last >> r) & 1u) at(P.last, rix<R>(g, r)) = last[r];
+      if ((d_commit >> r) & 1u) at(P.commit, rix<R>(g, r)) = commit[r];
+      if ((d_dl >> r) & 1u) at(P.tstart, rix<R>(g, r)) = dl[r] - dur[r];
       if ((d_rs >> r) & 1u)
-        at(prow(P.rs, r, P.Gp), g) =
+        at(P.rs, rix<R>(g, r)) =
             uint16_t(((roles >> (2 * r)) & 3u) | (((votes >> (4 * r)) & 15u) << 2) | (uint32_t(dur[r]) << 6));
-      if (SEM == SEM_RAFT && ((d_hw >> r) & 1u)) at(prow(P.hwm, r, P.Gp), g) = hw[r];
-      if ((d_lt >> r) & 1u) at(prow(P.lterm, r, P.Gp), g) = ltm[r];
-      if ((d_pm >> r) & 1u) at(prow(P.lmatch, r, P.Gp), g) = pm[r];
-      if (SEM == SEM_RAFT && ((d_pn >> r) & 1u)) at(prow(P.lnext, r, P.Gp), g) = pn[r];
+      if (SEM == SEM_RAFT && ((d_hw >> r) & 1u)) at(P.hwm, rix<R>(g, r)) = hw[r];
+      if ((d_lt >> r) & 1u) at(P.lterm, rix<R>(g, r)) = ltm[r];
+      if ((d_pm >> r) & 1u) at(P.lmatch, rix<R>(g, r)) = pm[r];
+      if (SEM == SEM_RAFT && ((d_pn >> r) & 1u)) at(P.lnext, rix<R>(g, r)) = pn[r];
     }
     {   // logs still empty: pick the phase of the next tick's first entry (the fast kernel may append it)
       bool empty = true;
@@ -417,8 +426,8 @@ struct Group {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == nl) continue;
-        at(prow(P.lmatch, p, P.Gp), g) = at(prow(P.xmatch, nl * R + p, P.Gp), g);
-        if constexpr (SEM == SEM_RAFT) at(prow(P.lnext, p, P.Gp), g) = at(prow(P.xnext, nl * R + p, P.Gp), g);
+        at(P.lmatch, rix<R>(g, p)) = at(prow(P.xmatch, nl * R + p, P.Gp), g);
+        if constexpr (SEM == SEM_RAFT) at(P.lnext, rix<R>(g, p)) = at(prow(P.xnext, nl * R + p, P.Gp), g);
       }
       pri = nl;
     }
@@ -465,7 +474,7 @@ struct Group {
   template <int Rp>
   __device__ __forceinline__ int deadline_of(const DevPlanes& P) {
     if (!((known >> Rp) & 1u)) {
-      dl[Rp] = eff_start(at(prow(P.tstart, Rp, P.Gp), g), Rp) + dur[Rp];
+      dl[Rp] = eff_start(at(P.tstart, rix<R>(g, Rp)), Rp) + dur[Rp];
       known |= 1u << Rp;
     }
     return dl[Rp];
@@ -703,7 +712,7 @@ struct Group {
     if (primary == c) {
       if (!rows_m) {
 #pragma unroll
-        for (int p = 0; p < R; ++p) pm[p] = at(prow(P.lmatch, p, P.Gp), g);
+        for (int p = 0; p < R; ++p) pm[p] = at(P.lmatch, rix<R>(g, p));
         rows_m = 1;
       }
 #pragma unroll
@@ -718,7 +727,7 @@ struct Group {
       dirty &= ~(1u << c);
       if (!rows_m && dirty != (((1u << R) - 1u) & ~(1u << c))) {   // partial update: fetch the row first
 #pragma unroll
-        for (int p = 0; p < R; ++p) pm[p] = at(prow(P.lmatch, p, P.Gp), g);
+        for (int p = 0; p < R; ++p) pm[p] = at(P.lmatch, rix<R>(g, p));
       }
       rows_m = 1;
 #pragma unroll
@@ -951,7 +960,7 @@ struct Group {
     if (primary == c) {
       if (!rows_n) {
 #pragma unroll
-        for (int p = 0; p < R; ++p) pn[p] = at(prow(P.lnext, p, P.Gp), g);
+        for (int p = 0; p < R; ++p) pn[p] = at(P.lnext, rix<R>(g, p));
         rows_n = 1;
       }
 #pragma unroll
@@ -966,7 +975,7 @@ struct Group {
       dirty &= ~(1u << c);
       if (!rows_n && dirty != (((1u << R) - 1u) & ~(1u << c))) {
 #pragma unroll
-        for (int p = 0; p < R; ++p) pn[p] = at(prow(P.lnext, p, P.Gp), g);
+        for (int p = 0; p < R; ++p) pn[p] = at(P.lnext, rix<R>(g, p));
       }
       rows_n = 1;
 #pragma unroll

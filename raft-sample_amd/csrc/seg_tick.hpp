@@ -38,9 +38,8 @@ struct Seg {
   int me;          // replica id of this lane
   bool act;        // me < R
   int sb0l;        // first lane of this segment in the wave
-  uint32_t ri;     // element index of this replica's slot in the [R][Gp] planes: r*Gp + g
-                   // (r = 0 on idle lanes); the engine routes a config with R*Gp*4 >= 2^32
-                   // to the one-lane kernel, so at()'s 32-bit byte offsets hold
+  uint32_t ri;     // element index of this replica's slot in the [Gp][R] planes: g*R + r
+                   // (r = 0 on idle lanes); the R slots of a group are contiguous
   // ---- this replica's state (registers)
   int term, last, commit, dl, dur, hw, ltm, role, vote;
   int pm, pn;      // primary leader's MatchIndex / NextIndex for this replica (as its peer)
@@ -108,7 +107,7 @@ struct Seg {
     me = lane & (SEGW - 1);
     act = me < R;
     g = g_;
-    ri = uint32_t(act ? me : 0) * uint32_t(P.Gp) + g;
+    ri = rix<R>(g, act ? me : 0);
     key = group_key(T.seed, P.gbase + g);
     tick = T.tick;
     now = T.now;

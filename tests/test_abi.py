@@ -76,7 +76,7 @@ def test_missing_library_fails_loudly(tmp_path):
 
 
 @pytest.mark.parametrize("field,value,msg", [
-    ("groups", (1 << 30) - 255, "too many groups"),   # Gp*4 would wrap the 32-bit byte offsets
+    ("groups", (1 << 30) // 3 + 1, "too many groups"),   # Gp*R*4 would wrap the 32-bit byte offsets
     ("groups", 0, "groups must be"),
     ("replicas", 9, "replicas"),
     ("ring_depth", 24, "power of two"),
@@ -93,9 +93,9 @@ def test_engine_create_rejects_bad_configs_before_touching_a_gpu(field, value, m
 
 
 def test_largest_engine_size_is_accepted_by_validation():
-    """groups = 2^30 - 256 passes the size checks (then fails only for lack of a device here)."""
+    """groups * R = 2^30 - 256 * R passes the size checks (then fails only for lack of a device here)."""
     lib = engine.load_library()
-    c = abi.default_config(groups=(1 << 30) - 256)
+    c = abi.default_config(replicas=1, groups=(1 << 30) - 256)
     h = C.c_void_p()
     rc = lib.raft_engine_create(C.byref(c), C.byref(h))
     assert rc != abi.RAFT_EINVAL or "too many groups" not in lib.raft_last_error().decode()
