@@ -392,8 +392,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* wt = getenv("RAFTSTEP_WRITE_THROUGH")) e->write_through = atoi(wt) != 0;
   if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
   if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
-    if (rc == RAFT_OK) rc = dev_alloc(e, reinterpret_cast<void**>(&e->P.dbg), 16 * 8);
-    if (rc == RAFT_OK && hipMemset(e->P.dbg, 0, 16 * 8) != hipSuccess) rc = fail(RAFT_EHIP, "hipMemset failed");
+    if (rc == RAFT_OK) rc = dev_alloc(e, reinterpret_cast<void**>(&e->P.dbg), 32 * 8);
+    if (rc == RAFT_OK && hipMemset(e->P.dbg, 0, 32 * 8) != hipSuccess) rc = fail(RAFT_EHIP, "hipMemset failed");
     if (rc != RAFT_OK) {
       std::string keep = g_err;
       raft_engine_destroy(e);
@@ -769,16 +769,16 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     e->prof_n += nticks;
   }
   if (e->P.dbg) {   // diagnostics: fast-kernel lane classes summed over this call's ticks (synchronising)
-    unsigned long long d[16];
+    unsigned long long d[32];
     HIPCHK(hipMemcpyAsync(d, e->P.dbg, sizeof d, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemsetAsync(e->P.dbg, 0, sizeof d, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     fprintf(stderr,
             "raftstep: ticks %lld..%lld lanes %llu skip %llu bail %llu iso %llu drift<=K %llu drift>K %llu switch %llu "
             "blk_hi %llu blk_seg %llu coop %llu drifted %llu | bail: not-steady %llu iso-leader/multi %llu "
-            "follower-out-of-step %llu raft-rows %llu other %llu\n",
+            "follower-out-of-step %llu raft-rows %llu other %llu | quiet-leaderless %llu\n",
             (long long)first_tick, (long long)(first_tick + nticks - 1), d[10], d[0], d[1], d[2], d[3], d[4], d[5], d[6],
-            d[7], d[8], d[9], d[11], d[12], d[13], d[14], d[15]);
+            d[7], d[8], d[9], d[11], d[12], d[13], d[14], d[15], d[16]);
   }
   return RAFT_OK;
 }

@@ -88,6 +88,61 @@ __device__ __forceinline__ bool xi_ok(int meta, int xi) {
   return (meta & M_STEADY) || (RAFT && (meta & M_ONECAND) && xi >= 0);
 }
 
+// A group without a leader whose tick changes nothing: no timer expires
+// and the one candidate's vote round (if any) is refused by every peer it
+// reaches without a state change — the run_tick steps of such a tick are
+// client (no leader: nothing, main.go:327), rounds (CandidateRun's default
+// branch, main.go:253-284 -> 157-170 / RAFT r_deliver_vr) and timers
+// (main.go:171-177, 248-251), none of which fires. This is the common state
+// of a group between a disruption and its next election, so the tick is
+// taken here instead of deferring the group. Conservative: anything else
+// (a second candidate, a grant, a term to adopt, a timer due) defers.
+template <int R, bool RAFT>
+__device__ __forceinline__ bool quiet_leaderless(const DevPlanes& P, const Trace& T, uint32_t g, uint64_t key) {
+  if (R < 2) return false;   // a lone candidate would win its round
+  int term[R], last[R], lt[R], ts[R];
+  load_row<R>(P.term, g, term);
+  load_row<R>(P.last, g, last);
+  load_row<R>(P.lterm, g, lt);
+  load_row<R>(P.tstart, g, ts);
+  const int hb = at(P.hb, g);
+  int rs[R];   // role:2 | vote:4 | d:10
+#pragma unroll
+  for (int r = 0; r < R; ++r) rs[r] = at(P.rs, rix<R>(g, r));
+  int c = -1;
+  bool quiet = true;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int role = rs[r] & 3;
+    quiet &= role != ROLE_L;
+    if (role == ROLE_C) { quiet &= c < 0; c = r; }
+    // non-leaders' effective timer start counts the last heartbeat (Group::eff_start)
+    quiet &= max(ts[r], hb) + (rs[r] >> 6) > T.now;
+  }
+  if (!quiet || c < 0) return quiet;
+  const uint32_t im = T.iso_p ? isolation_mask<R>(key, T) : 0u;
+  const int ct = sel(term, c), cl = sel(last, c);
+  const int clt = cl > 0 ? sel(lt, c) : 0;
+  const uint32_t cvote = (uint32_t(sel(rs, c)) >> 2) & 15u;
+  if (!RAFT && cvote == 0u) return false;   // REF: the round would set the candidate's Voted
+#pragma unroll
+  for (int p = 0; p < R; ++p) {
+    if (p == c || (((im >> p) | (im >> c)) & 1u)) continue;   // dropped: never delivered
+    const int vote = (rs[p] >> 2) & 15;
+    if constexpr (RAFT) {
+      // r_deliver_vr: the peer already holds the candidate's term (nothing to
+      // adopt, no stop) and refuses: voted for another, or log more up to date
+      const int mt = last[p] > 0 ? lt[p] : 0;
+      const bool uptodate = clt > mt || (clt == mt && cl >= last[p]);
+      quiet &= term[p] == ct && !((vote == 0 || vote == c + 1) && uptodate);
+    } else {
+      // deliver_vr (main.go:160-162): a follower refuses without a change
+      quiet &= ct < term[p] || vote != 0;
+    }
+  }
+  return quiet;
+}
+
 template <int R, bool WT, bool CRC, int SEM>
 __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, unsigned long long* stats,
                                                         uint32_t* work, int32_t* work_tick, uint32_t* work_count,
@@ -124,9 +179,14 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
     // RAFT also takes ONECAND groups (their candidate must be isolated this tick, checked below)
     bail = !skip && (force_slow || !(meta & (RAFT ? (M_STEADY | M_ONECAND) : M_STEADY)));
+    if (bail && !force_slow && c == NO_PRIMARY) {   // leaderless: a quiet tick needs no general kernel
+      const bool q = quiet_leaderless<R, RAFT>(P, T, g, T.iso_p ? group_key(T.seed, P.gbase + g) : 0ull);
+      bail = !q;
+      df |= q ? 65536u : 0u;
+    }
     int term[R], last[R], commit[R], lt[R], m[R];
     bool empty = true;   // every log of the group empty before this tick
-    const bool go = !skip && !bail;
+    const bool go = !skip && !bail && c != NO_PRIMARY;
     df |= skip ? 1u : 0u;
     DIAG_REASON(df |= bail ? 2048u : 0u;);   // diagnostics: deferral reason "group not steady"
     if (go) {
@@ -490,7 +550,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     DIAG_REASON(if (bail && !(df & (2048u | 4096u | 8192u | 16384u))) df |= 32768u;);   // reason: anything later
     DIAG_REASON(if (!bail) df &= ~(2048u | 4096u | 8192u | 16384u););
 #pragma unroll 1
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < 17; ++k) {
       const uint64_t b = __ballot((df >> k) & 1u);
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
     }
