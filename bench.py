@@ -247,7 +247,7 @@ def main():
     avg_kernel_s = kernel_ms / 1e3 / max(kernel_launches, 1)    # steady-state kernel, kernel-exact
     avg_region_s = region_ms / 1e3 / max(region_launches, 1)    # all launches of a tick + gaps
     achieved = B * G / avg_kernel_s / 1e9
-    workload = f"{wl_key}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}"
+    workload = f"{wl_key}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}, K={K}"
     traffic, traffic_src = load_pmc(workload)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
