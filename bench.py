@@ -20,7 +20,7 @@ roofline's `achieved` uses the steady-state kernel's own average duration,
 measured by HIP events attached to each of its dispatches (profile mode 1)
 in a separate, untimed pass of K ticks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2|C3|C4|C4REF|C5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2|C3|C4|C4R|C4REF|C5]
 """
 import argparse
 import json
@@ -52,19 +52,25 @@ WORKLOADS = {
                desc="steady-state AppendEntries+commit, 2^21 groups per GPU (16M over 8 GPUs)"),
     "C5": dict(groups=1 << 20, entries=64, ring_depth=128, crc=1, seed=0x5EED0005,
                desc="64-entry AppendEntries batches with per-entry CRC32C stamp+verify"),
-    # C4: NewNode start, seeded isolation churn: per 32-tick epoch w.p. 1/8
-    # (~1/256 per tick) one replica of a group is cut off for 8-32 ticks;
-    # RAFT semantics (REF faults on a new leader's first contact, SURVEY KAT-11)
+    # C4: NewNode start, leader isolation: per 32-tick epoch
+    # w.p. 1/8 (~1/256 per tick) a window of 8-32 ticks cuts off the group's
+    # leader (the lowest-id Leader at the window's first tick); RAFT semantics
+    # (REF faults on a new leader's first contact, SURVEY KAT-11)
     "C4": dict(groups=1 << 22, replicas=7, entries=1, ring_depth=128, crc=0, init="new", semantics=1, settle=48,
-               iso=(8192, 8, 32), seed=0x5EED0004,
-               desc="NewNode start, isolation churn (elections, term bumps, truncation), RAFT semantics"),
-    # C4REF: the same trace in REF semantics (main.go bit for bit): the first
+               iso=(8192, 8, 32, 1), seed=0x5EED0004,
+               desc="NewNode start, leader-isolation churn (elections, step-downs, truncation), RAFT semantics"),
+    # C4R: the same with the isolated replica drawn from the trace hash (any
+    # replica; the leader 1 time in 7) -- round 1's C4 line
+    "C4R": dict(groups=1 << 22, replicas=7, entries=1, ring_depth=128, crc=0, init="new", semantics=1, settle=48,
+                iso=(8192, 8, 32, 0), seed=0x5EED0004,
+                desc="NewNode start, hashed-replica isolation churn, RAFT semantics"),
+    # C4REF: C4's trace in REF semantics (main.go bit for bit): the first
     # contact of a new leader panics (GetLog, main.go:142 -> 404) and the
     # group freezes, so this line reports throughput over the prefix and the
     # fault counts (SURVEY §8(d) "REF parity on prefix + fault codes")
     "C4REF": dict(groups=1 << 22, replicas=7, entries=1, ring_depth=128, crc=0, init="new", semantics=0, settle=48,
-                  iso=(8192, 8, 32), seed=0x5EED0004, allow_faults=True,
-                  desc="NewNode start, isolation churn, REF semantics (prefix; groups freeze on their first fault)"),
+                  iso=(8192, 8, 32, 1), seed=0x5EED0004, allow_faults=True,
+                  desc="NewNode start, leader-isolation churn, REF semantics (prefix; groups freeze on their first fault)"),
 }
 
 
@@ -102,7 +108,8 @@ def engine_kwargs(wl, R, G, base, K, E, crc):
     kw = dict(replicas=R, groups=G, group_base=base, ring_depth=K, entries_per_tick=E, client_period=1,
               payload_crc=crc, seed=wl["seed"], semantics=wl.get("semantics", 0))
     if "iso" in wl:
-        kw.update(isolate_per_65536=wl["iso"][0], isolate_min_ticks=wl["iso"][1], isolate_max_ticks=wl["iso"][2])
+        kw.update(isolate_per_65536=wl["iso"][0], isolate_min_ticks=wl["iso"][1], isolate_max_ticks=wl["iso"][2],
+                  isolate_leader=wl["iso"][3])
     return kw
 
 
@@ -185,15 +192,16 @@ def main():
     if dist is not None and not same_dev:
         from raftstep import dist as rdist
         eng.comm_init(world, rank, rdist.exchange_comm_id(dist, rank, Engine.comm_unique_id))
+    untimed = np.zeros(len(STAT_NAMES), np.int64)   # stats of the settle and warm-up ticks
     if churn:   # NewNode start; the first elections happen in untimed settle ticks
         eng.init_new_nodes(0)
-        eng.tick(0, wl["settle"], stats=False)
+        untimed += eng.tick(0, wl["settle"], stats=True)
         tick = wl["settle"]
     else:
         eng.init_steady(args.leader, 0)
         tick = 1
     if args.warmup:
-        eng.tick(tick, args.warmup, stats=True)
+        untimed += eng.tick(tick, args.warmup, stats=True)
         tick += args.warmup
 
     def barrier():
@@ -281,6 +289,11 @@ def main():
         "stats": dict(zip(STAT_NAMES, [int(x) for x in stats])),
         "stats_check": bool(ok),
     }
+    if wl.get("allow_faults"):   # REF prefix: groups frozen by a main.go panic / deadlock so far
+        fi = STAT_NAMES.index("faults")
+        result["faults_prefix"] = {"groups": G * world, "faulted_before_timed": int(untimed[fi]),
+                                   "faulted_in_timed": int(stats[fi]),
+                                   "frozen_fraction": (int(untimed[fi]) + int(stats[fi])) / (G * world)}
     if world > 1:
         from raftstep import dist as rdist
         ranks = [None] * world

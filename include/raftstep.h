@@ -131,6 +131,8 @@ typedef struct raft_state_view {
                          Optional on load: absent or 0 derives match+1 (REF ignores it) */
   int32_t* hwm;       /* [g*R + r] highest LastApplied ever (== last in REF); the ring holds (hwm-K, last].
                          Optional on load: absent or < last means last (REF ignores it) */
+  uint8_t* iso_victim;/* per group, EXT leader-isolation mode: victims of the windows in flight, one nibble
+                         per epoch parity (8 | replica, 0 = none). Optional on load (absent: 0) */
 } raft_state_view;
 
 typedef struct raft_engine raft_engine;

@@ -115,7 +115,7 @@ class Oracle:
         return st
 
     def load_state(self, st):
-        st = {k: np.ascontiguousarray(st[k]) for k in abi.STATE_FIELDS}
+        st = abi.coerce_state(st, self.cfg.groups, self.cfg.replicas, self.cfg.ring_depth)
         v = abi.make_view(st)
         _check(self.lib.oracle_load_state(self.h, C.byref(v)))
 

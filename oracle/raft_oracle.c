@@ -49,19 +49,27 @@ int32_t oracle_timer_draw(const raft_config* c, uint64_t gid, uint32_t replica, 
   int32_t mn = cand ? c->candidate_timeout_min : c->follower_timeout_min;
   return mn + (int32_t)((uint32_t)(h >> 32) % span);
 }
-/* EXT isolation windows: per 32-tick epoch, with probability p/65536 one
- * replica is cut off for [start, start+len) ticks (len <= 32). */
+/* EXT isolation windows: per 32-tick epoch e, with probability p/65536 one
+ * replica is cut off for [start, start+len) ticks (len <= 32). Returns 1 if
+ * epoch e has a window covering `tick`; *start and the hashed victim out. */
+static int iso_window(const raft_config* c, uint64_t gid, int64_t e, int64_t tick, int64_t* start,
+                      uint32_t* victim) {
+  uint64_t h = oracle_rng(c->seed, gid, 0, ST_ISOLATE, (uint64_t)e);
+  if ((h & 0xFFFF) >= c->isolate_per_65536) return 0;
+  *victim = (uint32_t)((h >> 16) & 0xFF) % c->replicas;
+  *start = e * 32 + (int64_t)((h >> 24) & 31);
+  uint32_t span = c->isolate_max_ticks - c->isolate_min_ticks + 1;
+  int64_t len = c->isolate_min_ticks + (int64_t)((uint32_t)(h >> 32) % span);
+  return tick >= *start && tick < *start + len;
+}
+/* Hashed-victim mode (isolate_leader = 0): is `replica` cut off at `tick`? */
 int oracle_isolated(const raft_config* c, uint64_t gid, uint32_t replica, int64_t tick) {
   if (c->isolate_per_65536 == 0 || tick < 0) return 0;
   int64_t ep = tick >> 5;
   for (int64_t e = ep; e >= ep - 1 && e >= 0; --e) {
-    uint64_t h = oracle_rng(c->seed, gid, 0, ST_ISOLATE, (uint64_t)e);
-    if ((h & 0xFFFF) >= c->isolate_per_65536) continue;
-    uint32_t victim = (uint32_t)((h >> 16) & 0xFF) % c->replicas;
-    int64_t start = e * 32 + (int64_t)((h >> 24) & 31);
-    uint32_t span = c->isolate_max_ticks - c->isolate_min_ticks + 1;
-    int64_t len = c->isolate_min_ticks + (int64_t)((uint32_t)(h >> 32) % span);
-    if (victim == replica && tick >= start && tick < start + len) return 1;
+    int64_t start;
+    uint32_t victim;
+    if (iso_window(c, gid, e, tick, &start, &victim) && victim == replica) return 1;
   }
   return 0;
 }
@@ -113,7 +121,34 @@ typedef struct {                                 /* Node (main.go:14-39) */
 typedef struct {
   o_node n[RAFT_MAX_REPLICAS];
   int fault;
+  uint8_t iso;   /* EXT leader-isolation mode: victim per epoch parity, nibble e&1 = 8|replica (0 = none) */
 } o_group;
+
+/* Replicas cut off at `tick` (bit r). Leader mode (isolate_leader): a
+ * window's victim is the lowest-id Leader when the window's first tick
+ * begins (decided then, with decide = 1, and recorded in G->iso); no leader
+ * then, nobody. */
+static uint32_t group_iso_mask(const raft_config* c, uint64_t gid, o_group* G, int64_t tick, int decide) {
+  if (c->isolate_per_65536 == 0 || tick < 0) return 0;
+  uint32_t mask = 0;
+  int64_t ep = tick >> 5;
+  for (int64_t e = ep; e >= ep - 1 && e >= 0; --e) {
+    int64_t start;
+    uint32_t victim;
+    if (!iso_window(c, gid, e, tick, &start, &victim)) continue;
+    if (!c->isolate_leader) { mask |= 1u << victim; continue; }
+    int sh = 4 * (int)(e & 1);
+    if (decide && tick == start) {
+      int v = -1;
+      for (uint32_t r = 0; r < c->replicas && v < 0; ++r)
+        if (G->n[r].role == RAFT_LEADER) v = (int)r;
+      G->iso = (uint8_t)((G->iso & ~(0xF << sh)) | ((v >= 0 ? 8 | v : 0) << sh));
+    }
+    int nib = (G->iso >> sh) & 0xF;
+    if (nib & 8) mask |= 1u << (nib & 7);
+  }
+  return mask;
+}
 
 struct oracle {
   raft_config cfg;
@@ -125,7 +160,7 @@ typedef struct {                                 /* one handler invocation's con
   uint64_t gid;
   int64_t tick, now;
   int64_t st[RAFT_NSTATS];
-  int drops;                                     /* EXT isolation active */
+  uint32_t iso;                                  /* EXT: replicas cut off this tick (bit r) */
 } o_ctx;
 
 typedef struct {                                 /* AppendEntriesRequest (main.go:289-296) */
@@ -271,11 +306,7 @@ static int deliver_vr(const o_ctx* c, o_group* G, int x, int64_t rterm, int64_t*
 }
 
 /* ------------------------------------------------------- node steps ----- */
-static int dropped(const o_ctx* c, int a, int b) {
-  if (!c->drops) return 0;
-  return oracle_isolated(c->cfg, c->gid, (uint32_t)a, c->tick) ||
-         oracle_isolated(c->cfg, c->gid, (uint32_t)b, c->tick);
-}
+static int dropped(const o_ctx* c, int a, int b) { return (int)(((c->iso >> a) | (c->iso >> b)) & 1u); }
 
 /* CandidateRun default branch (main.go:253-284). Returns 1 if elected. */
 static int candidate_round(o_ctx* c, o_group* G, int cand) {
@@ -558,6 +589,8 @@ static int is_raft(const o_ctx* c) { return c->cfg->semantics == RAFT_SEM_RAFT; 
 static void tick_group(o_ctx* c, o_group* G) {
   const int R = (int)c->cfg->replicas;
   if (G->fault) return;
+  /* 0. EXT isolation of this tick (leader mode: a window starting now takes the current leader) */
+  c->iso = group_iso_mask(c->cfg, c->gid, G, c->tick, 1);
   /* 1. client (main.go:87-93): every replica whose State is Leader */
   if (c->cfg->client_period && c->tick % c->cfg->client_period == 0) {
     for (int r = 0; r < R && !G->fault; ++r) {
@@ -621,7 +654,8 @@ static o_ctx make_ctx(const oracle* o, uint64_t g, int64_t tick) {
   c.gid = o->cfg.group_base + g;
   c.tick = tick;
   c.now = tick * o->cfg.tick_seconds;
-  c.drops = o->cfg.isolate_per_65536 != 0;
+  /* message-level handlers see the windows as they stand (no leader-mode decision) */
+  c.iso = group_iso_mask(&o->cfg, c.gid, &((oracle*)o)->g[g], tick, 0);
   return c;
 }
 
@@ -673,6 +707,7 @@ int oracle_load_state(oracle* o, const raft_state_view* v) {
     o_group* G = &o->g[g];
     memset(G, 0, sizeof(o_group));
     G->fault = v->fault[g];
+    G->iso = v->iso_victim ? v->iso_victim[g] : 0;
     for (uint32_t r = 0; r < R; ++r) {
       uint64_t i = g * R + r;
       o_node* n = &G->n[r];
@@ -715,6 +750,7 @@ void oracle_store_state(const oracle* o, raft_state_view* v) {
   for (uint64_t g = 0; g < o->cfg.groups; ++g) {
     const o_group* G = &o->g[g];
     if (v->fault) v->fault[g] = (uint8_t)G->fault;
+    if (v->iso_victim) v->iso_victim[g] = G->iso;
     for (uint32_t r = 0; r < R; ++r) {
       uint64_t i = g * R + r;
       const o_node* n = &G->n[r];
@@ -939,7 +975,8 @@ int oracle_nodelog(const oracle* o, uint64_t group, char* buf, size_t cap) {
  * shard-independent). Words, per replica r in order: role | voted<<8 | r<<16;
  * term | last<<32; commit | deadline<<32; timeout | hwm<<32; for each peer p:
  * match | next<<32; for each live log index i (max(1, hwm-K+1)..last):
- * term | i<<32, value, crc; then the group's fault code. */
+ * term | i<<32, value, crc; then the group's fault code, then (only when
+ * nonzero) 0x1500 | the leader-isolation victim byte. */
 static uint64_t dg_mix(uint64_t h, uint64_t w) { return sm64(h ^ w); }
 static uint64_t lo32(int64_t v) { return (uint64_t)(uint32_t)(int32_t)v; }
 void oracle_state_digest(const oracle* o, uint64_t* per_group, uint64_t* total) {
@@ -969,6 +1006,7 @@ void oracle_state_digest(const oracle* o, uint64_t* per_group, uint64_t* total) 
       }
     }
     h = dg_mix(h, (uint64_t)G->fault);
+    if (G->iso) h = dg_mix(h, 0x1500u | G->iso);   /* EXT leader-isolation victims (absent: digest unchanged) */
     if (per_group) per_group[g] = h;
     sum += h;
   }

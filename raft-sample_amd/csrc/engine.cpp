@@ -151,6 +151,7 @@ Trace make_trace(const raft_engine* e, int64_t tick) {
   T.iso_p = e->cfg.isolate_per_65536;
   T.iso_min = e->cfg.isolate_min_ticks;
   T.iso_span = e->cfg.isolate_max_ticks - e->cfg.isolate_min_ticks + 1;
+  T.iso_leader = e->cfg.isolate_leader;
   T.secs = e->cfg.tick_seconds;
   T.period = e->cfg.client_period;
   T.entries = e->cfg.entries_per_tick;
@@ -309,7 +310,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (c.isolate_per_65536 > 65536) return fail(RAFT_EINVAL, "isolate_per_65536 must be <= 65536");
   if (c.payload_crc > 1) return fail(RAFT_EINVAL, "payload_crc must be 0 or 1");
   if (c.corrupt_per_65536 > 65536) return fail(RAFT_EINVAL, "corrupt_per_65536 must be <= 65536");
-  if (c.isolate_leader != 0) return fail(RAFT_EINVAL, "isolate_leader is not supported by this build");
+  if (c.isolate_leader > 1) return fail(RAFT_EINVAL, "isolate_leader must be 0 or 1");
   if (c.isolate_per_65536 &&
       (c.isolate_min_ticks < 1 || c.isolate_max_ticks > 32 || c.isolate_min_ticks > c.isolate_max_ticks))
     return fail(RAFT_EINVAL, "isolation length must satisfy 1 <= min <= max <= 32");
@@ -349,6 +350,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.lmatch), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.xmatch), R * R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.gmeta), Gp * 2);
+  A(reinterpret_cast<void**>(&e->P.giso), Gp);
   A(reinterpret_cast<void**>(&e->P.grot), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.grota), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.gsb), Gp * 4);
@@ -415,6 +417,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(e->P.gmeta), uint16_t(NO_PRIMARY), Gp,
                                            e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.lterm, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.giso, 0, Gp, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grot, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grota, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gsb, 0, Gp * 4, e->stream) : z;
@@ -490,6 +493,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   const bool raft = e->cfg.semantics == RAFT_SEM_RAFT;
   std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt, ln, xn, hw;
   std::vector<uint16_t> rs, meta, rot, rota;
+  std::vector<uint8_t> giso;
   std::vector<int32_t> sb;
   std::vector<int64_t> lv;
   std::vector<uint32_t> lcrc;
@@ -503,6 +507,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!rc) rc = d2h(e, lm, e->P.lmatch, R * Gp);
   if (!rc) rc = d2h(e, xm, e->P.xmatch, R * R * Gp);
   if (!rc) rc = d2h(e, meta, e->P.gmeta, Gp);
+  if (!rc && v->iso_victim) rc = d2h(e, giso, e->P.giso, Gp);
   if (!rc && raft) rc = d2h(e, ln, e->P.lnext, R * Gp);
   if (!rc && raft) rc = d2h(e, xn, e->P.xnext, R * R * Gp);
   if (!rc && raft) rc = d2h(e, hw, e->P.hwm, R * Gp);
@@ -523,6 +528,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
     const int primary = meta[g] & 0xF;
     const bool msync = meta[g] & M_MSYNC;
     if (v->fault) v->fault[g] = uint8_t((meta[g] >> 4) & 0xF);
+    if (v->iso_victim) v->iso_victim[g] = giso[g];
     for (uint64_t r = 0; r < R; ++r) {
       const uint64_t d = g * R + r, c = g * R + r;   // per-replica planes are group-major (rix)
       const int role = rs[d] & 3;
@@ -592,6 +598,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
       xm(R * R * Gp, 0), lt(R * KP * Gp, 0), hb(Gp, HB_NONE);
   std::vector<uint16_t> rs(R * Gp, 0);
   std::vector<uint16_t> meta(Gp, uint16_t(NO_PRIMARY));
+  std::vector<uint8_t> giso(Gp, 0);
   std::vector<int64_t> lv(R * KP * Gp, 0);
   std::vector<int32_t> ltm(R * Gp, 0);
   std::vector<uint32_t> lcrc(e->cfg.payload_crc ? R * KP * Gp : 0, 0);
@@ -600,6 +607,15 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   const int max_vote = raft ? int(R) : 1;   // REF Voted bool; RAFT votedFor + 1
   for (uint64_t g = 0; g < G; ++g) {
     if (v->fault[g] > RAFT_F_OVERFLOW) return fail(RAFT_EINVAL, "group %llu: bad fault code", (unsigned long long)g);
+    if (v->iso_victim) {   // nibbles 0 or 8 | replica
+      const uint8_t x = v->iso_victim[g];
+      for (int sh = 0; sh < 8; sh += 4) {
+        const int nib = (x >> sh) & 0xF;
+        if (nib && (!(nib & 8) || uint32_t(nib & 7) >= R))
+          return fail(RAFT_EINVAL, "group %llu: bad iso_victim %#x", (unsigned long long)g, x);
+      }
+      giso[g] = x;
+    }
     int primary = NO_PRIMARY;
     for (uint64_t r = 0; r < R; ++r) {
       const uint64_t c = g * R + r;
@@ -671,6 +687,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.lmatch, lm);
   if (!rc) rc = h2d(e, e->P.xmatch, xm);
   if (!rc) rc = h2d(e, e->P.gmeta, meta);
+  if (!rc) rc = h2d(e, e->P.giso, giso);
   const std::vector<uint16_t> rot(Gp, 0);   // loaded rings: rotation 0, one segment
   const std::vector<int32_t> sb0(Gp, 0);
   if (!rc) rc = h2d(e, e->P.grot, rot);
@@ -1067,7 +1084,7 @@ uint32_t crc32c_update(uint32_t crc, const uint8_t* p, size_t n) {
 }
 
 constexpr char CKPT_MAGIC[8] = {'R', 'A', 'F', 'T', 'C', 'K', 'P', 'T'};
-constexpr uint32_t CKPT_VERSION = 1;
+constexpr uint32_t CKPT_VERSION = 2;   // 2: + iso_victim
 struct CkptHeader {
   char magic[8];
   uint32_t version, nfields;
@@ -1100,7 +1117,8 @@ std::vector<ViewField> view_fields(raft_state_view& v, uint64_t G, uint64_t R, u
           {"log_value", reinterpret_cast<void**>(&v.log_value), 8, G * R * K},
           {"log_crc", reinterpret_cast<void**>(&v.log_crc), 4, G * R * K},
           {"next", reinterpret_cast<void**>(&v.next), 4, G * R * R},
-          {"hwm", reinterpret_cast<void**>(&v.hwm), 4, G * R}};
+          {"hwm", reinterpret_cast<void**>(&v.hwm), 4, G * R},
+          {"iso_victim", reinterpret_cast<void**>(&v.iso_victim), 1, G}};
 }
 
 struct File {

@@ -120,7 +120,16 @@ __device__ __forceinline__ bool quiet_leaderless(const DevPlanes& P, const Trace
     quiet &= max(ts[r], hb) + (rs[r] >> 6) > T.now;
   }
   if (!quiet || c < 0) return quiet;
-  const uint32_t im = T.iso_p ? isolation_mask<R>(key, T) : 0u;
+  uint32_t im = 0;
+  if (T.iso_p) {
+    uint32_t act = 0, starting = 0;
+    im = iso_windows<R>(key, T, &act, &starting);
+    if (T.iso_leader) {   // a window starting now is decided (and recorded) by the general kernel
+      if (starting) return false;
+      uint32_t gi = act ? uint32_t(at(P.giso, g)) : 0u;
+      im = leader_iso_mask(act, 0u, gi, 0u, false);
+    }
+  }
   const int ct = sel(term, c), cl = sel(last, c);
   const int clt = cl > 0 ? sel(lt, c) : 0;
   const uint32_t cvote = (uint32_t(sel(rs, c)) >> 2) & 15u;
@@ -223,7 +232,13 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     // (MSYNC: MatchIndex[xi] == LastApplied[xi], both unchanged).
     int xi = -1;
     if (go && T.iso_p) {
-      const uint32_t im = isolation_mask<R>(key, T);
+      uint32_t act = 0, starting = 0;
+      uint32_t im = iso_windows<R>(key, T, &act, &starting);
+      if (T.iso_leader) {   // leader mode: a window starting now is decided by the general kernel
+        if (starting) bail = true;
+        uint32_t gi = act ? uint32_t(at(P.giso, g)) : 0u;
+        im = leader_iso_mask(act, 0u, gi, 0u, false);
+      }
       if (RAFT && R >= 3 && im && (im & (im - 1u)) == 0u && int(__builtin_ctz(im)) != c) xi = int(__builtin_ctz(im));
       else bail |= im != 0u;
       if (im) df |= 4u;

@@ -22,6 +22,7 @@ __global__ __launch_bounds__(256) void init_new_kernel(DevPlanes P, Trace T) {
   }
   P.hb[g] = HB_NONE;
   P.gmeta[g] = uint16_t(NO_PRIMARY);
+  P.giso[g] = 0;
   P.grot[g] = 0;   // empty logs: the phase is chosen at the first append
   P.grota[g] = 0;
   P.gsb[g] = 0;
@@ -55,6 +56,7 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
     }
   }
   P.hb[g] = HB_NONE;
+  P.giso[g] = 0;
   P.gmeta[g] = uint16_t(L | (P.hwm ? 0 : M_MSYNC) | M_STEADY);
   P.grot[g] = uint16_t(T.entries_before(T.tick + 1) & P.kmask);   // entry 1 lands in the global phase
   P.grota[g] = 0;
@@ -120,6 +122,8 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
       }
     }
     h = dg_mix(h, uint64_t(fault));
+    const uint32_t gi = at(P.giso, g);
+    if (gi) h = dg_mix(h, 0x1500u | gi);   // EXT leader-isolation victims (absent: digest unchanged)
     per_group[g] = h;
   }
   // wrapping 64-bit sum: two 32-bit halves through the shuffle tree

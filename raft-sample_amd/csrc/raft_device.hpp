@@ -58,6 +58,7 @@ struct DevPlanes {
   int32_t* xnext;      // RAFT mode: [R][R][Gp] NextIndex rows of further leaders
   int32_t* hwm;        // RAFT mode: [Gp][R] highest LastApplied ever (== last in REF)
   uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
+  uint8_t* giso;       // [Gp] EXT leader-isolation victims, nibble per epoch parity: 8 | replica (0 = none)
   uint16_t* grot;      // ring rotation of the current segment: entry idx >= gsb sits at slot (idx-1+grot) mod KP
   uint16_t* grota;     // rotation of the previous segment (entries idx < gsb)
   int32_t* gsb;        // first index of the current segment (0: one segment)
@@ -140,6 +141,7 @@ struct Trace {          // per-launch trace parameters (virtual clock + RNG)
   int32_t now;          // tick * tick_seconds
   int32_t f_min, f_span, c_min, c_span;
   uint32_t iso_p, iso_min, iso_span;
+  uint32_t iso_leader;  // EXT: a window isolates the lowest-id leader at its first tick
   int32_t secs;         // tick_seconds
   uint32_t period, entries;  // client event every `period` ticks, `entries` each
   __device__ __forceinline__ Trace at_tick(int64_t t) const {
@@ -279,6 +281,7 @@ struct Group {
   uint32_t d_term, d_last, d_commit, d_dl, d_rs, d_hw;
   int primary, fault, meta0, hbt;
   uint32_t iso;         // EXT: replicas isolated during this tick
+  uint32_t giso, giso0; // EXT leader-isolation victims (giso plane) now / as loaded
   uint32_t g;           // group index on this engine (lane)
   uint64_t key;
   int64_t tick;
@@ -337,6 +340,7 @@ struct Group {
     rot = rot0 = at(P.grot, g);
     rota = rota0 = at(P.grota, g);
     sb = sb0 = at(P.gsb, g);
+    giso = giso0 = at(P.giso, g);
   }
   // Per-tick reset of a group whose state stays resident across ticks
   // (general kernel catch-up): clock, counters, this tick's entry cache.
@@ -416,6 +420,7 @@ struct Group {
       if (rt != rot0) at(P.grot, g) = uint16_t(rt);
       if (sbn != sb0) at(P.gsb, g) = sbn;
       if (rota != rota0) at(P.grota, g) = uint16_t(rota);
+      if (giso != giso0) at(P.giso, g) = uint8_t(giso);
     }
     // The primary leader stepped down while another replica leads: move that
     // leader's rows into the coalesced primary planes so the group can take

@@ -54,6 +54,8 @@ struct Seg {
   int sbd;         // ring segment boundary (gsb)
   bool rot_dirty;  // rot / sbd changed (align_ring)
   uint32_t iso;
+  uint32_t giso;   // EXT leader-isolation victims (giso plane)
+  bool giso_dirty;
   int ecur;        // client entries appended to every leader this tick
   // per-tick statistics: S_COMMITTED in full, the others (each < 256 per
   // group and tick) packed 8 bits apiece, to keep the lane's registers down
@@ -122,6 +124,8 @@ struct Seg {
     rota = at(P.grota, g);
     sbd = at(P.gsb, g);
     rot_dirty = false;
+    giso = at(P.giso, g);
+    giso_dirty = false;
     dirty = 0;
   }
   __device__ __forceinline__ void load(const DevPlanes& P) {
@@ -200,6 +204,7 @@ struct Seg {
         at(P.gsb, g) = sbn;
       }
       if (m != meta0) at(P.gmeta, g) = uint16_t(m);
+      if (giso_dirty) at(P.giso, g) = uint8_t(giso);
     }
   }
 
@@ -748,7 +753,11 @@ struct Seg {
   // ================================================================ tick
   // run_tick (tick_common.hpp), segment-parallel.
   __device__ __forceinline__ void run(const DevPlanes& P, const Trace& T, uint32_t E) {
-    if (T.iso_p) iso = isolation_mask<R>(key, T);
+    if (T.iso_p) {
+      const uint32_t g0 = giso;
+      iso = tick_iso_mask<R>(key, T, giso, mask(act && role == ROLE_L), true);
+      giso_dirty |= giso != g0;
+    }
     ecur = int(E);
     if (E) client_append(P, T, E);
     // 2. rounds in ascending replica id, against the roles as they are now

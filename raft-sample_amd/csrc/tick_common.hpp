@@ -10,10 +10,14 @@
 
 namespace raftstep {
 
-// EXT isolation windows (same definition as oracle_isolated()).
+// EXT isolation windows (same definition as the oracle's iso_window()): per
+// 32-tick epoch e, with probability iso_p/65536, one replica is cut off for
+// [start, start+len). Bit (e&1) of *active: epoch e's window covers T.tick;
+// of *starting: T.tick is its first tick. Returns the hashed victims.
 template <int R>
-__device__ __forceinline__ uint32_t isolation_mask(uint64_t key, const Trace& T) {
+__device__ __forceinline__ uint32_t iso_windows(uint64_t key, const Trace& T, uint32_t* active, uint32_t* starting) {
   uint32_t mask = 0;
+  *active = *starting = 0;
   const int64_t ep = T.tick >> 5;
   for (int64_t e = ep; e >= ep - 1 && e >= 0; --e) {
     const uint64_t h = rng_k(key, 0, ST_ISOLATE, uint64_t(e));
@@ -21,9 +25,46 @@ __device__ __forceinline__ uint32_t isolation_mask(uint64_t key, const Trace& T)
     const uint32_t victim = uint32_t((h >> 16) & 0xFF) % uint32_t(R);
     const int64_t start = e * 32 + int64_t((h >> 24) & 31);
     const int64_t len = int64_t(T.iso_min) + int64_t(uint32_t(h >> 32) % T.iso_span);
-    if (T.tick >= start && T.tick < start + len) mask |= 1u << victim;
+    if (T.tick >= start && T.tick < start + len) {
+      mask |= 1u << victim;
+      *active |= 1u << (e & 1);
+      *starting |= (T.tick == start ? 1u : 0u) << (e & 1);
+    }
   }
   return mask;
+}
+// Hashed-victim mode: the replicas cut off this tick.
+template <int R>
+__device__ __forceinline__ uint32_t isolation_mask(uint64_t key, const Trace& T) {
+  uint32_t a, s;
+  return iso_windows<R>(key, T, &a, &s);
+}
+// Leader mode (isolate_leader, oracle group_iso_mask): a window's victim is
+// the lowest-id Leader when its first tick begins (`leaders`: bit r = replica
+// r is a Leader), recorded in giso (nibble per epoch parity); no leader then,
+// nobody. decide = false (message-level handlers, the steady-state kernel)
+// only reads what was recorded.
+__device__ __forceinline__ uint32_t leader_iso_mask(uint32_t active, uint32_t starting, uint32_t& giso, uint32_t leaders,
+                                                    bool decide) {
+  uint32_t mask = 0;
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    if (!((active >> par) & 1u)) continue;
+    const int sh = 4 * par;
+    if (decide && ((starting >> par) & 1u))
+      giso = (giso & ~(0xFu << sh)) | ((leaders ? (8u | uint32_t(__builtin_ctz(leaders))) : 0u) << sh);
+    const uint32_t nib = (giso >> sh) & 0xFu;
+    if (nib & 8u) mask |= 1u << (nib & 7u);
+  }
+  return mask;
+}
+// The replicas cut off this tick, either mode (Group / general kernels).
+template <int R>
+__device__ __forceinline__ uint32_t tick_iso_mask(uint64_t key, const Trace& T, uint32_t& giso, uint32_t leaders,
+                                                  bool decide) {
+  uint32_t a, s;
+  const uint32_t hashed = iso_windows<R>(key, T, &a, &s);
+  return T.iso_leader ? leader_iso_mask(a, s, giso, leaders, decide) : hashed;
 }
 
 // Sum of one small per-lane counter over the wave. Counters are almost
@@ -42,9 +83,16 @@ __device__ __forceinline__ long long wave_sum(int v) {
   return x;
 }
 
+// Leaders of a Group as a replica bit mask (roles: 2 bits per replica).
+__device__ __forceinline__ uint32_t leader_bits(uint32_t roles, int R) {
+  uint32_t m = 0;
+  for (int r = 0; r < R; ++r) m |= (((roles >> (2 * r)) & 3u) == uint32_t(ROLE_L) ? 1u : 0u) << r;
+  return m;
+}
+
 template <int R, int SEM>
 __device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, const Trace& T, uint32_t E) {
-  if (T.iso_p) G.iso = isolation_mask<R>(G.key, T);
+  if (T.iso_p) G.iso = tick_iso_mask<R>(G.key, T, G.giso, leader_bits(G.roles, R), true);
 
   // 1. client: every Leader receives E NewLogRequests (main.go:87-93 -> 327-329).
   if (E) {

@@ -82,12 +82,12 @@ class StateView(C.Structure):
         ("last", C.c_void_p), ("commit", C.c_void_p), ("deadline", C.c_void_p),
         ("timeout", C.c_void_p), ("match", C.c_void_p), ("fault", C.c_void_p),
         ("log_term", C.c_void_p), ("log_value", C.c_void_p), ("log_crc", C.c_void_p),
-        ("next", C.c_void_p), ("hwm", C.c_void_p),
+        ("next", C.c_void_p), ("hwm", C.c_void_p), ("iso_victim", C.c_void_p),
     ]
 
 
 STATE_FIELDS = ("role", "voted", "term", "last", "commit", "deadline", "timeout",
-                "match", "fault", "log_term", "log_value", "log_crc", "next", "hwm")
+                "match", "fault", "log_term", "log_value", "log_crc", "next", "hwm", "iso_victim")
 
 
 def state_shapes(groups, replicas, ring_depth):
@@ -100,6 +100,7 @@ def state_shapes(groups, replicas, ring_depth):
         "fault": ((G,), np.uint8), "log_term": ((G, R, K), np.int32),
         "log_value": ((G, R, K), np.int64), "log_crc": ((G, R, K), np.uint32),
         "next": ((G, R, R), np.int32), "hwm": ((G, R), np.int32),
+        "iso_victim": ((G,), np.uint8),
     }
 
 
@@ -107,7 +108,7 @@ def empty_state(groups, replicas, ring_depth):
     return {k: np.zeros(s, d) for k, (s, d) in state_shapes(groups, replicas, ring_depth).items()}
 
 
-OPTIONAL_ON_LOAD = ("log_crc", "next", "hwm")   # raft_load_state: NULL derives them (raftstep.h)
+OPTIONAL_ON_LOAD = ("log_crc", "next", "hwm", "iso_victim")   # raft_load_state: NULL derives them (raftstep.h)
 
 
 def coerce_state(state, groups, replicas, ring_depth):

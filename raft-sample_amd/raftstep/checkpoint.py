@@ -18,8 +18,9 @@ import numpy as np
 from . import abi
 
 MAGIC = b"RAFTCKPT"
-VERSION = 1
-_DTYPES = {"role": np.uint8, "voted": np.uint8, "fault": np.uint8, "log_value": np.int64, "log_crc": np.uint32}
+VERSION = 2
+_DTYPES = {"role": np.uint8, "voted": np.uint8, "fault": np.uint8, "log_value": np.int64, "log_crc": np.uint32,
+           "iso_victim": np.uint8}
 
 
 def read(path):

@@ -88,7 +88,8 @@ def state_hash(st):
 
 def group_hashes(st, raft_fields=False):
     """Per-group digest (uint64) of every field — for per-tick trace diffs
-    (log_crc only when present and non-zero, i.e. with payload_crc on;
+    (log_crc / iso_victim only when present and non-zero, i.e. with
+    payload_crc / leader-isolation mode on;
     next/hwm only with raft_fields: in REF mode they are derived from
     match/last, and the committed golden digests predate them)."""
     G = st["fault"].shape[0]
@@ -98,7 +99,7 @@ def group_hashes(st, raft_fields=False):
         for k in abi.STATE_FIELDS:
             if k in ("next", "hwm") and not raft_fields:
                 continue
-            if k not in st or (k == "log_crc" and not st[k].any()):
+            if k not in st or (k in ("log_crc", "iso_victim") and not st[k].any()):
                 continue
             a = np.ascontiguousarray(st[k]).reshape(G, -1).astype(np.int64).view(np.uint64)
             for j in range(a.shape[1]):

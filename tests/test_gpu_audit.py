@@ -40,6 +40,9 @@ DIGEST_CASES = {
     "raft_churn_r7": (dict(replicas=7, groups=1024, client_period=1, ring_depth=64, semantics=abi.SEM_RAFT,
                            seed=0x44, isolate_per_65536=20000, isolate_min_ticks=4, isolate_max_ticks=32),
                       "new", 0, 200),
+    "raft_leader_iso_r7": (dict(replicas=7, groups=1024, client_period=1, ring_depth=64, semantics=abi.SEM_RAFT,
+                                seed=0x45, isolate_per_65536=20000, isolate_min_ticks=4, isolate_max_ticks=32,
+                                isolate_leader=1), "new", 0, 200),
     "crc_e16_r5": (dict(replicas=5, groups=512, client_period=1, entries_per_tick=16, ring_depth=64, payload_crc=1,
                         corrupt_per_65536=3000, seed=0x5EED0005), "steady", 1, 20),
 }

@@ -92,6 +92,12 @@ TRACES = {
     "crc_newnode_iso": (dict(replicas=3, groups=300, client_period=1, entries_per_tick=2, ring_depth=16,
                              payload_crc=1, corrupt_per_65536=5000, isolate_per_65536=12000,
                              seed=0xC5C), "new", 0, 150, 5),
+    # EXT leader-isolation mode: the window's victim is the leader at its first tick
+    "leader_iso_r3": (dict(replicas=3, groups=400, client_period=1, seed=0x5EED0014, isolate_per_65536=20000,
+                           isolate_leader=1), "new", 0, 240, 8),
+    "leader_iso_steady_r5": (dict(replicas=5, groups=500, client_period=1, ring_depth=16, seed=0x5EED0015,
+                                  isolate_per_65536=30000, isolate_min_ticks=4, isolate_max_ticks=24,
+                                  isolate_leader=1), "steady0", 1, 200, 5),
     "r1": (dict(replicas=1, groups=64, client_period=1, seed=1), "new", 0, 60, 5),
     "r2": (dict(replicas=2, groups=64, client_period=1, seed=2), "new", 0, 60, 5),
     "r4": (dict(replicas=4, groups=300, client_period=1, seed=4), "new", 0, 120, 5),

@@ -128,6 +128,13 @@ TRACES = {
     "raft_c4_shape": (dict(replicas=7, groups=2048, client_period=1, seed=0x5EED0002, ring_depth=64,
                            isolate_per_65536=8192, isolate_min_ticks=8, isolate_max_ticks=32),
                       "new", 0, 400, 25),
+    # SURVEY §8(d) C4 as specified: leader isolation (isolate_leader), at 2048 groups
+    "raft_c4_leader_iso": (dict(replicas=7, groups=2048, client_period=1, seed=0x5EED0004, ring_depth=64,
+                                isolate_per_65536=8192, isolate_min_ticks=8, isolate_max_ticks=32,
+                                isolate_leader=1), "new", 0, 400, 25),
+    "raft_leader_iso_r5_dense": (dict(replicas=5, groups=600, client_period=1, seed=0x1EAD, ring_depth=64,
+                                      isolate_per_65536=40000, isolate_min_ticks=4, isolate_max_ticks=32,
+                                      isolate_leader=1), "new", 0, 300, 10),
     "raft_r1": (dict(replicas=1, groups=64, client_period=1, seed=1), "new", 0, 60, 5),
     "raft_r2": (dict(replicas=2, groups=64, client_period=1, seed=2, isolate_per_65536=9000), "new", 0, 80, 5),
     "raft_r4": (dict(replicas=4, groups=300, client_period=1, seed=4, isolate_per_65536=9000), "new", 0, 120, 5),
