@@ -793,9 +793,9 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     fprintf(stderr,
             "raftstep: ticks %lld..%lld lanes %llu skip %llu bail %llu iso %llu drift<=K %llu drift>K %llu switch %llu "
             "blk_hi %llu blk_seg %llu coop %llu drifted %llu | bail: not-steady %llu iso-leader/multi %llu "
-            "follower-out-of-step %llu raft-rows %llu other %llu | quiet-leaderless %llu\n",
+            "follower-out-of-step %llu raft-rows %llu other %llu | quiet-leaderless %llu isolated-leader %llu\n",
             (long long)first_tick, (long long)(first_tick + nticks - 1), d[10], d[0], d[1], d[2], d[3], d[4], d[5], d[6],
-            d[7], d[8], d[9], d[11], d[12], d[13], d[14], d[15], d[16]);
+            d[7], d[8], d[9], d[11], d[12], d[13], d[14], d[15], d[16], d[17]);
   }
   return RAFT_OK;
 }

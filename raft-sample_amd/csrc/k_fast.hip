@@ -231,6 +231,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     // runs its own election timer. Its lagging MatchIndex stays implicit
     // (MSYNC: MatchIndex[xi] == LastApplied[xi], both unchanged).
     int xi = -1;
+    bool lx = false;   // RAFT: the primary leader is the one isolated replica (see below)
     if (go && T.iso_p) {
       uint32_t act = 0, starting = 0;
       uint32_t im = iso_windows<R>(key, T, &act, &starting);
@@ -240,6 +241,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         im = leader_iso_mask(act, 0u, gi, 0u, false);
       }
       if (RAFT && R >= 3 && im && (im & (im - 1u)) == 0u && int(__builtin_ctz(im)) != c) xi = int(__builtin_ctz(im));
+      else if (RAFT && R >= 3 && im == (1u << c) && (meta & M_STEADY)) lx = true;
       else bail |= im != 0u;
       if (im) df |= 4u;
     }
@@ -247,8 +249,66 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     if (go && !xi_ok<RAFT>(meta, xi)) bail = true;   // ONECAND needs its candidate isolated (role checked below)
     // leader view
     const int Lt = sel(term, c), Ll = sel(last, c), Lc = sel(commit, c), Llt = sel(lt, c);
-    if (go && !bail) bail = int64_t(Ll) + n > I32MAX || n >= int(P.K);
-    if (go) {
+    // RAFT: the leader itself cut off (leader isolation), every other replica
+    // a follower waiting for it. The tick is: the leader appends this tick's
+    // entries to its own log (client, main.go:327-329), every AppendEntries
+    // it sends is dropped (EXT: the sender sees a failure), the commit rule
+    // runs over unchanged MatchIndex values, and nobody's timer is reset; it
+    // is taken here while no follower's timer is due (that would start an
+    // election). MatchIndex must equal LastApplied for every follower (RAFT
+    // rows were checked against NextIndex / high-water marks above); both
+    // stand still, so the rows become implicit (MSYNC).
+    if (go && !bail && lx) {
+      bail = int64_t(Ll) + n > I32MAX || n >= int(P.K) || Ll == 0;
+#pragma unroll
+      for (int p = 0; p < R; ++p) bail |= p != c && m[p] != last[p];
+      int ts[R], rsv[R];
+      load_row<R>(P.tstart, g, ts);
+      const int hbt = at(P.hb, g);
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        rsv[p] = at(P.rs, rix<R>(g, p));
+        if (p != c) bail |= max(ts[p], hbt) + (rsv[p] >> 6) <= T.now;   // a follower's election timeout is due
+      }
+      // commitIndex: the largest N held by a majority (leader included), if
+      // log[N].term == currentTerm (Group::r_commit_rule); MatchIndex = LastApplied (MSYNC)
+      int N = -1;
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        const int vp = p == c ? Ll + n : last[p];
+        int cnt = 0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) cnt += (q == c ? Ll + n : last[q]) >= vp ? 1 : 0;
+        if (cnt >= R / 2 + 1 && vp > N) N = vp;
+      }
+      int cm = Lc;
+      if (N > Lc) {
+        if (N == Ll + n && n > 0) cm = N;                 // this tick's entries: current term
+        else if (N == Ll) cm = Llt == Lt ? N : Lc;        // the cached last-entry term
+        else bail = true;                                 // would need a ring read: general path
+      }
+      if (!bail) {
+        df |= 131072u;
+        sv[0] = cm - Lc;
+        sv[1] = 0;
+        sv[2] = R - 1;                                    // every AppendEntries dropped
+        sv[3] = 1;
+        sv[4] = 0;
+        if (n) {
+          st<WT>(P.last, rix<R>(g, c), Ll + n);
+          if (Llt != Lt) st<WT>(P.lterm, rix<R>(g, c), Lt);
+          wr = 1u << c;                                   // only the leader's log grows
+          w_term = Lt;
+          w_ph = int((uint32_t(Ll) + uint32_t(at(P.grot, g))) & P.kmask);
+          w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+        }
+        if (cm != Lc) st<WT>(P.commit, rix<R>(g, c), cm);
+        if (!(meta & M_MSYNC)) at(P.gmeta, g) = uint16_t(meta | M_MSYNC);
+      }
+    }
+    const bool gom = go && !lx;   // the main steady-state path
+    if (gom && !bail) bail = int64_t(Ll) + n > I32MAX || n >= int(P.K);
+    if (gom) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == xi) { bail |= m[p] != last[p] || m[p] > Ll; continue; }   // MSYNC stays exact for xi
@@ -261,7 +321,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     // the isolated replica's own state: role, vote, timer (eff. start = max(tstart, hb))
     int x_rs = 0, x_term = 0, x_fire = 0, x_dur = 0;
     if constexpr (RAFT) {
-      if (go && !bail && xi >= 0) {
+      if (gom && !bail && xi >= 0) {
         x_rs = at(P.rs, rix<R>(g, xi));
         x_term = sel(term, xi);
         const int role = x_rs & 3;
@@ -285,7 +345,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     // (the term's CRC state is shared, the term bytes are never corrupted)
     uint32_t crcbad = 0;
     if constexpr (CRC) {
-      if (go && !bail && n) {
+      if (gom && !bail && n) {
         uint32_t cm = 0;   // followers whose message is corrupted this tick
 #pragma unroll
         for (int p = 0; p < R; ++p)
@@ -307,7 +367,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       }
     }
     uint32_t okm = 0, cch = 0, mch = 0, ltch = 0;
-    if (go && !bail) {
+    if (gom && !bail) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == c || p == xi) continue;   // xi: dropped (sender sees false, receiver unchanged)
@@ -343,7 +403,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         }
       }
     }
-    if (go && !bail) {
+    if (gom && !bail) {
       int cm = Lc;
       bool sync = true;
       if constexpr (RAFT) {
@@ -565,7 +625,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     DIAG_REASON(if (bail && !(df & (2048u | 4096u | 8192u | 16384u))) df |= 32768u;);   // reason: anything later
     DIAG_REASON(if (!bail) df &= ~(2048u | 4096u | 8192u | 16384u););
 #pragma unroll 1
-    for (int k = 0; k < 17; ++k) {
+    for (int k = 0; k < 18; ++k) {
       const uint64_t b = __ballot((df >> k) & 1u);
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
     }
