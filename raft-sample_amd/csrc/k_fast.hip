@@ -85,7 +85,7 @@ __device__ __forceinline__ void store_row(int32_t* plane, uint32_t g, const int 
 // role, which must be the candidate, is checked once the rs row is read).
 template <bool RAFT>
 __device__ __forceinline__ bool xi_ok(int meta, int xi) {
-  return (meta & M_STEADY) || (RAFT && (meta & M_ONECAND) && xi >= 0);
+  return (meta & M_STEADY) || (RAFT && (meta & (M_ONECAND | M_ONESTALE)) && xi >= 0);
 }
 
 // A group without a leader whose tick changes nothing: no timer expires
@@ -187,13 +187,14 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     const int c = meta & 0xF;
     const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
     // RAFT also takes ONECAND groups (their candidate must be isolated this tick, checked below)
-    bail = !skip && (force_slow || !(meta & (RAFT ? (M_STEADY | M_ONECAND) : M_STEADY)));
+    bail = !skip && (force_slow || !(meta & (RAFT ? (M_STEADY | M_ONECAND | M_ONESTALE) : M_STEADY)));
     if (bail && !force_slow && c == NO_PRIMARY) {   // leaderless: a quiet tick needs no general kernel
       const bool q = quiet_leaderless<R, RAFT>(P, T, g, T.iso_p ? group_key(T.seed, P.gbase + g) : 0ull);
       bail = !q;
       df |= q ? 65536u : 0u;
     }
     int term[R], last[R], commit[R], lt[R], m[R];
+    uint32_t rowbad = 0;   // RAFT explicit rows out of step (replica bits)
     bool empty = true;   // every log of the group empty before this tick
     const bool go = !skip && !bail && c != NO_PRIMARY;
     df |= skip ? 1u : 0u;
@@ -216,12 +217,14 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
           // log may be shorter than its high-water mark (no pending truncation)
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            if (r != c) bail |= at(P.lnext, rix<R>(g, r)) != m[r] + 1;
-            bail |= at(P.hwm, rix<R>(g, r)) != last[r];
+            if (r != c && at(P.lnext, rix<R>(g, r)) != m[r] + 1) rowbad |= 1u << r;
+            if (at(P.hwm, rix<R>(g, r)) != last[r]) rowbad |= 1u << r;
           }
         }
       }
     }
+    // ONESTALE: the stale leader's row is its own (checked below, once it is known)
+    if (!RAFT || !(meta & M_ONESTALE)) bail |= rowbad != 0u;
     DIAG_REASON(if (bail && !(df & 2048u)) df |= 16384u;);   // reason: explicit RAFT rows out of step
     uint64_t key = 0;
     if (go && (T.iso_p || n)) key = group_key(T.seed, P.gbase + g);
@@ -247,6 +250,14 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     }
     DIAG_REASON(if (bail && !(df & (2048u | 16384u))) df |= 4096u;);   // reason: leader or >1 replica isolated
     if (go && !xi_ok<RAFT>(meta, xi)) bail = true;   // ONECAND needs its candidate isolated (role checked below)
+    // RAFT ONESTALE: the one non-follower besides the primary is a leader of a
+    // lower term, cut off this tick (xi). It appends this tick's client entries
+    // to its own log and every AppendEntries it sends is dropped; its commit
+    // rule cannot move (its MatchIndex row has not changed since it was cut
+    // off and its own log only grows past it). Its row in the primary's
+    // planes stays explicit, so the group keeps explicit rows (no MSYNC).
+    const bool stale = RAFT && (meta & M_ONESTALE) && xi >= 0;
+    if (RAFT && (meta & M_ONESTALE)) bail |= (rowbad & ~(stale ? 1u << xi : 0u)) != 0u;
     // leader view
     const int Lt = sel(term, c), Ll = sel(last, c), Lc = sel(commit, c), Llt = sel(lt, c);
     // RAFT: the leader itself cut off (leader isolation), every other replica
@@ -311,7 +322,10 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     if (gom) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
-        if (p == xi) { bail |= m[p] != last[p] || m[p] > Ll; continue; }   // MSYNC stays exact for xi
+        if (p == xi) {   // MSYNC stays exact for an isolated follower / candidate
+          if (!stale) bail |= m[p] != last[p] || m[p] > Ll;
+          continue;
+        }
         bail |= (p != c) && m[p] != Ll;
         // RAFT: a follower with extra entries or another term takes the general path
         if constexpr (RAFT) bail |= (p != c) && (last[p] != Ll || term[p] != Lt);
@@ -325,10 +339,13 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         x_rs = at(P.rs, rix<R>(g, xi));
         x_term = sel(term, xi);
         const int role = x_rs & 3;
-        // STEADY: xi is a follower; ONECAND: xi is the group's one candidate
-        if (role != ((meta & M_STEADY) ? ROLE_F : ROLE_C)) bail = true;
+        // STEADY: xi is a follower; ONECAND: the group's one candidate; ONESTALE: the stale leader
+        if (role != ((meta & M_STEADY) ? ROLE_F : stale ? ROLE_L : ROLE_C)) bail = true;
+        // (the stale leader appends at its own log's end with the ring rotation as it stands:
+        // an empty group would pick a new phase, see below)
+        if (stale && (x_term >= Lt || int64_t(sel(last, xi)) + n > I32MAX || empty)) bail = true;
         const int dl = max(at(P.tstart, rix<R>(g, xi)), at(P.hb, g)) + (x_rs >> 6);
-        if (dl <= T.now) {   // timer.C: Term++, vote for itself, new candidate timer (Raft §5.2)
+        if (!stale && dl <= T.now) {   // timer.C: Term++, vote for itself, new candidate timer (Raft §5.2)
           if (x_term >= I32MAX) bail = true;
           x_fire = 1;
           x_dur = T.c_min + int(uint32_t(rng_k(key, uint32_t(xi), ST_TIMER_C, uint64_t(T.tick)) >> 32) %
@@ -405,7 +422,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     }
     if (gom && !bail) {
       int cm = Lc;
-      bool sync = true;
+      bool sync = !stale;   // ONESTALE: the stale leader's row is explicit
       if constexpr (RAFT) {
         // every log now ends at Ll+n (all but at most one lagging isolated
         // replica, and R >= 3): the majority index is Ll+n, committed only if
@@ -425,7 +442,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       }
       sv[0] = cm - Lc;
       sv[1] = __builtin_popcount(okm);
-      sv[2] = (R - 1) - sv[1];
+      sv[2] = (R - 1) - sv[1] + (stale ? R - 1 : 0);   // + every AppendEntries of the cut-off stale leader
       sv[3] = 1;
       sv[4] = x_fire;
       // ---- stores (no bail past this point) ----
@@ -460,8 +477,33 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         if (((cch >> p) & 1u) && !commit_row) st<WT>(P.commit, rix<R>(g, p), commit[p]);
         if ((ltch >> p) & 1u) st<WT>(P.lterm, rix<R>(g, p), Lt);
         if (!RAFT && term[p] != Lt) st<WT>(P.term, rix<R>(g, p), Lt);  // main.go:155
+        if (RAFT && !sync && ((mch >> p) & 1u)) st<WT>(P.lnext, rix<R>(g, p), m[p] + 1);   // NextIndex explicit too
+        if (RAFT && !sync && n) st<WT>(P.hwm, rix<R>(g, p), last[p]);                      // high-water mark = new length
       }
       if constexpr (RAFT) {
+        if (stale) {
+          if (n) st<WT>(P.hwm, rix<R>(g, c), Ll + n);
+          // the stale leader's own client append (main.go:327-329) at its own log's end
+          const int xl = sel(last, xi);
+          if (n) {
+            const uint64_t xvb = rng_k(key, uint32_t(xi), ST_VALUE, uint64_t(T.tick));
+            const uint64_t tb = ring_tile(g, P.KP, R);
+            const uint32_t xrot = at(P.grot, g), xrota = at(P.grota, g);
+            const int xsb = at(P.gsb, g);
+            uint32_t cs = 0;
+            if constexpr (CRC) cs = crc_term_state(tab, x_term);
+            for (int e = 0; e < n; ++e) {
+              const int64_t v = int64_t(sm64(xvb ^ uint64_t(uint32_t(e))) >> 1);
+              const uint32_t o = ring_in_tile(g, R, ring_slot(xl + 1 + e, xrot, xrota, xsb, P.kmask), uint32_t(xi));
+              st<WT>(P.log_term + tb, o, x_term);
+              st<WT>(P.log_value + tb, o, v);
+              if constexpr (CRC) st<WT>(P.log_crc + tb, o, crc_value_final(tab, cs, v));
+            }
+            st<WT>(P.last, rix<R>(g, xi), xl + n);
+            if (sel(lt, xi) != x_term) st<WT>(P.lterm, rix<R>(g, xi), x_term);
+            if (at(P.hwm, rix<R>(g, xi)) < xl + n) st<WT>(P.hwm, rix<R>(g, xi), xl + n);
+          }
+        }
         if (x_fire) {   // the isolated replica became / stays a candidate: Term+1, votedFor itself
           st<WT>(P.term, rix<R>(g, xi), x_term + 1);
           st<WT>(P.rs, rix<R>(g, xi), uint16_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
@@ -496,7 +538,8 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
           const int ph = int(T.entries_before(T.tick) & P.kmask);
           const uint32_t d = uint32_t(ph - w_ph) & P.kmask;
           if (d != 0u) df |= d <= P.K ? 8u : 16u;
-          if (P.KP > P.K && d != 0u && d <= P.K && Ll > 0) {
+          // (not with a stale leader appending elsewhere in the ring this tick)
+          if (P.KP > P.K && d != 0u && d <= P.K && Ll > 0 && !stale) {
             int lo = Ll, hi = Ll;   // log lengths before this tick (== high-water marks on this path)
 #pragma unroll
             for (int p = 0; p < R; ++p) {

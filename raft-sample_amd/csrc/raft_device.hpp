@@ -38,6 +38,7 @@ constexpr int M_DEFER = 1 << 8;   // on the worklist with ticks pending; the fas
 constexpr int M_MSYNC = 1 << 9;   // primary's MatchIndex[p] == LastApplied[p] for every peer; lmatch is stale
 constexpr int M_STEADY = 1 << 10; // exactly one leader (the primary), every other replica a follower
 constexpr int M_ONECAND = 1 << 11; // as STEADY, except that exactly one other replica is a candidate
+constexpr int M_ONESTALE = 1 << 12; // as STEADY, except that exactly one other replica is a leader of a lower term
 constexpr int HB_NONE = -2147483647 - 1;
 constexpr int I32MAX = 2147483647;
 constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to cut atomic contention
@@ -422,27 +423,44 @@ struct Group {
       if (rota != rota0) at(P.grota, g) = uint16_t(rota);
       if (giso != giso0) at(P.giso, g) = uint8_t(giso);
     }
-    // The primary leader stepped down while another replica leads: move that
-    // leader's rows into the coalesced primary planes so the group can take
-    // the steady-state kernel again (placement only; no state changes).
+    // Primary placement (placement only; no state changes): the leader of the
+    // highest term owns the coalesced MatchIndex / NextIndex planes, so that
+    // a group whose newest leader is the active one (an older one cut off by
+    // isolation) can take the steady-state kernel. The rows of the leader
+    // that gives the planes up move to its xmatch / xnext rows.
     int pri = primary;
-    if (!fault && pri == NO_PRIMARY && ((roles >> 1) & 0x5555u)) {
-      const int nl = int(__builtin_ctz((roles >> 1) & 0x5555u)) >> 1;   // lowest-id leader
+    if (!fault && ((roles >> 1) & ~roles & 0x5555u)) {
+      int best = (pri < R && role(pri) == ROLE_L) ? pri : -1;
 #pragma unroll
-      for (int p = 0; p < R; ++p) {
-        if (p == nl) continue;
-        at(P.lmatch, rix<R>(g, p)) = at(prow(P.xmatch, nl * R + p, P.Gp), g);
-        if constexpr (SEM == SEM_RAFT) at(P.lnext, rix<R>(g, p)) = at(prow(P.xnext, nl * R + p, P.Gp), g);
+      for (int r = 0; r < R; ++r)
+        if (role(r) == ROLE_L && (best < 0 || sel(term, r) > sel(term, best))) best = r;
+      if (best != pri) {
+#pragma unroll
+        for (int p = 0; p < R; ++p) {
+          const int a = at(P.lmatch, rix<R>(g, p));
+          at(P.lmatch, rix<R>(g, p)) = at(prow(P.xmatch, best * R + p, P.Gp), g);
+          if (pri < R) at(prow(P.xmatch, pri * R + p, P.Gp), g) = a;
+          if constexpr (SEM == SEM_RAFT) {
+            const int b = at(P.lnext, rix<R>(g, p));
+            at(P.lnext, rix<R>(g, p)) = at(prow(P.xnext, best * R + p, P.Gp), g);
+            if (pri < R) at(prow(P.xnext, pri * R + p, P.Gp), g) = b;
+          }
+        }
+        pri = best;
       }
-      pri = nl;
     }
-    // DEFER and MSYNC are consumed by the general path; STEADY / ONECAND are recomputed
-    const uint32_t others = roles & ~(3u << (2 * pri));
+    // DEFER and MSYNC are consumed by the general path; the class flags are recomputed
+    const uint32_t others = roles & ~(3u << (2 * (pri & 15)));
     const bool led = pri < R && role(pri) == ROLE_L;
     const bool steady = led && others == 0u;
-    // exactly one non-follower besides the primary, and it is a candidate (ROLE_C = 1)
-    const bool onecand = led && others != 0u && (others & (others - 1u)) == 0u && (others & 0x5555u) != 0u;
-    const int m = pri | (fault << 4) | (steady ? M_STEADY : 0) | (onecand ? M_ONECAND : 0);
+    // exactly one non-follower besides the primary: a candidate (ROLE_C = 1) ...
+    const bool one = led && others != 0u && (others & (others - 1u)) == 0u;
+    const bool onecand = one && (others & 0x5555u) != 0u;
+    // ... or a leader (ROLE_L = 2) of a lower term (a stale leader still cut off)
+    const int sx = one ? int(__builtin_ctz(others)) >> 1 : 0;
+    const bool onestale = SEM == SEM_RAFT && one && (others & 0xAAAAu) != 0u && sel(term, sx) < sel(term, pri & 7);
+    const int m = pri | (fault << 4) | (steady ? M_STEADY : 0) | (onecand ? M_ONECAND : 0) |
+                  (onestale ? M_ONESTALE : 0);
     if (m != meta0) at(P.gmeta, g) = uint16_t(m);
   }
 

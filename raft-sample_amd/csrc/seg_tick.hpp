@@ -181,23 +181,40 @@ struct Seg {
     int sbn = sbd;
     bool rd = rot_dirty;
     if (empty && !fault) { rt = next_phase & P.kmask; sbn = 0; rd = true; }
+    // primary placement: the leader of the highest term (Group::store)
     const uint32_t leaders = mask(act && role == ROLE_L);
     int pri = primary;
-    if (!fault && pri == NO_PRIMARY && leaders) {   // move the lowest-id leader's rows into the primary planes
-      const int nl = first_of(leaders);
-      if (act && me != nl) {
-        at(P.lmatch, ri) = at(prow(P.xmatch, nl * R + me, P.Gp), g);
-        if constexpr (SEM == SEM_RAFT) at(P.lnext, ri) = at(prow(P.xnext, nl * R + me, P.Gp), g);
+    if (!fault && leaders) {
+      // highest term, ties to the lowest id; the current primary keeps the planes on a tie
+      const uint64_t kv = (act && role == ROLE_L)
+                              ? ((uint64_t(uint32_t(~term) ^ 0x80000000u) << 3) | uint64_t(me)) : ~0ull;
+      int best = int(seg_min64(kv) & 7u);
+      if (pri < R && ((leaders >> pri) & 1u) && bc(term, pri) == bc(term, best)) best = pri;
+      if (best != pri) {
+        if (act) {
+          const int a = at(P.lmatch, ri);
+          at(P.lmatch, ri) = at(prow(P.xmatch, best * R + me, P.Gp), g);
+          if (pri < R) at(prow(P.xmatch, pri * R + me, P.Gp), g) = a;
+          if constexpr (SEM == SEM_RAFT) {
+            const int b = at(P.lnext, ri);
+            at(P.lnext, ri) = at(prow(P.xnext, best * R + me, P.Gp), g);
+            if (pri < R) at(prow(P.xnext, pri * R + me, P.Gp), g) = b;
+          }
+        }
+        pri = best;
       }
-      pri = nl;
     }
     const uint32_t nonf = mask(act && role != ROLE_F);
     const uint32_t cands = mask(act && role == ROLE_C);
     const bool led = pri < R && ((leaders >> pri) & 1u);
     const uint32_t others = nonf & ~(1u << (pri & 15));
     const bool steady = led && others == 0u;
-    const bool onecand = led && others != 0u && (others & (others - 1u)) == 0u && (others & cands) != 0u;
-    const int m = pri | (fault << 4) | (steady ? M_STEADY : 0) | (onecand ? M_ONECAND : 0);
+    const bool one = led && others != 0u && (others & (others - 1u)) == 0u;
+    const bool onecand = one && (others & cands) != 0u;
+    const int sx = one ? first_of(others) : 0;
+    const bool onestale = SEM == SEM_RAFT && one && (others & leaders) != 0u && bc(term, sx) < bc(term, pri & 7);
+    const int m = pri | (fault << 4) | (steady ? M_STEADY : 0) | (onecand ? M_ONECAND : 0) |
+                  (onestale ? M_ONESTALE : 0);
     if (me == 0) {
       if (rd) {   // (grota never changes here)
         at(P.grot, g) = uint16_t(rt);

@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--kernel", default="tick_fast_kernel")
     ap.add_argument("--workload", required=True)
     ap.add_argument("--algorithmic-bytes", type=float, default=None)
+    ap.add_argument("--commit", default=None, help="git commit of the build the passes ran on")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -74,6 +75,8 @@ def main():
     }
     if a.algorithmic_bytes:
         out["traffic_over_algorithmic"] = (rd + wr) / a.algorithmic_bytes
+    if a.commit:
+        out["commit"] = a.commit
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out))
 
