@@ -195,6 +195,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     }
     int term[R], last[R], commit[R], lt[R], m[R];
     uint32_t rowbad = 0;   // RAFT explicit rows out of step (replica bits)
+    uint32_t hwup = 0;     // RAFT: replicas whose high-water mark is above their log length (truncated)
     bool empty = true;   // every log of the group empty before this tick
     const bool go = !skip && !bail && c != NO_PRIMARY;
     df |= skip ? 1u : 0u;
@@ -218,7 +219,12 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             if (r != c && at(P.lnext, rix<R>(g, r)) != m[r] + 1) rowbad |= 1u << r;
-            if (at(P.hwm, rix<R>(g, r)) != last[r]) rowbad |= 1u << r;
+            // a log truncated below its high-water mark stays in step as long as
+            // the entry this tick's AppendEntries checks (its last) is still
+            // inside the ring window (hwm-K, last] (Group::r_deliver_ae's evicted rule)
+            const int hwd = at(P.hwm, rix<R>(g, r)) - last[r];
+            if (hwd < 0 || hwd >= int(P.K)) rowbad |= 1u << r;
+            if (hwd > 0) hwup |= 1u << r;
           }
         }
       }
@@ -270,7 +276,8 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     // rows were checked against NextIndex / high-water marks above); both
     // stand still, so the rows become implicit (MSYNC).
     if (go && !bail && lx) {
-      bail = int64_t(Ll) + n > I32MAX || n >= int(P.K) || Ll == 0;
+      // (a truncated log, high-water mark above its length, would break MSYNC's hwm == last)
+      bail = int64_t(Ll) + n > I32MAX || n >= int(P.K) || Ll == 0 || hwup != 0u;
 #pragma unroll
       for (int p = 0; p < R; ++p) bail |= p != c && m[p] != last[p];
       int ts[R], rsv[R];
@@ -423,6 +430,14 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     if (gom && !bail) {
       int cm = Lc;
       bool sync = !stale;   // ONESTALE: the stale leader's row is explicit
+      if constexpr (RAFT) {  // MSYNC also means high-water mark == length for everyone
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (!((hwup >> r) & 1u)) continue;
+          const int la = r == c ? Ll + n : last[r];   // (accepting followers' last already moved)
+          if (at(P.hwm, rix<R>(g, r)) > la) sync = false;
+        }
+      }
       if constexpr (RAFT) {
         // every log now ends at Ll+n (all but at most one lagging isolated
         // replica, and R >= 3): the majority index is Ll+n, committed only if
@@ -478,11 +493,17 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         if ((ltch >> p) & 1u) st<WT>(P.lterm, rix<R>(g, p), Lt);
         if (!RAFT && term[p] != Lt) st<WT>(P.term, rix<R>(g, p), Lt);  // main.go:155
         if (RAFT && !sync && ((mch >> p) & 1u)) st<WT>(P.lnext, rix<R>(g, p), m[p] + 1);   // NextIndex explicit too
-        if (RAFT && !sync && n) st<WT>(P.hwm, rix<R>(g, p), last[p]);                      // high-water mark = new length
+        if (RAFT && !sync && n) {   // high-water mark = max(itself, new length)
+          const int h = ((hwup >> p) & 1u) ? at(P.hwm, rix<R>(g, p)) : 0;
+          if (h < last[p]) st<WT>(P.hwm, rix<R>(g, p), last[p]);
+        }
       }
       if constexpr (RAFT) {
+        if (!sync && n) {   // the leader's high-water mark
+          const int h = ((hwup >> c) & 1u) ? at(P.hwm, rix<R>(g, c)) : 0;
+          if (h < Ll + n) st<WT>(P.hwm, rix<R>(g, c), Ll + n);
+        }
         if (stale) {
-          if (n) st<WT>(P.hwm, rix<R>(g, c), Ll + n);
           // the stale leader's own client append (main.go:327-329) at its own log's end
           const int xl = sel(last, xi);
           if (n) {
