@@ -151,8 +151,8 @@ def main():
     ap.add_argument("--entries", type=int, default=None)
     ap.add_argument("--ring-depth", type=int, default=None)
     ap.add_argument("--leader", type=int, default=0, help="steady-state leader replica (-1: hashed per group)")
-    ap.add_argument("--cpu-groups", type=int, default=131072)
-    ap.add_argument("--cpu-ticks", type=int, default=256)
+    ap.add_argument("--cpu-groups", type=int, default=262144)
+    ap.add_argument("--cpu-ticks", type=int, default=384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
