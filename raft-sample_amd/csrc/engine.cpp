@@ -351,6 +351,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.xmatch), R * R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.gmeta), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.giso), Gp);
+  A(reinterpret_cast<void**>(&e->P.gss), Gp * sizeof(SsRec));
   A(reinterpret_cast<void**>(&e->P.grot), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.grota), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.gsb), Gp * 4);
@@ -418,6 +419,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
                                            e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.lterm, 0, R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.giso, 0, Gp, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.gss, 0, Gp * sizeof(SsRec), e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grot, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grota, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gsb, 0, Gp * 4, e->stream) : z;
@@ -518,12 +520,25 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!rc && logs) rc = d2h(e, rot, e->P.grot, Gp);
   if (!rc && logs) rc = d2h(e, rota, e->P.grota, Gp);
   if (!rc && logs) rc = d2h(e, sb, e->P.gsb, Gp);
+  std::vector<SsRec> gss;
+  if (!rc) rc = d2h(e, gss, e->P.gss, Gp);
   if (!rc && logs) rc = d2h(e, lt, e->P.log_term, R * KP * Gp);
   if (!rc && logs) rc = d2h(e, lv, e->P.log_value, R * KP * Gp);
   const bool crcs = v->log_crc && e->cfg.payload_crc;
   if (!rc && crcs) rc = d2h(e, lcrc, e->P.log_crc, R * KP * Gp);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(e->stream));
+  // SSYNC groups: the planes are stale, the gss record is the state
+  for (uint64_t g = 0; g < G; ++g) {
+    const int pr = meta[g] & 0xF;
+    if (!(meta[g] & M_SSYNC) || pr >= int(R)) continue;
+    for (uint64_t r = 0; r < R; ++r) {
+      term[g * R + r] = gss[g].term;
+      last[g * R + r] = gss[g].last;
+      commit[g * R + r] = int(r) == pr ? gss[g].cl : gss[g].cf;
+      if (!ltm.empty()) ltm[g * R + r] = gss[g].term;
+    }
+  }
   for (uint64_t g = 0; g < G; ++g) {
     const int primary = meta[g] & 0xF;
     const bool msync = meta[g] & M_MSYNC;
@@ -793,9 +808,9 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     fprintf(stderr,
             "raftstep: ticks %lld..%lld lanes %llu skip %llu bail %llu iso %llu drift<=K %llu drift>K %llu switch %llu "
             "blk_hi %llu blk_seg %llu coop %llu drifted %llu | bail: not-steady %llu iso-leader/multi %llu "
-            "follower-out-of-step %llu raft-rows %llu other %llu | quiet-leaderless %llu isolated-leader %llu\n",
+            "follower-out-of-step %llu raft-rows %llu other %llu | quiet-leaderless %llu isolated-leader %llu ssync %llu\n",
             (long long)first_tick, (long long)(first_tick + nticks - 1), d[10], d[0], d[1], d[2], d[3], d[4], d[5], d[6],
-            d[7], d[8], d[9], d[11], d[12], d[13], d[14], d[15], d[16], d[17]);
+            d[7], d[8], d[9], d[11], d[12], d[13], d[14], d[15], d[16], d[17], d[18]);
   }
   return RAFT_OK;
 }
@@ -1043,6 +1058,13 @@ int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap) {
   HIPCHK(hipSetDevice(e->cfg.device));
   static const char* names[] = {"follower", "candidate", "leader", "?"};   // State (main.go:51-57)
   std::string out;
+  uint16_t meta = 0;
+  SsRec ss{};
+  HIPCHK(hipMemcpyAsync(&meta, e->P.gmeta + group, 2, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&ss, e->P.gss + group, sizeof ss, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const int pr = meta & 0xF;
+  const bool ssync = (meta & M_SSYNC) && pr < int(e->cfg.replicas);   // compressed state
   for (uint32_t r = 0; r < e->cfg.replicas; ++r) {
     const uint64_t d = group * e->cfg.replicas + r;   // group-major (rix)
     int32_t term = 0, commit = 0, last = 0;
@@ -1052,6 +1074,7 @@ int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap) {
     HIPCHK(hipMemcpyAsync(&last, e->P.last + d, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&rs, e->P.rs + d, 2, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (ssync) { term = ss.term; last = ss.last; commit = int(r) == pr ? ss.cl : ss.cf; }
     char line[128];
     snprintf(line, sizeof line, "[Server%u:%d:%d:%d][%s]\n", r, term, commit, last, names[rs & 3]);
     out += line;

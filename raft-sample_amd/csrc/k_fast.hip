@@ -198,13 +198,27 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     uint32_t hwup = 0;     // RAFT: replicas whose high-water mark is above their log length (truncated)
     bool empty = true;   // every log of the group empty before this tick
     const bool go = !skip && !bail && c != NO_PRIMARY;
+    // SSYNC: the group's term / last / commit / lterm rows are one 16-B record
+    // (every replica at the same length and term, the followers at one
+    // CommitIndex; implies MSYNC). The rows are rebuilt in registers here and
+    // either written back as the record or, when the tick breaks the form,
+    // spilled as whole rows.
+    const bool ss = go && (meta & M_SSYNC);
     df |= skip ? 1u : 0u;
     DIAG_REASON(df |= bail ? 2048u : 0u;);   // diagnostics: deferral reason "group not steady"
     if (go) {
-      load_row<R>(P.term, g, term);
-      load_row<R>(P.last, g, last);
-      load_row<R>(P.commit, g, commit);
-      load_row<R>(P.lterm, g, lt);
+      if (ss) {
+        const SsRec ss_rec = P.gss[g];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          term[r] = ss_rec.term; last[r] = ss_rec.last; commit[r] = r == c ? ss_rec.cl : ss_rec.cf; lt[r] = ss_rec.term;
+        }
+      } else {
+        load_row<R>(P.term, g, term);
+        load_row<R>(P.last, g, last);
+        load_row<R>(P.commit, g, commit);
+        load_row<R>(P.lterm, g, lt);
+      }
 #pragma unroll
       for (int r = 0; r < R; ++r) empty &= last[r] == 0;
       if (meta & M_MSYNC) {
@@ -307,6 +321,16 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       }
       if (!bail) {
         df |= 131072u;
+        if (ss) {   // the record's rows become explicit (the leader's elements change below)
+          const SsRec ss_rec = P.gss[g];   // (re-read: rare, keeps it out of the live registers)
+          int trow[R], lrow[R], crow[R];
+#pragma unroll
+          for (int p = 0; p < R; ++p) { trow[p] = ss_rec.term; lrow[p] = ss_rec.last; crow[p] = p == c ? ss_rec.cl : ss_rec.cf; }
+          store_row<R>(P.term, g, trow);
+          store_row<R>(P.last, g, lrow);
+          store_row<R>(P.commit, g, crow);
+          store_row<R>(P.lterm, g, trow);
+        }
         sv[0] = cm - Lc;
         sv[1] = 0;
         sv[2] = R - 1;                                    // every AppendEntries dropped
@@ -321,7 +345,8 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
           w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
         }
         if (cm != Lc) st<WT>(P.commit, rix<R>(g, c), cm);
-        if (!(meta & M_MSYNC)) at(P.gmeta, g) = uint16_t(meta | M_MSYNC);
+        const int nm = (meta | M_MSYNC) & ~M_SSYNC;
+        if (nm != meta) at(P.gmeta, g) = uint16_t(nm);
       }
     }
     const bool gom = go && !lx;   // the main steady-state path
@@ -465,6 +490,30 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       // changes (the steady state), else the changed elements
       const uint32_t all = (1u << R) - 1u;
       const uint32_t peers = all & ~(1u << c);
+      // SSYNC after this tick: every follower accepted and every log ends at
+      // Ll+n with an entry of term Lt (REF: an accepting follower takes Lt,
+      // main.go:155; RAFT: terms were checked equal), the followers share one
+      // CommitIndex, and the rows stay implicit (MSYNC)
+      const int cf = sel(commit, c == 0 ? 1 : 0);
+      bool keep_ss = R >= 2 && sync && !stale && xi < 0 && okm == peers && Ll + n > 0 && (n > 0 || Llt == Lt);
+#pragma unroll
+      for (int p = 0; p < R; ++p)
+        if (p != c) keep_ss &= commit[p] == cf && last[p] == Ll + n && (n > 0 || lt[p] == Lt);
+      if (keep_ss) {
+        df |= 262144u;
+        P.gss[g] = SsRec{Ll + n, Lt, cm, cf};
+        st<WT>(P.hb, g, T.now);                                   // timer.Reset(d) of every follower
+      } else {
+      if (ss) {   // leaving the compressed form: the rows as they stood, then the element stores below
+        const SsRec ss_rec = P.gss[g];   // (re-read: rare, keeps it out of the live registers)
+        int trow[R], lrow[R], crow[R];
+#pragma unroll
+        for (int p = 0; p < R; ++p) { trow[p] = ss_rec.term; lrow[p] = ss_rec.last; crow[p] = p == c ? ss_rec.cl : ss_rec.cf; }
+        store_row<R>(P.term, g, trow);
+        store_row<R>(P.last, g, lrow);
+        store_row<R>(P.commit, g, crow);
+        store_row<R>(P.lterm, g, trow);
+      }
       const bool last_row = !WT && n && okm == peers;
       const bool commit_row = !WT && cm != Lc && cch == peers;
       if (last_row || commit_row) {
@@ -531,8 +580,10 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
           st<WT>(P.tstart, rix<R>(g, xi), T.now);
         }
       }
+      }   // !keep_ss
       // RAFT: MSYNC also makes NextIndex (= match+1) and the high-water marks (= last) implicit
       int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
+      nm = keep_ss ? (nm | M_SSYNC) : (nm & ~M_SSYNC);
       if (x_fire) nm = (nm & ~M_STEADY) | M_ONECAND;
       if (nm != meta) at(P.gmeta, g) = uint16_t(nm);
       // this tick's entries go to the leader log + every follower that accepted
@@ -689,7 +740,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
     DIAG_REASON(if (bail && !(df & (2048u | 4096u | 8192u | 16384u))) df |= 32768u;);   // reason: anything later
     DIAG_REASON(if (!bail) df &= ~(2048u | 4096u | 8192u | 16384u););
 #pragma unroll 1
-    for (int k = 0; k < 18; ++k) {
+    for (int k = 0; k < 19; ++k) {
       const uint64_t b = __ballot((df >> k) & 1u);
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
     }

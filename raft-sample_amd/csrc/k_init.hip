@@ -80,10 +80,12 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
     const int meta = at(P.gmeta, g);
     const int primary = meta & 0xF, fault = (meta >> 4) & 0xF;
     const bool msync = (meta & M_MSYNC) && primary < R;
+    const bool ssync = (meta & M_SSYNC) && primary < R;   // compressed state: the gss record
+    const SsRec ss = ssync ? P.gss[g] : SsRec{0, 0, 0, 0};
     const int hb = at(P.hb, g);
     int last[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) last[r] = at(P.last, rix<R>(g, r));
+    for (int r = 0; r < R; ++r) last[r] = ssync ? ss.last : at(P.last, rix<R>(g, r));
     h = sm64(0x5241465444494721ULL ^ (P.gbase + g));
 #pragma unroll 1
     for (int r = 0; r < R; ++r) {
@@ -94,8 +96,10 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
       const int dl = (role == ROLE_L ? ts : max(ts, hb)) + dur;
       const int hwm = (raft && !msync) ? at(P.hwm, rix<R>(g, r)) : l;
       h = dg_mix(h, uint64_t(role) | (uint64_t((x >> 2) & 15u) << 8) | (uint64_t(r) << 16));
-      h = dg_mix(h, lo32(at(P.term, rix<R>(g, r))) | (lo32(l) << 32));
-      h = dg_mix(h, lo32(at(P.commit, rix<R>(g, r))) | (lo32(dl) << 32));
+      const int tm = ssync ? ss.term : at(P.term, rix<R>(g, r));
+      const int cm = ssync ? (r == primary ? ss.cl : ss.cf) : at(P.commit, rix<R>(g, r));
+      h = dg_mix(h, lo32(tm) | (lo32(l) << 32));
+      h = dg_mix(h, lo32(cm) | (lo32(dl) << 32));
       h = dg_mix(h, lo32(dur) | (lo32(hwm) << 32));
 #pragma unroll 1
       for (int p = 0; p < R; ++p) {

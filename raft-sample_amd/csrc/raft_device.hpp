@@ -39,6 +39,14 @@ constexpr int M_MSYNC = 1 << 9;   // primary's MatchIndex[p] == LastApplied[p] f
 constexpr int M_STEADY = 1 << 10; // exactly one leader (the primary), every other replica a follower
 constexpr int M_ONECAND = 1 << 11; // as STEADY, except that exactly one other replica is a candidate
 constexpr int M_ONESTALE = 1 << 12; // as STEADY, except that exactly one other replica is a leader of a lower term
+// SSYNC (with STEADY and MSYNC): every replica holds the same log length and
+// term, every last entry is of that term, the followers share one
+// CommitIndex. The group's term / last / commit / lterm planes are then stale
+// and the 16-B record gss[g] = {LastApplied, Term, leader's CommitIndex,
+// followers' CommitIndex} is the state (the steady-state kernel reads and
+// writes only it); every other reader materialises the planes from it.
+constexpr int M_SSYNC = 1 << 13;
+struct __attribute__((aligned(16))) SsRec { int32_t last, term, cl, cf; };
 constexpr int HB_NONE = -2147483647 - 1;
 constexpr int I32MAX = 2147483647;
 constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to cut atomic contention
@@ -60,6 +68,7 @@ struct DevPlanes {
   int32_t* hwm;        // RAFT mode: [Gp][R] highest LastApplied ever (== last in REF)
   uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
   uint8_t* giso;       // [Gp] EXT leader-isolation victims, nibble per epoch parity: 8 | replica (0 = none)
+  SsRec* gss;          // [Gp] the compressed state of an SSYNC group
   uint16_t* grot;      // ring rotation of the current segment: entry idx >= gsb sits at slot (idx-1+grot) mod KP
   uint16_t* grota;     // rotation of the previous segment (entries idx < gsb)
   int32_t* gsb;        // first index of the current segment (0: one segment)
@@ -375,6 +384,15 @@ struct Group {
 #pragma unroll
     for (int r = 0; r < R; ++r) dl[r] = with_deadlines ? eff_start(at(P.tstart, rix<R>(g, r)), r) + dur[r] : 0;
     known = with_deadlines ? (1u << R) - 1u : 0u;
+    // materialise the compressed state of an SSYNC group (written back by store)
+    if ((meta0 & M_SSYNC) && primary < R) {
+      const SsRec s = P.gss[g];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        term[r] = s.term; last[r] = s.last; commit[r] = r == primary ? s.cl : s.cf; ltm[r] = s.term;
+      }
+      d_term = d_last = d_commit = d_lt = (1u << R) - 1u;
+    }
     // materialise the rows the fast kernel kept implicit: MatchIndex = LastApplied
     // (RAFT also NextIndex = LastApplied+1 and high-water mark = LastApplied)
     if ((meta0 & M_MSYNC) && primary < R) {

@@ -147,6 +147,11 @@ struct Seg {
       if constexpr (SEM == SEM_RAFT) pn = at(P.lnext, ri);
     }
     dl = (role == ROLE_L ? ts : max(ts, hbt)) + dur;   // effective timer start counts the heartbeat
+    if ((meta0 & M_SSYNC) && primary < R && act) {     // compressed state (Group::load)
+      const SsRec s = P.gss[g];
+      term = s.term; last = s.last; commit = me == primary ? s.cl : s.cf; ltm = s.term;
+      dirty |= SD_TERM | SD_LAST | SD_COMMIT | SD_LT;
+    }
     if (!act) { role = ROLE_F; dl = I32MAX; last = 0; hw = 0; }
     // rows the fast kernel kept implicit (MSYNC): MatchIndex = LastApplied
     // (RAFT also NextIndex = LastApplied+1, high-water mark = LastApplied)

@@ -175,3 +175,45 @@ def test_full_size_steady_state_properties():
         ref = o.store_state()
         sl = {k: v[g0:g0 + 700] for k, v in full.items()}
         H.assert_same_state(sl, ref, f"slice at {g0}")
+
+
+@pytest.mark.parametrize("sem", [abi.SEM_REF, abi.SEM_RAFT])
+def test_handler_batches_on_compressed_steady_groups(sem):
+    """Groups the steady-state kernel keeps in compressed form (SSYNC: the
+    term / LastApplied / CommitIndex / last-entry-term rows of a group held as
+    one 16-B record) go through every handler batch, a nodelog and further
+    ticks; every reader must see the rows the record stands for."""
+    R, G, K = 5, 320, 16
+    e, o = pair(replicas=R, groups=G, ring_depth=K, client_period=1, seed=0x5515 + sem, semantics=sem)
+    for x in (e, o):
+        x.init_steady(0, 0)
+    assert list(e.tick(1, 6)) == list(o.tick(1, 6))
+    compare(e, o, "after 6 steady ticks")
+    assert e.nodelog(7) == o.nodelog(7)
+    rng = np.random.default_rng(0x55 + sem)
+    for rnd in range(9):
+        now = 7 + 2 * rnd   # the handler batches' tick, between the fused ticks (time is monotone)
+        kind = rnd % 3
+        groups = rng.permutation(G)[: G // 3]
+        if kind == 0:
+            items = [dict(group=int(g), to=int(rng.integers(1, R)), term=int(rng.integers(1, 4)),
+                          prev_log_index=int(rng.integers(4, 9)), prev_log_term=int(rng.integers(1, 3)),
+                          leader_commit=int(rng.integers(0, 9)),
+                          logs=[(int(rng.integers(1, 4)), int(rng.integers(0, 1 << 62)))
+                                for _ in range(int(rng.integers(0, 3)))]) for g in groups]
+            reqs, ents = H.ae_reqs(items)
+            a, b = e.append_entries(now, reqs, ents), o.append_entries(now, reqs, ents)
+        elif kind == 1:
+            reqs = H.vote_reqs([dict(group=int(g), to=int(rng.integers(0, R)), term=int(rng.integers(1, 4)))
+                                for g in groups])
+            a, b = e.request_vote(now, reqs), o.request_vote(now, reqs)
+        else:
+            ops = H.ops([dict(group=int(g), replica=int(rng.integers(0, R)), kind=int(rng.integers(1, 6)),
+                              arg=int(rng.integers(0, 1 << 62))) for g in groups])
+            a, b = e.group_ops(now, ops), o.group_ops(now, ops)
+        assert a.tobytes() == b.tobytes(), f"round {rnd} kind {kind}: responses differ"
+        compare(e, o, f"round {rnd} kind {kind}")
+        # the untouched groups are still compressed: tick everything once more
+        se, so = e.tick(8 + 2 * rnd, 1), o.tick(8 + 2 * rnd, 1)
+        assert list(se) == list(so), f"round {rnd}: tick stats differ"
+        compare(e, o, f"round {rnd} tick")
