@@ -154,6 +154,8 @@ def main():
     ap.add_argument("--cpu-groups", type=int, default=262144)
     ap.add_argument("--cpu-ticks", type=int, default=384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--isolate", type=int, default=None,
+                    help="diagnostics: override the workload's isolation windows per 65536 epochs (0: none)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -181,6 +183,8 @@ def main():
     from raftstep import Engine, STAT_NAMES
 
     wl = WORKLOADS[wl_key]
+    if args.isolate is not None and "iso" in wl:
+        wl = dict(wl, iso=(args.isolate,) + tuple(wl["iso"][1:]))
     R = args.replicas or wl.get("replicas", R_DEFAULT)
     G = args.groups_per_gpu or wl["groups"]
     E = args.entries or wl["entries"]
@@ -233,6 +237,12 @@ def main():
     eng.profile(1)
     eng.tick(tick, args.steps, stats=False)
     kernel_ms, kernel_launches = eng.profile_read()
+    two_pass = os.environ.get("RAFTSTEP_TWO_PASS", "1") != "0"
+    list_ms = list_launches = 0
+    if two_pass:   # the second pass (list kernel over the groups the lean kernel passed on)
+        eng.profile(3)
+        eng.tick(tick + args.steps, args.steps, stats=False)
+        list_ms, list_launches = eng.profile_read()
     eng.profile(0)
     nranks, _, allreduces = eng.comm_info()
 
@@ -262,7 +272,9 @@ def main():
             "frac_measured": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
             "traffic_source": traffic_src,
             "bytes_per_group_step": B, "units_per_launch": G,
-            "kernel": "tick_fast_kernel", "avg_kernel_us": avg_kernel_s * 1e6, "kernel_launches": kernel_launches,
+            "kernel": "tick_lean_kernel" if two_pass else "tick_fast_kernel",
+            "avg_kernel_us": avg_kernel_s * 1e6, "kernel_launches": kernel_launches,
+            "list_kernel_us": (list_ms * 1e3 / max(list_launches, 1)) if two_pass else None,
             "avg_region_us_per_tick": avg_region_s * 1e6,
             "achieved_region": B * G / avg_region_s / 1e9}
     result = {

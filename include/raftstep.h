@@ -288,6 +288,8 @@ int raft_comm_info(raft_engine* e, int32_t* nranks, int32_t* rank, uint64_t* all
  * mode 2: one event pair on the engine stream around all launches of each
  *         raft_tick call (no per-launch cost; includes the general kernel and
  *         launch gaps, so it upper-bounds the tick kernel's duration);
+ * mode 3: as mode 1 for the second pass of the two-pass tick (the list
+ *         kernel over the groups the lean steady-state kernel passed on);
  * mode 0: off. raft_profile_read() syncs and returns the summed milliseconds
  * and the number of tick launches covered. */
 int raft_profile_enable(raft_engine* e, int mode);

@@ -104,12 +104,17 @@ struct raft_engine {
   // worklist of groups the steady-state kernel hands to the general kernel
   uint32_t* work = nullptr;     // deferred group ids
   int32_t* work_tick = nullptr; // tick each one was deferred at
-  uint32_t* wcount = nullptr;   // [2], indexed by window parity
+  uint32_t* wcount = nullptr;   // shard counters: worklist [2 parities][SHARD_WORDS], then the two-pass list [2][SHARD_WORDS]
   int force_general = 0;        // debug: route every group through the general kernel
   int lane_general = 0;         // RAFTSTEP_GENERAL=lane: one-lane-per-group general kernel (A/B) instead of the segment one
   uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
   int write_through = 0;        // fast kernel stores with sc1 (write-through) instead of write-back
   int debug_work = 0;           // RAFTSTEP_DEBUG_WORK: print each general-kernel worklist size
+  // two-pass tick (RAFTSTEP_TWO_PASS, default on): the lean kernel takes the
+  // compressed steady groups, the list kernel every other live group
+  int two_pass = 1;
+  uint32_t* blist = nullptr;    // [Gp] groups the lean kernel passed on
+  uint32_t lpar = 0;            // parity of the two-pass list's shard counters
   // handler-batch staging
   void* stage = nullptr;
   size_t stage_cap = 0;
@@ -264,6 +269,18 @@ int h2d(raft_engine* e, T* d, const std::vector<T>& h) {
   return RAFT_OK;
 }
 
+// Group records <-> per-row host arrays [Gp][R] (row k of group g at
+// blk[(g*NPL + k)*R ..], raft_device.hpp rix)
+void rec_rows(const std::vector<int32_t>& blk, int k, uint64_t R, uint64_t Gp, std::vector<int32_t>& out) {
+  out.resize(R * Gp);
+  for (uint64_t g = 0; g < Gp; ++g)
+    std::memcpy(&out[g * R], &blk[(g * NPL + uint64_t(k)) * R], R * 4);
+}
+void rec_put(std::vector<int32_t>& blk, int k, uint64_t R, uint64_t Gp, const std::vector<int32_t>& rows) {
+  for (uint64_t g = 0; g < Gp; ++g)
+    std::memcpy(&blk[(g * NPL + uint64_t(k)) * R], &rows[g * R], R * 4);
+}
+
 }  // namespace
 
 extern "C" {
@@ -316,10 +333,10 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
     return fail(RAFT_EINVAL, "isolation length must satisfy 1 <= min <= max <= 32");
   const uint64_t Gp = (c.groups + 255) & ~uint64_t(255);
   // device addressing (raft_device.hpp at(), rix()): 64-bit plane/tile bases,
-  // 32-bit per-lane BYTE offsets, so the group-major per-replica planes (4-B
-  // elements) must satisfy Gp*R*4 < 2^32 (ring tiles: KP*64*R*8 < 2^26)
-  if (Gp * c.replicas * 4 > uint64_t(0xFFFFFFFFu))
-    return fail(RAFT_EINVAL, "too many groups for one engine (need groups * replicas <= 2^30 - 256 * replicas)");
+  // 32-bit per-lane BYTE offsets, so the group records (NPL rows of R 4-B
+  // words) must satisfy Gp*NPL*R*4 < 2^32 (ring tiles: KP*64*R*8 < 2^26)
+  if (Gp * NPL * c.replicas * 4 > uint64_t(0xFFFFFFFFu))
+    return fail(RAFT_EINVAL, "too many groups for one engine (need groups * replicas * %d * 4 < 2^32)", NPL);
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RAFT_ENODEV, "no HIP device");
   if (c.device < 0 || c.device >= ndev) return fail(RAFT_ENODEV, "device %d out of range", c.device);
@@ -341,13 +358,24 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* rp = getenv("RAFTSTEP_RING_PHYS")) phys = atoi(rp) == 2 ? 2 : 1;
   const uint64_t K = c.ring_depth * phys;
   e->KP = K;
-  A(reinterpret_cast<void**>(&e->P.term), R * Gp * 4);
-  A(reinterpret_cast<void**>(&e->P.last), R * Gp * 4);
-  A(reinterpret_cast<void**>(&e->P.commit), R * Gp * 4);
-  A(reinterpret_cast<void**>(&e->P.tstart), R * Gp * 4);
+  const bool raft = c.semantics == RAFT_SEM_RAFT;
+  // group records: every per-replica row of a group in NPL*R contiguous words
+  A(reinterpret_cast<void**>(&e->P.rec), Gp * NPL * R * 4);
+  if (rc == RAFT_OK) {
+    int32_t* rec = e->P.rec;
+    e->P.term = rec + PL_TERM * R;
+    e->P.last = rec + PL_LAST * R;
+    e->P.commit = rec + PL_COMMIT * R;
+    e->P.tstart = rec + PL_TSTART * R;
+    e->P.lterm = rec + PL_LTERM * R;
+    e->P.rs = rec + PL_RS * R;
+    e->P.lmatch = rec + PL_LMATCH * R;
+    if (raft) {   // NextIndex rows and high-water marks exist only in RAFT mode (null: REF)
+      e->P.lnext = rec + PL_LNEXT * R;
+      e->P.hwm = rec + PL_HWM * R;
+    }
+  }
   A(reinterpret_cast<void**>(&e->P.hb), Gp * 4);
-  A(reinterpret_cast<void**>(&e->P.rs), R * Gp * 2);
-  A(reinterpret_cast<void**>(&e->P.lmatch), R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.xmatch), R * R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.gmeta), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.giso), Gp);
@@ -355,19 +383,16 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.grot), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.grota), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.gsb), Gp * 4);
-  A(reinterpret_cast<void**>(&e->P.lterm), R * Gp * 4);
-  A(reinterpret_cast<void**>(&e->work), Gp * 4);
-  A(reinterpret_cast<void**>(&e->work_tick), Gp * 4);
-  A(reinterpret_cast<void**>(&e->wcount), 256);
+  // sharded group lists (raft_device.hpp): NSHARD shards of scap entries
+  const uint64_t scap = ((Gp / 256 + NSHARD - 1) / NSHARD) * 256;
+  A(reinterpret_cast<void**>(&e->work), NSHARD * scap * 4);
+  A(reinterpret_cast<void**>(&e->work_tick), NSHARD * scap * 4);
+  A(reinterpret_cast<void**>(&e->wcount), 4 * SHARD_WORDS * 4);   // worklist x2 parities, two-pass list x2
+  A(reinterpret_cast<void**>(&e->blist), NSHARD * scap * 4);
   A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.log_value), R * K * Gp * 8);
   if (c.payload_crc) A(reinterpret_cast<void**>(&e->P.log_crc), R * K * Gp * 4);
-  const bool raft = c.semantics == RAFT_SEM_RAFT;
-  if (raft) {   // NextIndex rows and high-water marks exist only in RAFT mode
-    A(reinterpret_cast<void**>(&e->P.lnext), R * Gp * 4);
-    A(reinterpret_cast<void**>(&e->P.xnext), R * R * Gp * 4);
-    A(reinterpret_cast<void**>(&e->P.hwm), R * Gp * 4);
-  }
+  if (raft) A(reinterpret_cast<void**>(&e->P.xnext), R * R * Gp * 4);
   uint32_t* d_tab = nullptr;
   A(reinterpret_cast<void**>(&d_tab), 8 * 256 * 4);
   e->P.crc_tab = d_tab;
@@ -382,6 +407,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
     return rc;
   }
   e->P.Gp = Gp;
+  e->P.scap = uint32_t(scap);
   e->P.G = c.groups;
   e->P.gbase = c.group_base;
   e->P.K = c.ring_depth;
@@ -394,6 +420,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* se = getenv("RAFTSTEP_SLOW_EVERY")) e->slow_every = std::max(1, atoi(se));
   if (const char* wt = getenv("RAFTSTEP_WRITE_THROUGH")) e->write_through = atoi(wt) != 0;
   if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
+  if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
   if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
     if (rc == RAFT_OK) rc = dev_alloc(e, reinterpret_cast<void**>(&e->P.dbg), 32 * 8);
     if (rc == RAFT_OK && hipMemset(e->P.dbg, 0, 32 * 8) != hipSuccess) rc = fail(RAFT_EHIP, "hipMemset failed");
@@ -407,31 +434,21 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   // zero everything once so that padding / unused rows are deterministic
   for (void* p : e->allocs) (void)p;
   hipError_t z = hipSuccess;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.term, 0, R * Gp * 4, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.last, 0, R * Gp * 4, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.commit, 0, R * Gp * 4, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.tstart, 0, R * Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.rec, 0, Gp * NPL * R * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.hb, 0x80, Gp * 4, e->stream) : z;  // 0x80808080 < any time
-  z = z == hipSuccess ? hipMemsetAsync(e->P.rs, 0, R * Gp * 2, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.lmatch, 0, R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.xmatch, 0, R * R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(e->P.gmeta), uint16_t(NO_PRIMARY), Gp,
                                            e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.lterm, 0, R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.giso, 0, Gp, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gss, 0, Gp * sizeof(SsRec), e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grot, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grota, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gsb, 0, Gp * 4, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, 256, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, 4 * SHARD_WORDS * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_value, 0, R * K * Gp * 8, e->stream) : z;
   if (c.payload_crc) z = z == hipSuccess ? hipMemsetAsync(e->P.log_crc, 0, R * K * Gp * 4, e->stream) : z;
-  if (raft) {
-    z = z == hipSuccess ? hipMemsetAsync(e->P.lnext, 0, R * Gp * 4, e->stream) : z;
-    z = z == hipSuccess ? hipMemsetAsync(e->P.xnext, 0, R * R * Gp * 4, e->stream) : z;
-    z = z == hipSuccess ? hipMemsetAsync(e->P.hwm, 0, R * Gp * 4, e->stream) : z;
-  }
+  if (raft) z = z == hipSuccess ? hipMemsetAsync(e->P.xnext, 0, R * R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemcpyAsync(d_tab, crc_tab_host().data(), 8 * 256 * 4, hipMemcpyHostToDevice, e->stream) : z;
   z = z == hipSuccess ? hipStreamSynchronize(e->stream) : z;
   if (z != hipSuccess) {
@@ -472,8 +489,6 @@ int raft_init_new_nodes(raft_engine* e, int64_t tick0) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
   if (int rc = check_ticks(e, tick0, 1)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
-  const uint64_t R = e->cfg.replicas, Gp = e->Gp;
-  HIPCHK(hipMemsetAsync(e->P.lmatch, 0, R * Gp * 4, e->stream));
   HIPCHK(launch_init_new(e->R, e->P, make_trace(e, tick0), e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return RAFT_OK;
@@ -493,29 +508,21 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   HIPCHK(hipSetDevice(e->cfg.device));
   const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
   const bool raft = e->cfg.semantics == RAFT_SEM_RAFT;
-  std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt, ln, xn, hw;
-  std::vector<uint16_t> rs, meta, rot, rota;
+  std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt, ln, xn, hw, rs, blk;
+  std::vector<uint16_t> meta, rot, rota;
   std::vector<uint8_t> giso;
   std::vector<int32_t> sb;
   std::vector<int64_t> lv;
   std::vector<uint32_t> lcrc;
   int rc = RAFT_OK;
-  if (!rc) rc = d2h(e, term, e->P.term, R * Gp);
-  if (!rc) rc = d2h(e, last, e->P.last, R * Gp);
-  if (!rc) rc = d2h(e, commit, e->P.commit, R * Gp);
-  if (!rc) rc = d2h(e, ts, e->P.tstart, R * Gp);
+  if (!rc) rc = d2h(e, blk, e->P.rec, Gp * NPL * R);   // group records (rows extracted below)
   if (!rc) rc = d2h(e, hb, e->P.hb, Gp);
-  if (!rc) rc = d2h(e, rs, e->P.rs, R * Gp);
-  if (!rc) rc = d2h(e, lm, e->P.lmatch, R * Gp);
   if (!rc) rc = d2h(e, xm, e->P.xmatch, R * R * Gp);
   if (!rc) rc = d2h(e, meta, e->P.gmeta, Gp);
   if (!rc && v->iso_victim) rc = d2h(e, giso, e->P.giso, Gp);
-  if (!rc && raft) rc = d2h(e, ln, e->P.lnext, R * Gp);
   if (!rc && raft) rc = d2h(e, xn, e->P.xnext, R * R * Gp);
-  if (!rc && raft) rc = d2h(e, hw, e->P.hwm, R * Gp);
   const bool logs = v->log_term || v->log_value || v->log_crc;
   std::vector<int32_t> ltm;
-  if (!rc && logs) rc = d2h(e, ltm, e->P.lterm, R * Gp);
   const uint64_t KP = e->KP;
   if (!rc && logs) rc = d2h(e, rot, e->P.grot, Gp);
   if (!rc && logs) rc = d2h(e, rota, e->P.grota, Gp);
@@ -528,6 +535,16 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!rc && crcs) rc = d2h(e, lcrc, e->P.log_crc, R * KP * Gp);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(e->stream));
+  rec_rows(blk, PL_TERM, R, Gp, term);
+  rec_rows(blk, PL_LAST, R, Gp, last);
+  rec_rows(blk, PL_COMMIT, R, Gp, commit);
+  rec_rows(blk, PL_TSTART, R, Gp, ts);
+  rec_rows(blk, PL_RS, R, Gp, rs);
+  rec_rows(blk, PL_LMATCH, R, Gp, lm);
+  if (raft) rec_rows(blk, PL_LNEXT, R, Gp, ln);
+  if (raft) rec_rows(blk, PL_HWM, R, Gp, hw);
+  if (logs) rec_rows(blk, PL_LTERM, R, Gp, ltm);
+  std::vector<int32_t>().swap(blk);
   // SSYNC groups: the planes are stale, the gss record is the state
   for (uint64_t g = 0; g < G; ++g) {
     const int pr = meta[g] & 0xF;
@@ -611,7 +628,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   const uint64_t KP = e->KP;
   std::vector<int32_t> term(R * Gp, 0), last(R * Gp, 0), commit(R * Gp, 0), ts(R * Gp, 0), lm(R * Gp, 0),
       xm(R * R * Gp, 0), lt(R * KP * Gp, 0), hb(Gp, HB_NONE);
-  std::vector<uint16_t> rs(R * Gp, 0);
+  std::vector<int32_t> rs(R * Gp, 0);
   std::vector<uint16_t> meta(Gp, uint16_t(NO_PRIMARY));
   std::vector<uint8_t> giso(Gp, 0);
   std::vector<int64_t> lv(R * KP * Gp, 0);
@@ -650,7 +667,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
       last[d] = v->last[c];
       commit[d] = v->commit[c];
       ts[d] = v->deadline[c] - v->timeout[c];
-      rs[d] = uint16_t(v->role[c] | (v->voted[c] << 2) | (uint32_t(v->timeout[c]) << 6));
+      rs[d] = int32_t(v->role[c] | (v->voted[c] << 2) | (uint32_t(v->timeout[c]) << 6));
       if (v->role[c] == RAFT_LEADER)
         for (uint64_t p = 0; p < R; ++p) {
           if (p == r) continue;
@@ -692,14 +709,19 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
       if (v->last[c] > 0) ltm[d] = v->log_term[c * K + uint64_t((v->last[c] - 1) & int64_t(K - 1))];
     }
   }
+  std::vector<int32_t> blk(Gp * NPL * R, 0);   // group records
+  rec_put(blk, PL_TERM, R, Gp, term);
+  rec_put(blk, PL_LAST, R, Gp, last);
+  rec_put(blk, PL_COMMIT, R, Gp, commit);
+  rec_put(blk, PL_TSTART, R, Gp, ts);
+  rec_put(blk, PL_LTERM, R, Gp, ltm);
+  rec_put(blk, PL_RS, R, Gp, rs);
+  rec_put(blk, PL_LMATCH, R, Gp, lm);
+  if (raft) rec_put(blk, PL_LNEXT, R, Gp, ln);
+  if (raft) rec_put(blk, PL_HWM, R, Gp, hw);
   int rc = RAFT_OK;
-  if (!rc) rc = h2d(e, e->P.term, term);
-  if (!rc) rc = h2d(e, e->P.last, last);
-  if (!rc) rc = h2d(e, e->P.commit, commit);
-  if (!rc) rc = h2d(e, e->P.tstart, ts);
+  if (!rc) rc = h2d(e, e->P.rec, blk);
   if (!rc) rc = h2d(e, e->P.hb, hb);
-  if (!rc) rc = h2d(e, e->P.rs, rs);
-  if (!rc) rc = h2d(e, e->P.lmatch, lm);
   if (!rc) rc = h2d(e, e->P.xmatch, xm);
   if (!rc) rc = h2d(e, e->P.gmeta, meta);
   if (!rc) rc = h2d(e, e->P.giso, giso);
@@ -708,10 +730,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.grot, rot);
   if (!rc) rc = h2d(e, e->P.grota, rot);
   if (!rc) rc = h2d(e, e->P.gsb, sb0);
-  if (!rc) rc = h2d(e, e->P.lterm, ltm);
-  if (!rc && raft) rc = h2d(e, e->P.lnext, ln);
   if (!rc && raft) rc = h2d(e, e->P.xnext, xn);
-  if (!rc && raft) rc = h2d(e, e->P.hwm, hw);
   if (!rc && e->cfg.payload_crc) rc = h2d(e, e->P.log_crc, lcrc);
   if (!rc) rc = h2d(e, e->P.log_term, lt);
   if (!rc) rc = h2d(e, e->P.log_value, lv);
@@ -761,7 +780,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     unsigned long long* st = stats ? e->hist + size_t(i) * STAT_SLOTS * NSTAT : nullptr;
     // worklist counter of this window; zeroed by the previous general kernel
     // (or at engine creation), so no per-call memset
-    uint32_t* cnt = e->wcount + (e->wpar & 1);
+    uint32_t* cnt = e->wcount + (e->wpar & 1) * SHARD_WORDS;
     hipEvent_t a = nullptr, b = nullptr;
     if (e->prof == 1) {
       a = next_event(e);
@@ -769,18 +788,35 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
     }
     const int force = e->force_general;
-    HIPCHK(launch_tick_fast(e->R, int(e->cfg.semantics), e->P, T, st, e->work, e->work_tick, cnt, force, e->write_through,
-                            e->stream, a, b));
+    if (e->two_pass && !force && !e->write_through) {
+      // lean pass appends to list counter lpar, the list pass zeroes the other one
+      hipEvent_t c = nullptr, d = nullptr;
+      if (e->prof == 3) {
+        c = next_event(e);
+        d = next_event(e);
+        if (!c || !d) return fail(RAFT_EHIP, "hipEventCreate failed");
+      }
+      HIPCHK(launch_tick_two_pass(e->R, int(e->cfg.semantics), e->P, T, st, e->work, e->work_tick, cnt, e->blist,
+                                  e->wcount + (2 + (e->lpar & 1)) * SHARD_WORDS,
+                                  e->wcount + (2 + ((e->lpar + 1) & 1)) * SHARD_WORDS, e->stream, a, b,
+                                  c, d));
+      ++e->lpar;
+    } else {
+      HIPCHK(launch_tick_fast(e->R, int(e->cfg.semantics), e->P, T, st, e->work, e->work_tick, cnt, force,
+                              e->write_through, e->stream, a, b));
+    }
     // deferred groups catch up every slow_every ticks and at the end of the call
     if ((i + 1) % e->slow_every == 0 || i + 1 == nticks) {
       if (e->debug_work) {   // diagnostics: worklist size of each general-kernel launch (synchronising)
-        uint32_t nw = 0;
-        HIPCHK(hipMemcpyAsync(&nw, cnt, 4, hipMemcpyDeviceToHost, e->stream));
+        uint32_t sh[SHARD_WORDS], nw = 0;
+        HIPCHK(hipMemcpyAsync(sh, cnt, sizeof sh, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
+        for (int k = 0; k < NSHARD; ++k) nw += sh[k * SHARD_STRIDE];
         fprintf(stderr, "raftstep: general kernel ticks %lld..%lld worklist %u\n", (long long)win_first, (long long)t, nw);
       }
       HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t, stats ? e->hist : nullptr,
-                              e->work, e->work_tick, cnt, e->wcount + ((e->wpar + 1) & 1), e->lane_general, e->stream));
+                              e->work, e->work_tick, cnt, e->wcount + ((e->wpar + 1) & 1) * SHARD_WORDS, e->lane_general,
+                              e->stream));
       ++e->wpar;
       if (stats)
         if (int rc = flush_window_stats(e, uint32_t(win_first - first_tick), i)) return rc;
@@ -1005,7 +1041,7 @@ int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats) {
 
 int raft_profile_enable(raft_engine* e, int mode) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
-  if (mode < 0 || mode > 2) return fail(RAFT_EINVAL, "profile mode must be 0, 1 or 2");
+  if (mode < 0 || mode > 3) return fail(RAFT_EINVAL, "profile mode must be 0, 1, 2 or 3");
   e->prof = mode;
   e->ev_used = 0;
   e->prof_ms = 0.0;
@@ -1021,7 +1057,7 @@ int raft_profile_read(raft_engine* e, double* total_ms, uint64_t* launches) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, e->ev[i], e->ev[i + 1]));
     e->prof_ms += ms;
-    if (e->prof == 1) e->prof_n += 1;   // mode 2 counts launches as it records
+    if (e->prof != 2) e->prof_n += 1;   // mode 2 counts launches as it records
   }
   e->ev_used = 0;
   if (total_ms) *total_ms = e->prof_ms;
@@ -1066,13 +1102,12 @@ int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap) {
   const int pr = meta & 0xF;
   const bool ssync = (meta & M_SSYNC) && pr < int(e->cfg.replicas);   // compressed state
   for (uint32_t r = 0; r < e->cfg.replicas; ++r) {
-    const uint64_t d = group * e->cfg.replicas + r;   // group-major (rix)
-    int32_t term = 0, commit = 0, last = 0;
-    uint16_t rs = 0;
+    const uint64_t d = group * NPL * e->cfg.replicas + r;   // group record (rix)
+    int32_t term = 0, commit = 0, last = 0, rs = 0;
     HIPCHK(hipMemcpyAsync(&term, e->P.term + d, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&commit, e->P.commit + d, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&last, e->P.last + d, 4, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(&rs, e->P.rs + d, 2, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&rs, e->P.rs + d, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (ssync) { term = ss.term; last = ss.last; commit = int(r) == pr ? ss.cl : ss.cf; }
     char line[128];

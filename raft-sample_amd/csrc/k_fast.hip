@@ -152,21 +152,16 @@ __device__ __forceinline__ bool quiet_leaderless(const DevPlanes& P, const Trace
   return quiet;
 }
 
-template <int R, bool WT, bool CRC, int SEM>
-__global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, unsigned long long* stats,
-                                                        uint32_t* work, int32_t* work_tick, uint32_t* work_count,
-                                                        int force_slow) {
+// The tick of one group (lane) — the body of both launch forms: the dense
+// one over all groups (tick_fast_kernel, `g` = the lane's group) and the one
+// over the list of groups the lean kernel passed on (tick_list_kernel, LIST:
+// the lanes of a wave hold scattered groups, so every ring write is the
+// lane's own). Block-uniform control flow (it reduces over the block).
+template <int R, bool WT, bool CRC, int SEM, bool LIST>
+__device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                                           int32_t* work_tick, uint32_t* work_count, int force_slow, const uint32_t g,
+                                           const uint32_t* tab) {
   constexpr bool RAFT = SEM == SEM_RAFT;
-  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-  // EXT CRC32C tables (8 KiB) staged in LDS for the stamp/verify lookups
-  __shared__ uint32_t tab[CRC ? 2048 : 1];
-  if constexpr (CRC) {
-    const uint4* src = reinterpret_cast<const uint4*>(P.crc_tab);
-    uint4* dst = reinterpret_cast<uint4*>(tab);
-    dst[threadIdx.x] = src[threadIdx.x];
-    dst[threadIdx.x + 256] = src[threadIdx.x + 256];
-    __syncthreads();
-  }
   int sv[5] = {0, 0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups, term bumps
   bool bail = false;
   const int n = int(T.client_entries());   // entries per leader this tick (wave-uniform)
@@ -576,7 +571,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
         }
         if (x_fire) {   // the isolated replica became / stays a candidate: Term+1, votedFor itself
           st<WT>(P.term, rix<R>(g, xi), x_term + 1);
-          st<WT>(P.rs, rix<R>(g, xi), uint16_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
+          st<WT>(P.rs, rix<R>(g, xi), int32_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
           st<WT>(P.tstart, rix<R>(g, xi), T.now);
         }
       }
@@ -666,7 +661,37 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
   // entry. Every other writing lane stores its own R-contiguous segment.
   // s0: the global phase entries_before(tick) (groups rotated at their first
   // entry, init_steady) or the first writer's slot, whichever more lanes share.
-  if (n) {
+  if (LIST && n && wr != 0) {   // scattered groups: each lane writes its own R-contiguous segment
+    const uint64_t tb = ring_tile(g, P.KP, R);
+    int32_t* const rt = P.log_term + tb;
+    int64_t* const rv = P.log_value + tb;
+    uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
+    df |= 512u;
+    uint32_t cs = 0;
+    if constexpr (CRC) cs = crc_term_state(tab, w_term);
+    for (int e = 0; e < n; ++e) {
+      const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
+      uint32_t stamp = 0;
+      if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+      {
+            const uint32_t o = ring_in_tile(g, R, uint32_t((w_ph + e) & int(P.kmask)), 0u);
+            if (!WT && wr == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
+              fill_seg<R>(rt + o, w_term);
+              fill_seg<R>(rv + o, v);
+              if constexpr (CRC) fill_seg<R>(rc + o, stamp);
+            } else {
+#pragma unroll
+              for (int p = 0; p < R; ++p) {
+                if (!((wr >> p) & 1u)) continue;
+                st<WT>(rt, o + p, w_term);
+                st<WT>(rv, o + p, v);
+                if constexpr (CRC) st<WT>(rc, o + p, stamp);
+              }
+            }
+      }
+    }
+  }
+  if (!LIST && n) {
     const uint64_t wball = __ballot(wr != 0);
     if (wball) {
       const int lane = threadIdx.x & 63;
@@ -745,23 +770,35 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
     }
   }
-  // groups that need the general path go to the dense worklist: block-local
-  // prefix over the wave ballots, one atomic per block that defers anything
-  __shared__ uint32_t wn[4], wbase;
-  const uint64_t bm = __ballot(bail);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) wn[wave] = uint32_t(__popcll(bm));
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t tot = wn[0] + wn[1] + wn[2] + wn[3];
-    wbase = tot ? atomicAdd(work_count, tot) : 0u;
-  }
-  __syncthreads();
-  if (bail) {
-    uint32_t off = wbase + uint32_t(__popcll(bm & ((1ull << lane) - 1ull)));
-    for (int w = 0; w < wave; ++w) off += wn[w];
-    work[off] = g;
-    work_tick[off] = int32_t(T.tick);
+  // groups that need the general path go to the sharded worklist: dense
+  // launch, block-local prefix over the wave ballots and one atomic on the
+  // block's shard; list launch (scattered groups), one atomic per deferred
+  // lane on its group's shard
+  if constexpr (LIST) {
+    if (bail) {
+      const uint32_t k = shard_home(g);
+      const uint32_t off = k * P.scap + atomicAdd(&work_count[k * SHARD_STRIDE], 1u);
+      work[off] = g;
+      work_tick[off] = int32_t(T.tick);
+    }
+  } else {
+    __shared__ uint32_t wn[4], wbase;
+    const uint64_t bm = __ballot(bail);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t k = blockIdx.x & uint32_t(NSHARD - 1);   // == shard_home(g)
+    if (lane == 0) wn[wave] = uint32_t(__popcll(bm));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t tot = wn[0] + wn[1] + wn[2] + wn[3];
+      wbase = tot ? atomicAdd(&work_count[k * SHARD_STRIDE], tot) : 0u;
+    }
+    __syncthreads();
+    if (bail) {
+      uint32_t off = k * P.scap + wbase + uint32_t(__popcll(bm & ((1ull << lane) - 1ull)));
+      for (int w = 0; w < wave; ++w) off += wn[w];
+      work[off] = g;
+      work_tick[off] = int32_t(T.tick);
+    }
   }
   if (stats) {
     if constexpr (RAFT) {
@@ -771,6 +808,254 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
       const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
       const int v4[4] = {sv[0], sv[1], sv[2], sv[3]};
       block_stats<4>(v4, idx, stats);
+    }
+  }
+}
+
+// EXT CRC32C tables (8 KiB) staged in LDS for the stamp/verify lookups
+template <bool CRC>
+__device__ __forceinline__ void stage_crc_tab(const DevPlanes& P, uint32_t* tab) {
+  if constexpr (CRC) {
+    const uint4* src = reinterpret_cast<const uint4*>(P.crc_tab);
+    uint4* dst = reinterpret_cast<uint4*>(tab);
+    dst[threadIdx.x] = src[threadIdx.x];
+    dst[threadIdx.x + 256] = src[threadIdx.x + 256];
+    __syncthreads();
+  }
+}
+
+// Every group, one lane each (the single-pass plan).
+template <int R, bool WT, bool CRC, int SEM>
+__global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, unsigned long long* stats,
+                                                        uint32_t* work, int32_t* work_tick, uint32_t* work_count,
+                                                        int force_slow) {
+  __shared__ uint32_t tab[CRC ? 2048 : 1];
+  stage_crc_tab<CRC>(P, tab);
+  fast_group<R, WT, CRC, SEM, false>(P, T, stats, work, work_tick, work_count, force_slow,
+                                     blockIdx.x * 256u + threadIdx.x, tab);
+}
+
+// The groups the lean kernel passed on (list[0 .. *count)), grid-striding
+// with a resident grid; zeroes the other parity's list counter (the next
+// tick's lean kernel appends there).
+template <int R, bool WT, bool CRC, int SEM>
+__global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, unsigned long long* stats,
+                                                        uint32_t* work, int32_t* work_tick, uint32_t* work_count,
+                                                        const uint32_t* list, const uint32_t* count,
+                                                        uint32_t* next_count) {
+  __shared__ uint32_t tab[CRC ? 2048 : 1];
+  __shared__ uint32_t pre[NSHARD + 1];
+  shard_zero(next_count);
+  const uint32_t n = shard_prefix(count, pre);
+  if (blockIdx.x * 256u >= n) return;
+  stage_crc_tab<CRC>(P, tab);
+  for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t g = i < n ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
+    fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab);
+    __syncthreads();   // the body's block reductions reuse their LDS words next round
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Lean steady-state kernel (the two-pass plan's first pass): one lane per
+// group, takes exactly the groups that are in the compressed steady state
+// (SSYNC: one 16-B record for term / LastApplied / CommitIndex rows), that
+// no EXT isolation window touches this tick (drifted ring phases included);
+// every other live group goes to the list that
+// tick_list_kernel (the full fast_group) runs right after. For a taken
+// group the tick of fast_group reduces to closed form (all R logs end at
+// L = LastApplied with an entry of the leader's term T, the followers share
+// one CommitIndex cf, leader's CommitIndex cl):
+//   client append of n entries (main.go:327-329) -> LastApplied L+n;
+//   one AppendEntries per follower with prevLogIndex L, prevLogTerm T and the
+//   n entries (main.go:341-372): each accepts (main.go:121-156: same term,
+//   prevIdx = its length, log[L].term = T), appends, takes CommitIndex
+//   max(cf, cl) (min(LeaderCommit, len+1) / min(LeaderCommit, last new)),
+//   MatchIndex = L+n (main.go:375-377), timer reset (hb = now);
+//   commit rule (main.go:381-391): all R-1 peers at L+n -> cl' = L+n if
+//   2(R-1) > R and L+n > cl; RAFT (majority order statistic incl. the
+//   leader, entry of the current term): cl' = max(cl, L+n).
+// Per group it reads gmeta 2 B + gss 16 B + grot 2 B and writes gss 16 B,
+// hb 4 B and the entries (12·n·R B, +4·n·R with CRC32C) as whole ring rows
+// (a drifted group: its own R-contiguous segment, or a ring segment switch).
+template <int R, bool CRC, int SEM>
+__global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, unsigned long long* stats, uint32_t* list,
+                                                        uint32_t* count) {
+  constexpr bool RAFT = SEM == SEM_RAFT;
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  __shared__ uint32_t tab[CRC ? 2048 : 1];
+  stage_crc_tab<CRC>(P, tab);
+  const int n = int(T.client_entries());
+  const int ph = int(T.entries_before(T.tick) & P.kmask);   // global ring phase of this tick's first entry
+  bool take = false, pass = false;
+  int committed = 0, w_term = 0, w_slot = -1;   // w_slot >= 0: drifted lane, its own segment from that slot
+  uint64_t w_vb = 0;
+  uint32_t df = 0;
+  if (g < P.G) {
+    const int meta = at(P.gmeta, g);
+    const int c = meta & 0xF;
+    const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
+    take = !skip && (meta & M_SSYNC) && c < R;
+    pass = !skip && !take;
+    df |= skip ? 1u : 0u;
+    if (take) {
+      const SsRec s = P.gss[g];
+      const uint64_t key = group_key(T.seed, P.gbase + g);
+      if (T.iso_p) {   // any window over this group this tick (either mode): the list kernel
+        uint32_t act = 0, starting = 0;
+        const uint32_t im = iso_windows<R>(key, T, &act, &starting);
+        if (T.iso_leader ? act != 0u : im != 0u) take = false;
+      }
+      const int L = s.last;
+      take &= L > 0 && int64_t(L) + n <= I32MAX && n < int(P.K);
+      // ring phase: a group whose logs stood still under churn appends out of
+      // the global phase (drifted); it switches its ring segment in place
+      // when that is safe (ring_slot; as fast_group), else writes its own
+      // R-contiguous segment at its own slot
+      const int rot = at(P.grot, g);
+      const int wph = (L + rot) & int(P.kmask);
+      int sw_d = 0;   // segment switch by this rotation jump (placement only, stored once the lane is taken)
+      if (take && n && wph != ph) {
+        const uint32_t d = uint32_t(ph - wph) & P.kmask;
+        df |= d <= P.K ? 8u : 16u;
+        bool sw = false;
+        if (P.KP > P.K && d <= P.K) {
+          const int sbo = at(P.gsb, g);
+          sw = sbo <= 1 || sbo <= L - int(P.K) + 1;   // the previous segment holds no readable entry
+        }
+        if (sw) sw_d = int(d);
+        else w_slot = wph;
+      }
+      const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+      if constexpr (CRC) {   // EXT: every follower verifies the stamp of each entry it received
+        if (take && n) {
+          uint32_t cm = 0;   // followers whose message is corrupted this tick: the list kernel (rejection)
+#pragma unroll
+          for (int p = 0; p < R; ++p)
+            if (p != c && P.corrupt_p && (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(T.tick)) & 0xFFFF) < P.corrupt_p)
+              cm |= 1u << p;
+          uint32_t bad = 0;   // (as fast_group: each follower checks the copy it received)
+          const uint32_t cs = crc_term_state(tab, s.term);
+          for (int e = 0; e < n; ++e) {
+            const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+            const uint32_t stamp = crc_value_final(tab, cs, v);   // leader's stamp
+#pragma unroll
+            for (int p = 0; p < R; ++p) {
+              if (p == c) continue;
+              const int64_t rv = v ^ ((((cm >> p) & 1u) && e == n - 1) ? 1 : 0);   // what p received
+              if (crc_value_final(tab, cs, rv) != stamp) bad |= 1u << p;
+            }
+          }
+          take &= bad == 0u;
+        }
+      }
+      if (take) {
+        const int nl = L + n;
+        int cl2 = s.cl;
+        if (RAFT ? nl > s.cl : (2 * (R - 1) > R && nl > s.cl)) cl2 = nl;
+        const int cf2 = s.cl > s.cf ? s.cl : s.cf;
+        P.gss[g] = SsRec{nl, s.term, cl2, cf2};
+        at(P.hb, g) = T.now;                               // timer.Reset(d) of every follower
+        if (sw_d) {   // the new segment starts at this tick's first entry
+          at(P.grota, g) = uint16_t(rot);
+          at(P.gsb, g) = L + 1;
+          at(P.grot, g) = uint16_t((rot + sw_d) & int(P.kmask));
+          df |= 32u;
+        }
+        committed = cl2 - s.cl;
+        w_term = s.term;
+        w_vb = vb;
+        df |= 262144u | (w_slot < 0 ? 256u : 512u);
+      } else {
+        pass = true;
+      }
+    }
+  }
+  // this tick's entries: the taken lanes at the global phase as whole ring
+  // rows, all R replicas (the cooperative row stores of fast_group); a
+  // drifted lane its own R-contiguous segment
+  const bool wr = take && n && w_slot < 0;
+  const bool wd = take && n && w_slot >= 0;
+  if (__ballot(wr || wd)) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g), P.KP, R);
+    int32_t* const rt = P.log_term + tb;
+    int64_t* const rv = P.log_value + tb;
+    uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
+    uint32_t cs = 0;
+    if constexpr (CRC) cs = crc_term_state(tab, w_term);
+    int k_term[R], k_src[R];
+    bool k_on[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int src = (k * 64 + lane) / R;
+      k_src[k] = src;
+      k_term[k] = __shfl(w_term, src);
+      k_on[k] = __shfl(int(wr), src) != 0;
+    }
+    for (int e = 0; e < n; ++e) {
+      const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
+      uint32_t stamp = 0;
+      if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+      const uint32_t row = uint32_t((ph + e) & int(P.kmask)) * 64u * R;
+      const int vlo = int(uint32_t(uint64_t(v))), vhi = int(uint32_t(uint64_t(v) >> 32));
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int lo = __shfl(vlo, k_src[k]), hi = __shfl(vhi, k_src[k]);
+        uint32_t sk = 0;
+        if constexpr (CRC) sk = uint32_t(__shfl(int(stamp), k_src[k]));
+        if (k_on[k]) {
+          const uint32_t o = row + uint32_t(k * 64 + lane);
+          at(rt, o) = k_term[k];
+          at(rv, o) = int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
+          if constexpr (CRC) at(rc, o) = sk;
+        }
+      }
+      if (wd) {
+        const uint32_t o = ring_in_tile(g, R, uint32_t((w_slot + e) & int(P.kmask)), 0u);
+        fill_seg<R>(rt + o, w_term);
+        fill_seg<R>(rv + o, v);
+        if constexpr (CRC) fill_seg<R>(rc + o, stamp);
+      }
+    }
+  }
+  if (P.dbg) {   // diagnostics (same class bits as fast_group): lanes, skipped, taken by the lean pass
+    df |= (g < P.G) ? 1024u : 0u;
+#pragma unroll 1
+    for (int k = 0; k < 19; ++k) {
+      const uint64_t b = __ballot((df >> k) & 1u);
+      if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
+    }
+  }
+  // the rest go to the list kernel: block-local prefix, one atomic per block
+  // on the block's shard of the list
+  __shared__ uint32_t wn[4], wbase;
+  const uint64_t bm = __ballot(pass);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t k = blockIdx.x & uint32_t(NSHARD - 1);
+  if (lane == 0) wn[wave] = uint32_t(__popcll(bm));
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = wn[0] + wn[1] + wn[2] + wn[3];
+    wbase = tot ? atomicAdd(&count[k * SHARD_STRIDE], tot) : 0u;
+  }
+  __syncthreads();
+  if (pass) {
+    uint32_t off = k * P.scap + wbase + uint32_t(__popcll(bm & ((1ull << lane) - 1ull)));
+    for (int w = 0; w < wave; ++w) off += wn[w];
+    list[off] = g;
+  }
+  if (stats) {
+    const int t = take ? 1 : 0;
+    if constexpr (RAFT) {
+      const int v[5] = {committed, t * (R - 1), 0, t, 0};
+      const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
+      block_stats<5>(v, idx, stats);
+    } else {
+      const int v[4] = {committed, t * (R - 1), 0, t};
+      const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
+      block_stats<4>(v, idx, stats);
     }
   }
 }
@@ -800,6 +1085,57 @@ hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, 
     if (crc) { RAFT_FAST(false, true); } else { RAFT_FAST(false, false); }
   }
 #undef RAFT_FAST
+  return hipGetLastError();
+}
+
+// Resident blocks of a kernel (CUs x blocks per CU at its occupancy), per device.
+template <typename Kern>
+static unsigned resident_blocks_fast(Kern k) {
+  constexpr int MAXDEV = 64;
+  static unsigned resident_of[MAXDEV] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  unsigned& resident = resident_of[dev % MAXDEV];
+  if (!resident) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 256, 0) == hipSuccess && cus > 0 && per > 0)
+      resident = unsigned(cus) * unsigned(per);
+    else
+      resident = 2048;
+  }
+  return resident;
+}
+
+template <int R, bool CRC, int SEM>
+static void launch_two_pass_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                              int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
+                              uint32_t* next_count, hipStream_t s, hipEvent_t a, hipEvent_t b, hipEvent_t c,
+                              hipEvent_t d) {
+  hipExtLaunchKernelGGL(tick_lean_kernel<R, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, list,
+                        count);
+  const unsigned blocks =
+      unsigned(std::min<uint64_t>((P.G + 255) / 256, resident_blocks_fast(tick_list_kernel<R, false, CRC, SEM>)));
+  hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats,
+                        work, work_tick, work_count, list, count, next_count);
+}
+hipError_t launch_tick_two_pass(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats,
+                                uint32_t* work, int32_t* work_tick, uint32_t* work_count, uint32_t* list,
+                                uint32_t* count, uint32_t* next_count, hipStream_t s, hipEvent_t lean_start,
+                                hipEvent_t lean_stop, hipEvent_t list_start, hipEvent_t list_stop) {
+  const bool crc = P.crc_on != 0;
+#define RAFT_TWO(CRC_)                                                                                            \
+  if (sem == SEM_RAFT) {                                                                                           \
+    RAFT_DISPATCH_R(R, (launch_two_pass_t<RR, CRC_, SEM_RAFT>(P, T, stats, work, work_tick, work_count, list, count, \
+                                                              next_count, s, lean_start, lean_stop, list_start,      \
+                                                              list_stop)))                                           \
+  } else {                                                                                                         \
+    RAFT_DISPATCH_R(R, (launch_two_pass_t<RR, CRC_, SEM_REF>(P, T, stats, work, work_tick, work_count, list, count,  \
+                                                             next_count, s, lean_start, lean_stop, list_start,       \
+                                                             list_stop)))                                            \
+  }
+  if (crc) { RAFT_TWO(true); } else { RAFT_TWO(false); }
+#undef RAFT_TWO
   return hipGetLastError();
 }
 

@@ -12,12 +12,13 @@ __global__ __launch_bounds__(256) void init_new_kernel(DevPlanes P, Trace T) {
   const uint64_t key = group_key(T.seed, P.gbase + g);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const uint64_t i = g * uint64_t(R) + uint64_t(r);   // group-major [Gp][R] (rix)
+    const uint32_t i = rix<R>(uint32_t(g), r);   // group record (rix)
     const int d = T.f_min + int(uint32_t(rng_k(key, r, ST_TIMER_F, uint64_t(T.tick)) >> 32) % uint32_t(T.f_span));
     P.term[i] = 0; P.last[i] = 0; P.commit[i] = 0;
     P.tstart[i] = T.now;
-    P.rs[i] = uint16_t(ROLE_F | (uint32_t(d) << 6));   // vote 0 (REF: not voted; RAFT: votedFor none)
+    P.rs[i] = int32_t(ROLE_F | (uint32_t(d) << 6));   // vote 0 (REF: not voted; RAFT: votedFor none)
     P.lterm[i] = 0;
+    P.lmatch[i] = 0;
     if (P.hwm) P.hwm[i] = 0;
   }
   P.hb[g] = HB_NONE;
@@ -38,7 +39,7 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
   const int L = leader >= 0 ? leader % R : int(uint32_t(sm64(T.seed ^ 0x1EADE5ULL ^ sm64(gid)) >> 33) % uint32_t(R));
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const uint64_t i = g * uint64_t(R) + uint64_t(r);   // group-major [Gp][R] (rix)
+    const uint32_t i = rix<R>(uint32_t(g), r);   // group record (rix)
     const bool isL = r == L;
     const uint64_t h = rng_k(key, r, isL ? ST_TIMER_C : ST_TIMER_F, uint64_t(T.tick));
     const int d = isL ? T.c_min + int(uint32_t(h >> 32) % uint32_t(T.c_span))
@@ -47,7 +48,7 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
     const uint32_t vote = P.hwm ? uint32_t(L + 1) : 1u;
     P.term[i] = 1; P.last[i] = 0; P.commit[i] = 0;
     P.tstart[i] = T.now;
-    P.rs[i] = uint16_t((isL ? ROLE_L : ROLE_F) | (vote << 2) | (uint32_t(d) << 6));
+    P.rs[i] = int32_t((isL ? ROLE_L : ROLE_F) | (vote << 2) | (uint32_t(d) << 6));
     P.lmatch[i] = 0;
     P.lterm[i] = 0;
     if (P.hwm) {                       // RAFT mode: NextIndex = last + 1 = 1, high-water 0

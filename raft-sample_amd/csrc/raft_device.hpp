@@ -59,7 +59,7 @@ struct DevPlanes {
   int32_t* commit;     // Node.CommitIndex          (main.go:24)
   int32_t* tstart;     // election timer start (virtual s); deadline = start + d
   int32_t* hb;         // [Gp] time of the last steady-state heartbeat that reset every follower
-  uint16_t* rs;        // role:2 | vote:4 | timer duration d:10 (main.go:16, 20, 114, 194);
+  int32_t* rs;         // role:2 | vote:4 | timer duration d:10 (main.go:16, 20, 114, 194);
                        // vote = Voted (REF) or votedFor+1 (RAFT, 0 = none)
   int32_t* lmatch;     // [Gp][R] MatchIndex row of the group's primary leader (main.go:29)
   int32_t* xmatch;     // [R][R][Gp] rows of any further concurrent leaders (EXT only)
@@ -86,7 +86,52 @@ struct DevPlanes {
   uint32_t KP;         // physical ring slots per replica: K, or 2K when segment switches are on
   uint32_t kmask;      // KP - 1 (physical slot mask)
   unsigned long long* dbg;  // diagnostics (RAFTSTEP_DEBUG_FAST): fast-kernel lane class counters, else null
+  int32_t* rec;        // [Gp][NPL][R] group records holding every per-replica row above (see rix)
+  uint32_t scap;       // capacity of one shard of a sharded group list (see below)
 };
+
+// Sharded group lists (the general kernel's worklist, the two-pass tick's
+// list). A returning device-scope atomicAdd on one word saturates at ~88 per
+// us (MI355X_MICROARCH.md, work queues), so one counter bumped once by each
+// of the ~16K blocks of a 4M-group launch costs ~190 us. A list is instead
+// NSHARD sub-lists, one counter each (64 B apart): group g belongs to shard
+// (g >> 8) & (NSHARD-1), the shard of its block in the dense launches, so a
+// dense block appends with one atomic on its own shard and every shard holds
+// at most scap = ceil(blocks / NSHARD) * 256 entries (each group is listed at
+// most once per list). Consumers take the block-level prefix over the NSHARD
+// counts and map a dense index to (shard, slot).
+constexpr int NSHARD = 64;
+constexpr int SHARD_STRIDE = 16;   // u32 words between two shard counters
+constexpr int SHARD_WORDS = NSHARD * SHARD_STRIDE;
+__device__ __forceinline__ uint32_t shard_home(uint32_t g) { return (g >> 8) & uint32_t(NSHARD - 1); }
+// pre[0..NSHARD] (LDS) = exclusive prefix of the shard counts; returns the total.
+// Block-wide: every thread calls it.
+__device__ __forceinline__ uint32_t shard_prefix(const uint32_t* cnt, uint32_t* pre) {
+  if (threadIdx.x < 64) {
+    const uint32_t v = threadIdx.x < uint32_t(NSHARD) ? cnt[threadIdx.x * SHARD_STRIDE] : 0u;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (int(threadIdx.x) >= o) x += y;
+    }
+    if (threadIdx.x < uint32_t(NSHARD)) pre[threadIdx.x + 1] = x;
+    if (threadIdx.x == 0) pre[0] = 0;
+  }
+  __syncthreads();
+  return pre[NSHARD];
+}
+// element index of dense position i < total
+__device__ __forceinline__ uint32_t shard_locate(const uint32_t* pre, uint32_t scap, uint32_t i) {
+  uint32_t k = 0;
+#pragma unroll
+  for (uint32_t step = NSHARD / 2; step > 0; step >>= 1)
+    if (pre[k + step] <= i) k += step;
+  return k * scap + (i - pre[k]);
+}
+__device__ __forceinline__ void shard_zero(uint32_t* cnt) {   // block 0, threads 0..NSHARD-1
+  if (blockIdx.x == 0 && threadIdx.x < uint32_t(NSHARD)) cnt[threadIdx.x * SHARD_STRIDE] = 0;
+}
 
 // Ring phase segments. A group whose logs stop growing for L ticks (no
 // leader under churn) comes back out of phase with the global slot
@@ -130,14 +175,20 @@ template <typename T>
 __device__ __forceinline__ T* prow(T* plane, int r, uint64_t Gp) {   // [..][Gp] row r (xmatch / xnext)
   return plane + uint64_t(r) * Gp;
 }
-// Per-replica scalar planes are group-major, [Gp][R]: replica r of group g
-// at element g*R + r. A group's R values are contiguous (28 B at R=7: one
-// line for the replica-parallel general kernel instead of R scattered
-// lines), and a lane's loads of one plane share one VGPR offset g*R*4 with
-// immediate offsets r*4. raft_engine_create keeps Gp*R*4 < 2^32.
+// Per-replica rows live in one record per group, [Gp][NPL][R] int32: row k
+// of group g is R contiguous words at (g*NPL + k)*R, and the plane pointers
+// term, last, ... are rec + k*R, so replica r of group g of any of them is
+// element rix(g, r) = g*NPL*R + r. A group's whole per-replica state is then
+// NPL*R*4 contiguous bytes (252 B at R=7): a scattered group (the list and
+// general kernels) costs 2-3 lines instead of one line per row, and a
+// block stages its groups' records into LDS with coalesced loads. A lane's
+// loads of one row still share one VGPR offset with immediate offsets r*4.
+// raft_engine_create keeps Gp*NPL*R*4 < 2^32.
+constexpr int NPL = 9;   // rows per record
+enum : int { PL_TERM = 0, PL_LAST, PL_COMMIT, PL_TSTART, PL_LTERM, PL_RS, PL_LMATCH, PL_LNEXT, PL_HWM };
 template <int R>
 __device__ __forceinline__ uint32_t rix(uint32_t g, int r) {
-  return g * uint32_t(R) + uint32_t(r);
+  return g * uint32_t(NPL * R) + uint32_t(r);
 }
 template <typename T>
 __device__ __forceinline__ T& at(T* base, uint32_t idx) {
@@ -423,7 +474,7 @@ struct Group {
       if ((d_dl >> r) & 1u) at(P.tstart, rix<R>(g, r)) = dl[r] - dur[r];
       if ((d_rs >> r) & 1u)
         at(P.rs, rix<R>(g, r)) =
-            uint16_t(((roles >> (2 * r)) & 3u) | (((votes >> (4 * r)) & 15u) << 2) | (uint32_t(dur[r]) << 6));
+            int32_t(((roles >> (2 * r)) & 3u) | (((votes >> (4 * r)) & 15u) << 2) | (uint32_t(dur[r]) << 6));
       if (SEM == SEM_RAFT && ((d_hw >> r) & 1u)) at(P.hwm, rix<R>(g, r)) = hw[r];
       if ((d_lt >> r) & 1u) at(P.lterm, rix<R>(g, r)) = ltm[r];
       if ((d_pm >> r) & 1u) at(P.lmatch, rix<R>(g, r)) = pm[r];

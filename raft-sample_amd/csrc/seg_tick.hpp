@@ -174,7 +174,7 @@ struct Seg {
       if (dirty & SD_LAST) at(P.last, ri) = last;
       if (dirty & SD_COMMIT) at(P.commit, ri) = commit;
       if (dirty & SD_DL) at(P.tstart, ri) = dl - dur;
-      if (dirty & SD_RS) at(P.rs, ri) = uint16_t(uint32_t(role) | (uint32_t(vote) << 2) | (uint32_t(dur) << 6));
+      if (dirty & SD_RS) at(P.rs, ri) = int32_t(uint32_t(role) | (uint32_t(vote) << 2) | (uint32_t(dur) << 6));
       if (SEM == SEM_RAFT && (dirty & SD_HW)) at(P.hwm, ri) = hw;
       if (dirty & SD_LT) at(P.lterm, ri) = ltm;
       if (dirty & SD_PM) at(P.lmatch, ri) = pm;

@@ -196,7 +196,8 @@ class Engine:
 
     # -- instrumentation -----------------------------------------------
     def profile(self, mode=1):
-        """0 off, 1 per-dispatch kernel events, 2 one event pair per tick() call."""
+        """0 off, 1 per-dispatch events on the steady-state kernel, 2 one event pair per tick()
+        call, 3 per-dispatch events on the two-pass plan's list kernel."""
         _check(self.lib.raft_profile_enable(self.h, int(mode)))
 
     def profile_read(self):

@@ -92,13 +92,23 @@ def test_engine_create_rejects_bad_configs_before_touching_a_gpu(field, value, m
     assert msg in lib.raft_last_error().decode()
 
 
+NPL = 9   # int32 rows per group record (raft_device.hpp): padded groups * NPL * R * 4 must stay below 2^32
+
+
 def test_largest_engine_size_is_accepted_by_validation():
-    """groups * R = 2^30 - 256 * R passes the size checks (then fails only for lack of a device here)."""
+    """The largest group count whose records keep 32-bit byte offsets passes the
+    size checks (then fails only for lack of a device here); one more block of
+    256 groups is refused."""
     lib = engine.load_library()
-    c = abi.default_config(replicas=1, groups=(1 << 30) - 256)
-    h = C.c_void_p()
-    rc = lib.raft_engine_create(C.byref(c), C.byref(h))
-    assert rc != abi.RAFT_EINVAL or "too many groups" not in lib.raft_last_error().decode()
+    for R in (1, 5, 7):
+        top = ((1 << 32) - 1) // (NPL * R * 4) // 256 * 256
+        c = abi.default_config(replicas=R, groups=top)
+        h = C.c_void_p()
+        rc = lib.raft_engine_create(C.byref(c), C.byref(h))
+        assert rc != abi.RAFT_EINVAL or "too many groups" not in lib.raft_last_error().decode()
+        c = abi.default_config(replicas=R, groups=top + 1)
+        rc = lib.raft_engine_create(C.byref(c), C.byref(h))
+        assert rc == abi.RAFT_EINVAL and "too many groups" in lib.raft_last_error().decode()
 
 
 def test_coerce_state_checks_dtype_shape_and_optional_fields():

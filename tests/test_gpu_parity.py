@@ -10,22 +10,26 @@ from raftstep import Engine, abi
 pytestmark = pytest.mark.gpu
 
 
-def pair(general=False, **kw):
+def pair(general=False, single=False, **kw):
     """(engine, oracle) on the same config. general=True routes every group
-    through the general tick kernel (debug knob RAFTSTEP_FORCE_GENERAL), so
-    both device paths are checked against the oracle on the same traces."""
+    through the general tick kernel (debug knob RAFTSTEP_FORCE_GENERAL);
+    single=True runs the one-pass steady-state kernel instead of the default
+    two-pass plan (lean kernel + list kernel, RAFTSTEP_TWO_PASS=0), so every
+    device path is checked against the oracle on the same traces."""
     import os
 
     import oracle
-    old = os.environ.get("RAFTSTEP_FORCE_GENERAL")
-    os.environ["RAFTSTEP_FORCE_GENERAL"] = "1" if general else "0"
+    env = {"RAFTSTEP_FORCE_GENERAL": "1" if general else "0", "RAFTSTEP_TWO_PASS": "0" if single else "1"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         e = Engine(**kw)
     finally:
-        if old is None:
-            del os.environ["RAFTSTEP_FORCE_GENERAL"]
-        else:
-            os.environ["RAFTSTEP_FORCE_GENERAL"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     return e, oracle.Oracle(**kw)
 
 
@@ -106,11 +110,11 @@ TRACES = {
 }
 
 
-@pytest.mark.parametrize("path", ["auto", "general"])
+@pytest.mark.parametrize("path", ["auto", "single", "general"])
 @pytest.mark.parametrize("name", sorted(TRACES))
 def test_tick_trace(name, path):
     kw, init, t0, n, every = TRACES[name]
-    e, o = pair(general=(path == "general"), **kw)
+    e, o = pair(general=(path == "general"), single=(path == "single"), **kw)
     for x in (e, o):
         if init == "new":
             x.init_new_nodes(t0)

@@ -10,6 +10,7 @@ from raftstep import Engine
 pytestmark = pytest.mark.gpu
 
 PATHS = {"auto": {"RAFTSTEP_FORCE_GENERAL": "0"},
+         "single": {"RAFTSTEP_FORCE_GENERAL": "0", "RAFTSTEP_TWO_PASS": "0"},
          "general": {"RAFTSTEP_FORCE_GENERAL": "1"},
          "general_lane": {"RAFTSTEP_FORCE_GENERAL": "1", "RAFTSTEP_GENERAL": "lane"}}
 
