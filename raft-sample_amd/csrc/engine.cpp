@@ -270,15 +270,17 @@ int h2d(raft_engine* e, T* d, const std::vector<T>& h) {
 }
 
 // Group records <-> per-row host arrays [Gp][R] (row k of group g at
-// blk[(g*NPL + k)*R ..], raft_device.hpp rix)
+// blk[g*recw + k*R ..], raft_device.hpp rix)
 void rec_rows(const std::vector<int32_t>& blk, int k, uint64_t R, uint64_t Gp, std::vector<int32_t>& out) {
+  const uint64_t W = recw_of(uint32_t(R));
   out.resize(R * Gp);
   for (uint64_t g = 0; g < Gp; ++g)
-    std::memcpy(&out[g * R], &blk[(g * NPL + uint64_t(k)) * R], R * 4);
+    std::memcpy(&out[g * R], &blk[g * W + uint64_t(k) * R], R * 4);
 }
 void rec_put(std::vector<int32_t>& blk, int k, uint64_t R, uint64_t Gp, const std::vector<int32_t>& rows) {
+  const uint64_t W = recw_of(uint32_t(R));
   for (uint64_t g = 0; g < Gp; ++g)
-    std::memcpy(&blk[(g * NPL + uint64_t(k)) * R], &rows[g * R], R * 4);
+    std::memcpy(&blk[g * W + uint64_t(k) * R], &rows[g * R], R * 4);
 }
 
 }  // namespace
@@ -335,8 +337,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   // device addressing (raft_device.hpp at(), rix()): 64-bit plane/tile bases,
   // 32-bit per-lane BYTE offsets, so the group records (NPL rows of R 4-B
   // words) must satisfy Gp*NPL*R*4 < 2^32 (ring tiles: KP*64*R*8 < 2^26)
-  if (Gp * NPL * c.replicas * 4 > uint64_t(0xFFFFFFFFu))
-    return fail(RAFT_EINVAL, "too many groups for one engine (need groups * replicas * %d * 4 < 2^32)", NPL);
+  if (Gp * recw_of(c.replicas) * 4 > uint64_t(0xFFFFFFFFu))
+    return fail(RAFT_EINVAL, "too many groups for one engine (need groups * %u * 4 < 2^32)", recw_of(c.replicas));
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RAFT_ENODEV, "no HIP device");
   if (c.device < 0 || c.device >= ndev) return fail(RAFT_ENODEV, "device %d out of range", c.device);
@@ -360,7 +362,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->KP = K;
   const bool raft = c.semantics == RAFT_SEM_RAFT;
   // group records: every per-replica row of a group in NPL*R contiguous words
-  A(reinterpret_cast<void**>(&e->P.rec), Gp * NPL * R * 4);
+  A(reinterpret_cast<void**>(&e->P.rec), Gp * recw_of(R) * 4);
   if (rc == RAFT_OK) {
     int32_t* rec = e->P.rec;
     e->P.term = rec + PL_TERM * R;
@@ -434,7 +436,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   // zero everything once so that padding / unused rows are deterministic
   for (void* p : e->allocs) (void)p;
   hipError_t z = hipSuccess;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.rec, 0, Gp * NPL * R * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.rec, 0, Gp * recw_of(R) * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.hb, 0x80, Gp * 4, e->stream) : z;  // 0x80808080 < any time
   z = z == hipSuccess ? hipMemsetAsync(e->P.xmatch, 0, R * R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(e->P.gmeta), uint16_t(NO_PRIMARY), Gp,
@@ -515,7 +517,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   std::vector<int64_t> lv;
   std::vector<uint32_t> lcrc;
   int rc = RAFT_OK;
-  if (!rc) rc = d2h(e, blk, e->P.rec, Gp * NPL * R);   // group records (rows extracted below)
+  if (!rc) rc = d2h(e, blk, e->P.rec, Gp * recw_of(R));   // group records (rows extracted below)
   if (!rc) rc = d2h(e, hb, e->P.hb, Gp);
   if (!rc) rc = d2h(e, xm, e->P.xmatch, R * R * Gp);
   if (!rc) rc = d2h(e, meta, e->P.gmeta, Gp);
@@ -709,7 +711,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
       if (v->last[c] > 0) ltm[d] = v->log_term[c * K + uint64_t((v->last[c] - 1) & int64_t(K - 1))];
     }
   }
-  std::vector<int32_t> blk(Gp * NPL * R, 0);   // group records
+  std::vector<int32_t> blk(Gp * recw_of(R), 0);   // group records
   rec_put(blk, PL_TERM, R, Gp, term);
   rec_put(blk, PL_LAST, R, Gp, last);
   rec_put(blk, PL_COMMIT, R, Gp, commit);
@@ -1102,7 +1104,7 @@ int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap) {
   const int pr = meta & 0xF;
   const bool ssync = (meta & M_SSYNC) && pr < int(e->cfg.replicas);   // compressed state
   for (uint32_t r = 0; r < e->cfg.replicas; ++r) {
-    const uint64_t d = group * NPL * e->cfg.replicas + r;   // group record (rix)
+    const uint64_t d = group * recw_of(e->cfg.replicas) + r;   // group record (rix)
     int32_t term = 0, commit = 0, last = 0, rs = 0;
     HIPCHK(hipMemcpyAsync(&term, e->P.term + d, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&commit, e->P.commit + d, 4, hipMemcpyDeviceToHost, e->stream));

@@ -58,8 +58,7 @@ typedef int32_t row2 __attribute__((ext_vector_type(2), aligned(4)));
 typedef int32_t row3 __attribute__((ext_vector_type(3), aligned(4)));
 typedef int32_t row4 __attribute__((ext_vector_type(4), aligned(4)));
 template <int R>
-__device__ __forceinline__ void load_row(const int32_t* plane, uint32_t g, int (&o)[R]) {
-  const int32_t* q = &at(plane, rix<R>(g, 0));
+__device__ __forceinline__ void load_row_p(const int32_t* q, int (&o)[R]) {
 #pragma unroll
   for (int i = 0; i + 4 <= R; i += 4) {
     const row4 a = *reinterpret_cast<const row4*>(q + i);
@@ -71,14 +70,81 @@ __device__ __forceinline__ void load_row(const int32_t* plane, uint32_t g, int (
   if constexpr (rem == 1) o[b] = q[b];
 }
 template <int R>
-__device__ __forceinline__ void store_row(int32_t* plane, uint32_t g, const int (&v)[R]) {
-  int32_t* q = &at(plane, rix<R>(g, 0));
+__device__ __forceinline__ void store_row_p(int32_t* q, const int (&v)[R]) {
 #pragma unroll
   for (int i = 0; i + 4 <= R; i += 4) *reinterpret_cast<row4*>(q + i) = row4{v[i], v[i + 1], v[i + 2], v[i + 3]};
   constexpr int b = R & ~3, rem = R & 3;
   if constexpr (rem == 3) *reinterpret_cast<row3*>(q + b) = row3{v[b], v[b + 1], v[b + 2]};
   if constexpr (rem == 2) *reinterpret_cast<row2*>(q + b) = row2{v[b], v[b + 1]};
   if constexpr (rem == 1) q[b] = v[b];
+}
+
+// Row and per-group word access of one group inside fast_group: in the
+// dense launches its record in HBM (the SGPR plane base and a 32-bit lane
+// offset) and the per-group planes at g; in the list kernel the lane's LDS
+// copies (pointers derived from the __shared__ arrays, so the accesses are
+// ds_ instructions: a flat access would wait on every outstanding global
+// store, vmcnt counting stores on gfx950).
+template <int R, bool LDS>
+struct RowAcc {
+  int32_t* base;   // global: P.rec; LDS: the lane's record copy
+  uint32_t o;      // global: g * recw (element offset); LDS: 0
+  __device__ __forceinline__ int32_t& at(int k, int r) const {
+    if constexpr (LDS) return base[k * R + r];
+    else return raftstep::at(base, o + uint32_t(k * R + r));
+  }
+  template <bool WT>
+  __device__ __forceinline__ void st(int k, int r, int32_t v) const {
+    if constexpr (LDS) base[k * R + r] = v;
+    else raftstep::st<WT>(base, o + uint32_t(k * R + r), v);
+  }
+  __device__ __forceinline__ void load(int k, int (&a)[R]) const {
+    if constexpr (LDS) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) a[r] = base[k * R + r];
+    } else {
+      load_row_p<R>(&raftstep::at(base, o + uint32_t(k * R)), a);
+    }
+  }
+  __device__ __forceinline__ void store(int k, const int (&a)[R]) const {
+    if constexpr (LDS) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) base[k * R + r] = a[r];
+    } else {
+      store_row_p<R>(&raftstep::at(base, o + uint32_t(k * R)), a);
+    }
+  }
+};
+template <bool LDS>
+struct WordAcc {
+  // global: the plane bases and g; LDS: the lane's slots (g unused)
+  uint16_t* meta_;
+  uint16_t* rot_;
+  uint16_t* rota_;
+  uint8_t* iso_;
+  int32_t* hb_;
+  int32_t* sb_;
+  SsRec* ss_;
+  uint32_t g;
+  __device__ __forceinline__ uint16_t& meta() const { if constexpr (LDS) return *meta_; else return raftstep::at(meta_, g); }
+  __device__ __forceinline__ uint16_t& rot() const { if constexpr (LDS) return *rot_; else return raftstep::at(rot_, g); }
+  __device__ __forceinline__ uint16_t& rota() const { if constexpr (LDS) return *rota_; else return raftstep::at(rota_, g); }
+  __device__ __forceinline__ uint8_t& iso() const { if constexpr (LDS) return *iso_; else return raftstep::at(iso_, g); }
+  __device__ __forceinline__ int32_t& hb() const { if constexpr (LDS) return *hb_; else return raftstep::at(hb_, g); }
+  __device__ __forceinline__ int32_t& sb() const { if constexpr (LDS) return *sb_; else return raftstep::at(sb_, g); }
+  __device__ __forceinline__ SsRec& ss() const { if constexpr (LDS) return *ss_; else return ss_[g]; }
+  template <bool WT>
+  __device__ __forceinline__ void st_hb(int32_t v) const {
+    if constexpr (LDS) *hb_ = v;
+    else raftstep::st<WT>(hb_, g, v);
+  }
+};
+template <int R>
+__device__ __forceinline__ RowAcc<R, false> rows_global(const DevPlanes& P, uint32_t g) {
+  return RowAcc<R, false>{P.rec, rix<R>(g, 0)};
+}
+__device__ __forceinline__ WordAcc<false> words_global(const DevPlanes& P, uint32_t g) {
+  return WordAcc<false>{P.gmeta, P.grot, P.grota, P.giso, P.hb, P.gsb, P.gss, g};
 }
 
 // A ONECAND group is taken only when a replica is isolated this tick (its
@@ -97,18 +163,19 @@ __device__ __forceinline__ bool xi_ok(int meta, int xi) {
 // of a group between a disruption and its next election, so the tick is
 // taken here instead of deferring the group. Conservative: anything else
 // (a second candidate, a grant, a term to adopt, a timer due) defers.
-template <int R, bool RAFT>
-__device__ __forceinline__ bool quiet_leaderless(const DevPlanes& P, const Trace& T, uint32_t g, uint64_t key) {
+template <int R, bool RAFT, class Rows, class Words>
+__device__ __forceinline__ bool quiet_leaderless(const DevPlanes& P, const Trace& T, const Rows& RW, const Words& GW,
+                                                 uint64_t key) {
   if (R < 2) return false;   // a lone candidate would win its round
   int term[R], last[R], lt[R], ts[R];
-  load_row<R>(P.term, g, term);
-  load_row<R>(P.last, g, last);
-  load_row<R>(P.lterm, g, lt);
-  load_row<R>(P.tstart, g, ts);
-  const int hb = at(P.hb, g);
+  RW.load(PL_TERM, term);
+  RW.load(PL_LAST, last);
+  RW.load(PL_LTERM, lt);
+  RW.load(PL_TSTART, ts);
+  const int hb = GW.hb();
   int rs[R];   // role:2 | vote:4 | d:10
 #pragma unroll
-  for (int r = 0; r < R; ++r) rs[r] = at(P.rs, rix<R>(g, r));
+  for (int r = 0; r < R; ++r) rs[r] = RW.at(PL_RS, r);
   int c = -1;
   bool quiet = true;
 #pragma unroll
@@ -126,7 +193,7 @@ __device__ __forceinline__ bool quiet_leaderless(const DevPlanes& P, const Trace
     im = iso_windows<R>(key, T, &act, &starting);
     if (T.iso_leader) {   // a window starting now is decided (and recorded) by the general kernel
       if (starting) return false;
-      uint32_t gi = act ? uint32_t(at(P.giso, g)) : 0u;
+      uint32_t gi = act ? uint32_t(GW.iso()) : 0u;
       im = leader_iso_mask(act, 0u, gi, 0u, false);
     }
   }
@@ -157,10 +224,10 @@ __device__ __forceinline__ bool quiet_leaderless(const DevPlanes& P, const Trace
 // over the list of groups the lean kernel passed on (tick_list_kernel, LIST:
 // the lanes of a wave hold scattered groups, so every ring write is the
 // lane's own). Block-uniform control flow (it reduces over the block).
-template <int R, bool WT, bool CRC, int SEM, bool LIST>
-__device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+template <int R, bool WT, bool CRC, int SEM, bool LIST, class Rows, class Words>
+__device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                                            int32_t* work_tick, uint32_t* work_count, int force_slow, const uint32_t g,
-                                           const uint32_t* tab) {
+                                           const uint32_t* tab, const Rows& RW, const Words& GW) {
   constexpr bool RAFT = SEM == SEM_RAFT;
   int sv[5] = {0, 0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups, term bumps
   bool bail = false;
@@ -170,6 +237,7 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
   int w_term = 0, w_ph = 0;    // their term and the ring slot of the first entry
   uint64_t w_vb = 0;    // value stream base of this tick's entries
   uint32_t df = 0;      // diagnostics: lane class bits (P.dbg)
+  bool stored = false;  // the group's rows may have been written (returned)
   // deferral-reason bits 11-15 only in a diagnostics build (make DIAG=1),
   // so the product kernel carries no extra instructions for them
 #ifdef RAFTSTEP_DIAG_REASONS
@@ -178,13 +246,13 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
 #define DIAG_REASON(x)
 #endif
   if (g < P.G) {
-    const int meta = at(P.gmeta, g);
+    const int meta = GW.meta();
     const int c = meta & 0xF;
     const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
     // RAFT also takes ONECAND groups (their candidate must be isolated this tick, checked below)
     bail = !skip && (force_slow || !(meta & (RAFT ? (M_STEADY | M_ONECAND | M_ONESTALE) : M_STEADY)));
     if (bail && !force_slow && c == NO_PRIMARY) {   // leaderless: a quiet tick needs no general kernel
-      const bool q = quiet_leaderless<R, RAFT>(P, T, g, T.iso_p ? group_key(T.seed, P.gbase + g) : 0ull);
+      const bool q = quiet_leaderless<R, RAFT>(P, T, RW, GW, T.iso_p ? group_key(T.seed, P.gbase + g) : 0ull);
       bail = !q;
       df |= q ? 65536u : 0u;
     }
@@ -203,16 +271,16 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
     DIAG_REASON(df |= bail ? 2048u : 0u;);   // diagnostics: deferral reason "group not steady"
     if (go) {
       if (ss) {
-        const SsRec ss_rec = P.gss[g];
+        const SsRec ss_rec = GW.ss();
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           term[r] = ss_rec.term; last[r] = ss_rec.last; commit[r] = r == c ? ss_rec.cl : ss_rec.cf; lt[r] = ss_rec.term;
         }
       } else {
-        load_row<R>(P.term, g, term);
-        load_row<R>(P.last, g, last);
-        load_row<R>(P.commit, g, commit);
-        load_row<R>(P.lterm, g, lt);
+        RW.load(PL_TERM, term);
+        RW.load(PL_LAST, last);
+        RW.load(PL_COMMIT, commit);
+        RW.load(PL_LTERM, lt);
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) empty &= last[r] == 0;
@@ -221,17 +289,17 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
         for (int r = 0; r < R; ++r) m[r] = (r != c) ? last[r] : 0;
       } else {
 #pragma unroll
-        for (int r = 0; r < R; ++r) m[r] = (r != c) ? at(P.lmatch, rix<R>(g, r)) : 0;
+        for (int r = 0; r < R; ++r) m[r] = (r != c) ? RW.at(PL_LMATCH, r) : 0;
         if constexpr (RAFT) {
           // RAFT rows kept explicitly: NextIndex must be MatchIndex+1 and no
           // log may be shorter than its high-water mark (no pending truncation)
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            if (r != c && at(P.lnext, rix<R>(g, r)) != m[r] + 1) rowbad |= 1u << r;
+            if (r != c && RW.at(PL_LNEXT, r) != m[r] + 1) rowbad |= 1u << r;
             // a log truncated below its high-water mark stays in step as long as
             // the entry this tick's AppendEntries checks (its last) is still
             // inside the ring window (hwm-K, last] (Group::r_deliver_ae's evicted rule)
-            const int hwd = at(P.hwm, rix<R>(g, r)) - last[r];
+            const int hwd = RW.at(PL_HWM, r) - last[r];
             if (hwd < 0 || hwd >= int(P.K)) rowbad |= 1u << r;
             if (hwd > 0) hwup |= 1u << r;
           }
@@ -255,7 +323,7 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
       uint32_t im = iso_windows<R>(key, T, &act, &starting);
       if (T.iso_leader) {   // leader mode: a window starting now is decided by the general kernel
         if (starting) bail = true;
-        uint32_t gi = act ? uint32_t(at(P.giso, g)) : 0u;
+        uint32_t gi = act ? uint32_t(GW.iso()) : 0u;
         im = leader_iso_mask(act, 0u, gi, 0u, false);
       }
       if (RAFT && R >= 3 && im && (im & (im - 1u)) == 0u && int(__builtin_ctz(im)) != c) xi = int(__builtin_ctz(im));
@@ -290,11 +358,11 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
 #pragma unroll
       for (int p = 0; p < R; ++p) bail |= p != c && m[p] != last[p];
       int ts[R], rsv[R];
-      load_row<R>(P.tstart, g, ts);
-      const int hbt = at(P.hb, g);
+      RW.load(PL_TSTART, ts);
+      const int hbt = GW.hb();
 #pragma unroll
       for (int p = 0; p < R; ++p) {
-        rsv[p] = at(P.rs, rix<R>(g, p));
+        rsv[p] = RW.at(PL_RS, p);
         if (p != c) bail |= max(ts[p], hbt) + (rsv[p] >> 6) <= T.now;   // a follower's election timeout is due
       }
       // commitIndex: the largest N held by a majority (leader included), if
@@ -317,14 +385,14 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
       if (!bail) {
         df |= 131072u;
         if (ss) {   // the record's rows become explicit (the leader's elements change below)
-          const SsRec ss_rec = P.gss[g];   // (re-read: rare, keeps it out of the live registers)
+          const SsRec ss_rec = GW.ss();   // (re-read: rare, keeps it out of the live registers)
           int trow[R], lrow[R], crow[R];
 #pragma unroll
           for (int p = 0; p < R; ++p) { trow[p] = ss_rec.term; lrow[p] = ss_rec.last; crow[p] = p == c ? ss_rec.cl : ss_rec.cf; }
-          store_row<R>(P.term, g, trow);
-          store_row<R>(P.last, g, lrow);
-          store_row<R>(P.commit, g, crow);
-          store_row<R>(P.lterm, g, trow);
+          RW.store(PL_TERM, trow);
+          RW.store(PL_LAST, lrow);
+          RW.store(PL_COMMIT, crow);
+          RW.store(PL_LTERM, trow);
         }
         sv[0] = cm - Lc;
         sv[1] = 0;
@@ -332,16 +400,16 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
         sv[3] = 1;
         sv[4] = 0;
         if (n) {
-          st<WT>(P.last, rix<R>(g, c), Ll + n);
-          if (Llt != Lt) st<WT>(P.lterm, rix<R>(g, c), Lt);
+          RW.template st<WT>(PL_LAST, c, Ll + n);
+          if (Llt != Lt) RW.template st<WT>(PL_LTERM, c, Lt);
           wr = 1u << c;                                   // only the leader's log grows
           w_term = Lt;
-          w_ph = int((uint32_t(Ll) + uint32_t(at(P.grot, g))) & P.kmask);
+          w_ph = int((uint32_t(Ll) + uint32_t(GW.rot())) & P.kmask);
           w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
         }
-        if (cm != Lc) st<WT>(P.commit, rix<R>(g, c), cm);
+        if (cm != Lc) RW.template st<WT>(PL_COMMIT, c, cm);
         const int nm = (meta | M_MSYNC) & ~M_SSYNC;
-        if (nm != meta) at(P.gmeta, g) = uint16_t(nm);
+        if (nm != meta) GW.meta() = uint16_t(nm);
       }
     }
     const bool gom = go && !lx;   // the main steady-state path
@@ -363,7 +431,7 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
     int x_rs = 0, x_term = 0, x_fire = 0, x_dur = 0;
     if constexpr (RAFT) {
       if (gom && !bail && xi >= 0) {
-        x_rs = at(P.rs, rix<R>(g, xi));
+        x_rs = RW.at(PL_RS, xi);
         x_term = sel(term, xi);
         const int role = x_rs & 3;
         // STEADY: xi is a follower; ONECAND: the group's one candidate; ONESTALE: the stale leader
@@ -371,7 +439,7 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
         // (the stale leader appends at its own log's end with the ring rotation as it stands:
         // an empty group would pick a new phase, see below)
         if (stale && (x_term >= Lt || int64_t(sel(last, xi)) + n > I32MAX || empty)) bail = true;
-        const int dl = max(at(P.tstart, rix<R>(g, xi)), at(P.hb, g)) + (x_rs >> 6);
+        const int dl = max(RW.at(PL_TSTART, xi), GW.hb()) + (x_rs >> 6);
         if (!stale && dl <= T.now) {   // timer.C: Term++, vote for itself, new candidate timer (Raft §5.2)
           if (x_term >= I32MAX) bail = true;
           x_fire = 1;
@@ -455,7 +523,7 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
         for (int r = 0; r < R; ++r) {
           if (!((hwup >> r) & 1u)) continue;
           const int la = r == c ? Ll + n : last[r];   // (accepting followers' last already moved)
-          if (at(P.hwm, rix<R>(g, r)) > la) sync = false;
+          if (RW.at(PL_HWM, r) > la) sync = false;
         }
       }
       if constexpr (RAFT) {
@@ -496,18 +564,18 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
         if (p != c) keep_ss &= commit[p] == cf && last[p] == Ll + n && (n > 0 || lt[p] == Lt);
       if (keep_ss) {
         df |= 262144u;
-        P.gss[g] = SsRec{Ll + n, Lt, cm, cf};
-        st<WT>(P.hb, g, T.now);                                   // timer.Reset(d) of every follower
+        GW.ss() = SsRec{Ll + n, Lt, cm, cf};
+        GW.template st_hb<WT>(T.now);                                   // timer.Reset(d) of every follower
       } else {
       if (ss) {   // leaving the compressed form: the rows as they stood, then the element stores below
-        const SsRec ss_rec = P.gss[g];   // (re-read: rare, keeps it out of the live registers)
+        const SsRec ss_rec = GW.ss();   // (re-read: rare, keeps it out of the live registers)
         int trow[R], lrow[R], crow[R];
 #pragma unroll
         for (int p = 0; p < R; ++p) { trow[p] = ss_rec.term; lrow[p] = ss_rec.last; crow[p] = p == c ? ss_rec.cl : ss_rec.cf; }
-        store_row<R>(P.term, g, trow);
-        store_row<R>(P.last, g, lrow);
-        store_row<R>(P.commit, g, crow);
-        store_row<R>(P.lterm, g, trow);
+        RW.store(PL_TERM, trow);
+        RW.store(PL_LAST, lrow);
+        RW.store(PL_COMMIT, crow);
+        RW.store(PL_LTERM, trow);
       }
       const bool last_row = !WT && n && okm == peers;
       const bool commit_row = !WT && cm != Lc && cch == peers;
@@ -518,34 +586,34 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
           lrow[p] = p == c ? Ll + n : last[p];
           crow[p] = p == c ? cm : commit[p];
         }
-        if (last_row) store_row<R>(P.last, g, lrow);
-        if (commit_row) store_row<R>(P.commit, g, crow);
+        if (last_row) RW.store(PL_LAST, lrow);
+        if (commit_row) RW.store(PL_COMMIT, crow);
       }
       if (n) {
-        if (!last_row) st<WT>(P.last, rix<R>(g, c), Ll + n);
-        if (Llt != Lt) st<WT>(P.lterm, rix<R>(g, c), Lt);
+        if (!last_row) RW.template st<WT>(PL_LAST, c, Ll + n);
+        if (Llt != Lt) RW.template st<WT>(PL_LTERM, c, Lt);
       }
-      if (cm != Lc && !commit_row) st<WT>(P.commit, rix<R>(g, c), cm);
-      if (xi < 0) st<WT>(P.hb, g, T.now);                         // timer.Reset(d) of every follower
+      if (cm != Lc && !commit_row) RW.template st<WT>(PL_COMMIT, c, cm);
+      if (xi < 0) GW.template st_hb<WT>(T.now);                         // timer.Reset(d) of every follower
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == c || !((okm >> p) & 1u)) continue;
-        if (xi >= 0) st<WT>(P.tstart, rix<R>(g, p), T.now);   // xi isolated: reset each receiver, not hb
-        if (n && !last_row) st<WT>(P.last, rix<R>(g, p), last[p]);
-        if (!sync && ((mch >> p) & 1u)) st<WT>(P.lmatch, rix<R>(g, p), m[p]);
-        if (((cch >> p) & 1u) && !commit_row) st<WT>(P.commit, rix<R>(g, p), commit[p]);
-        if ((ltch >> p) & 1u) st<WT>(P.lterm, rix<R>(g, p), Lt);
-        if (!RAFT && term[p] != Lt) st<WT>(P.term, rix<R>(g, p), Lt);  // main.go:155
-        if (RAFT && !sync && ((mch >> p) & 1u)) st<WT>(P.lnext, rix<R>(g, p), m[p] + 1);   // NextIndex explicit too
+        if (xi >= 0) RW.template st<WT>(PL_TSTART, p, T.now);   // xi isolated: reset each receiver, not hb
+        if (n && !last_row) RW.template st<WT>(PL_LAST, p, last[p]);
+        if (!sync && ((mch >> p) & 1u)) RW.template st<WT>(PL_LMATCH, p, m[p]);
+        if (((cch >> p) & 1u) && !commit_row) RW.template st<WT>(PL_COMMIT, p, commit[p]);
+        if ((ltch >> p) & 1u) RW.template st<WT>(PL_LTERM, p, Lt);
+        if (!RAFT && term[p] != Lt) RW.template st<WT>(PL_TERM, p, Lt);  // main.go:155
+        if (RAFT && !sync && ((mch >> p) & 1u)) RW.template st<WT>(PL_LNEXT, p, m[p] + 1);   // NextIndex explicit too
         if (RAFT && !sync && n) {   // high-water mark = max(itself, new length)
-          const int h = ((hwup >> p) & 1u) ? at(P.hwm, rix<R>(g, p)) : 0;
-          if (h < last[p]) st<WT>(P.hwm, rix<R>(g, p), last[p]);
+          const int h = ((hwup >> p) & 1u) ? RW.at(PL_HWM, p) : 0;
+          if (h < last[p]) RW.template st<WT>(PL_HWM, p, last[p]);
         }
       }
       if constexpr (RAFT) {
         if (!sync && n) {   // the leader's high-water mark
-          const int h = ((hwup >> c) & 1u) ? at(P.hwm, rix<R>(g, c)) : 0;
-          if (h < Ll + n) st<WT>(P.hwm, rix<R>(g, c), Ll + n);
+          const int h = ((hwup >> c) & 1u) ? RW.at(PL_HWM, c) : 0;
+          if (h < Ll + n) RW.template st<WT>(PL_HWM, c, Ll + n);
         }
         if (stale) {
           // the stale leader's own client append (main.go:327-329) at its own log's end
@@ -553,8 +621,8 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
           if (n) {
             const uint64_t xvb = rng_k(key, uint32_t(xi), ST_VALUE, uint64_t(T.tick));
             const uint64_t tb = ring_tile(g, P.KP, R);
-            const uint32_t xrot = at(P.grot, g), xrota = at(P.grota, g);
-            const int xsb = at(P.gsb, g);
+            const uint32_t xrot = GW.rot(), xrota = GW.rota();
+            const int xsb = GW.sb();
             uint32_t cs = 0;
             if constexpr (CRC) cs = crc_term_state(tab, x_term);
             for (int e = 0; e < n; ++e) {
@@ -564,15 +632,15 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
               st<WT>(P.log_value + tb, o, v);
               if constexpr (CRC) st<WT>(P.log_crc + tb, o, crc_value_final(tab, cs, v));
             }
-            st<WT>(P.last, rix<R>(g, xi), xl + n);
-            if (sel(lt, xi) != x_term) st<WT>(P.lterm, rix<R>(g, xi), x_term);
-            if (at(P.hwm, rix<R>(g, xi)) < xl + n) st<WT>(P.hwm, rix<R>(g, xi), xl + n);
+            RW.template st<WT>(PL_LAST, xi, xl + n);
+            if (sel(lt, xi) != x_term) RW.template st<WT>(PL_LTERM, xi, x_term);
+            if (RW.at(PL_HWM, xi) < xl + n) RW.template st<WT>(PL_HWM, xi, xl + n);
           }
         }
         if (x_fire) {   // the isolated replica became / stays a candidate: Term+1, votedFor itself
-          st<WT>(P.term, rix<R>(g, xi), x_term + 1);
-          st<WT>(P.rs, rix<R>(g, xi), int32_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
-          st<WT>(P.tstart, rix<R>(g, xi), T.now);
+          RW.template st<WT>(PL_TERM, xi, x_term + 1);
+          RW.template st<WT>(PL_RS, xi, int32_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
+          RW.template st<WT>(PL_TSTART, xi, T.now);
         }
       }
       }   // !keep_ss
@@ -580,7 +648,7 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
       int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
       nm = keep_ss ? (nm | M_SSYNC) : (nm & ~M_SSYNC);
       if (x_fire) nm = (nm & ~M_STEADY) | M_ONECAND;
-      if (nm != meta) at(P.gmeta, g) = uint16_t(nm);
+      if (nm != meta) GW.meta() = uint16_t(nm);
       // this tick's entries go to the leader log + every follower that accepted
       if (n) {
         bool same = true;   // every writer appends at Ll+1 (REF: a follower's log may run past its MatchIndex)
@@ -590,10 +658,10 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
         const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
         // ring rotation: index i at slot (i-1+rot) mod K; an empty group's first
         // entry goes to the global phase (its logs hold nothing to move)
-        int rot = at(P.grot, g);
+        int rot = GW.rot();
         if (empty) {
           const int r0 = int(T.entries_before(T.tick) & P.kmask);
-          if (r0 != rot) { rot = r0; at(P.grot, g) = uint16_t(rot); }
+          if (r0 != rot) { rot = r0; GW.rot() = uint16_t(rot); }
         }
         if (same) {
           wr = okm | (1u << c);
@@ -614,22 +682,22 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
               lo = min(lo, pre);
               hi = max(hi, pre);
             }
-            const int sbo = at(P.gsb, g);
+            const int sbo = GW.sb();
             df |= hi > Ll ? 64u : 0u;
             df |= (sbo <= 1 || sbo <= lo - int(P.K) + 1) ? 0u : 128u;
             if (hi <= Ll && (sbo <= 1 || sbo <= lo - int(P.K) + 1)) {
               df |= 32u;
-              at(P.grota, g) = uint16_t(rot);
-              at(P.gsb, g) = Ll + 1;
+              GW.rota() = uint16_t(rot);
+              GW.sb() = Ll + 1;
               rot = (rot + int(d)) & int(P.kmask);
-              at(P.grot, g) = uint16_t(rot);
+              GW.rot() = uint16_t(rot);
               w_ph = ph;
             }
           }
         } else {   // rare: write here, each replica at its own LastApplied+1+e
           const uint64_t tb = ring_tile(g, P.KP, R);
-          const uint32_t rota = at(P.grota, g);
-          const int sb = at(P.gsb, g);
+          const uint32_t rota = GW.rota();
+          const int sb = GW.sb();
           uint32_t cs = 0;
           if constexpr (CRC) cs = crc_term_state(tab, Lt);
           for (int e = 0; e < n; ++e) {
@@ -649,7 +717,8 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
         }
       }
     }
-    if (bail) at(P.gmeta, g) = uint16_t(meta | M_DEFER);
+    if (bail) GW.meta() = uint16_t(meta | M_DEFER);
+    stored = !skip && !bail;
   }
   // ---- this tick's log entries into the rings (all lanes of the wave) ----
   // Ring row of one slot = 64 lanes x R replicas, contiguous. The lanes of
@@ -810,6 +879,7 @@ __device__ __forceinline__ void fast_group(const DevPlanes& P, const Trace& T, u
       block_stats<4>(v4, idx, stats);
     }
   }
+  return stored;
 }
 
 // EXT CRC32C tables (8 KiB) staged in LDS for the stamp/verify lookups
@@ -831,18 +901,105 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
                                                         int force_slow) {
   __shared__ uint32_t tab[CRC ? 2048 : 1];
   stage_crc_tab<CRC>(P, tab);
-  fast_group<R, WT, CRC, SEM, false>(P, T, stats, work, work_tick, work_count, force_slow,
-                                     blockIdx.x * 256u + threadIdx.x, tab);
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  fast_group<R, WT, CRC, SEM, false>(P, T, stats, work, work_tick, work_count, force_slow, g, tab,
+                                     rows_global<R>(P, g), words_global(P, g));
 }
 
 // The groups the lean kernel passed on (list[0 .. *count)), grid-striding
 // with a resident grid; zeroes the other parity's list counter (the next
-// tick's lean kernel appends there).
+// tick's lean kernel appends there). Listed groups are scattered, so a lane
+// reading its group's rows and per-group words from HBM would issue ~25
+// dependent, uncoalesced requests. Instead each block stages the records of
+// its 256 groups into LDS with coalesced loads (consecutive lanes read
+// consecutive 16-B pieces of one record: recw*4 contiguous bytes per group) plus
+// each lane's per-group words (meta, heartbeat, isolation victims, ring
+// rotation/segment, compressed record), runs fast_group on the LDS copies
+// (RowAcc / WordAcc over the __shared__ arrays: ds_ instructions), and
+// writes back the records
+// it may have changed (coalesced) and the per-group words that did change.
 template <int R, bool WT, bool CRC, int SEM>
 __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, unsigned long long* stats,
                                                         uint32_t* work, int32_t* work_tick, uint32_t* work_count,
                                                         const uint32_t* list, const uint32_t* count,
                                                         uint32_t* next_count) {
+  constexpr uint32_t RW = recw<R>();   // words per group record (16-B multiple)
+  constexpr uint32_t RQ = RW / 4;      // 16-B pieces per record
+  __shared__ uint32_t tab[CRC ? 2048 : 1];
+  __shared__ uint32_t pre[NSHARD + 1];
+  __shared__ int4 srec4[256 * RQ];
+  int32_t* const srec = reinterpret_cast<int32_t*>(srec4);
+  __shared__ uint32_t sg[256];
+  __shared__ SsRec sgss[256];
+  __shared__ int32_t shb[256], sgsb[256];
+  __shared__ uint16_t smeta[256], sgrot[256], sgrota[256];
+  __shared__ uint8_t sgiso[256], sdirty[256];
+  shard_zero(next_count);
+  const uint32_t n = shard_prefix(count, pre);
+  if (blockIdx.x * 256u >= n) return;
+  stage_crc_tab<CRC>(P, tab);
+  const uint32_t t = threadIdx.x;
+  for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+    const uint32_t i = base + t;
+    const uint32_t g = i < n ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
+    const bool valid = g < P.G;
+    sg[t] = g;
+    uint16_t m0 = 0, r0 = 0, ra0 = 0;
+    uint8_t gi0 = 0;
+    int32_t hb0 = 0, sb0 = 0;
+    SsRec ss0{0, 0, 0, 0};
+    if (valid) {
+      m0 = at(P.gmeta, g); r0 = at(P.grot, g); ra0 = at(P.grota, g); gi0 = at(P.giso, g);
+      hb0 = at(P.hb, g); sb0 = at(P.gsb, g); ss0 = P.gss[g];
+    }
+    smeta[t] = m0; sgrot[t] = r0; sgrota[t] = ra0; sgiso[t] = gi0; shb[t] = hb0; sgsb[t] = sb0; sgss[t] = ss0;
+    __syncthreads();
+    {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
+      const int4* grec = reinterpret_cast<const int4*>(P.rec);
+      int4 v[RQ];
+#pragma unroll
+      for (uint32_t k = 0; k < RQ; ++k) {
+        const uint32_t w = t + 256u * k, j = w / RQ, gj = sg[j];
+        v[k] = gj < P.G ? grec[uint64_t(gj) * RQ + (w - j * RQ)] : int4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < RQ; ++k) srec4[t + 256u * k] = v[k];
+    }
+    __syncthreads();
+    const RowAcc<R, true> rw{&srec[t * RW], 0u};
+    const WordAcc<true> gw{&smeta[t], &sgrot[t], &sgrota[t], &sgiso[t], &shb[t], &sgsb[t], &sgss[t], g};
+    const bool wrote = fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab, rw, gw);
+    sdirty[t] = valid && wrote;
+    __syncthreads();
+    {   // coalesced write-back of the records that may have changed
+      int4* grec = reinterpret_cast<int4*>(P.rec);
+#pragma unroll
+      for (uint32_t k = 0; k < RQ; ++k) {
+        const uint32_t w = t + 256u * k, j = w / RQ;
+        if (sdirty[j]) grec[uint64_t(sg[j]) * RQ + (w - j * RQ)] = srec4[w];
+      }
+    }
+    if (valid) {   // per-group words that changed
+      if (smeta[t] != m0) at(P.gmeta, g) = smeta[t];
+      if (sgrot[t] != r0) at(P.grot, g) = sgrot[t];
+      if (sgrota[t] != ra0) at(P.grota, g) = sgrota[t];
+      if (sgiso[t] != gi0) at(P.giso, g) = sgiso[t];
+      if (shb[t] != hb0) at(P.hb, g) = shb[t];
+      if (sgsb[t] != sb0) at(P.gsb, g) = sgsb[t];
+      const SsRec s1 = sgss[t];
+      if (s1.last != ss0.last || s1.term != ss0.term || s1.cl != ss0.cl || s1.cf != ss0.cf) P.gss[g] = s1;
+    }
+    __syncthreads();   // the LDS copies and the body's block reductions are reused next round
+  }
+}
+
+// The same over the list without staging: each lane reads its group's rows
+// and words from HBM itself (A/B: RAFTSTEP_LIST_STAGE=0).
+template <int R, bool WT, bool CRC, int SEM>
+__global__ __launch_bounds__(256) void tick_list_plain_kernel(DevPlanes P, Trace T, unsigned long long* stats,
+                                                              uint32_t* work, int32_t* work_tick, uint32_t* work_count,
+                                                              const uint32_t* list, const uint32_t* count,
+                                                              uint32_t* next_count) {
   __shared__ uint32_t tab[CRC ? 2048 : 1];
   __shared__ uint32_t pre[NSHARD + 1];
   shard_zero(next_count);
@@ -852,7 +1009,8 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
   for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
     const uint32_t i = base + threadIdx.x;
     const uint32_t g = i < n ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
-    fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab);
+    fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab, rows_global<R>(P, g),
+                                      words_global(P, g));
     __syncthreads();   // the body's block reductions reuse their LDS words next round
   }
 }
@@ -914,16 +1072,14 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       // when that is safe (ring_slot; as fast_group), else writes its own
       // R-contiguous segment at its own slot
       const int rot = at(P.grot, g);
+      const int sbo = P.KP > P.K ? at(P.gsb, g) : 0;   // (loaded with the rest: no dependent round trip for drifted lanes)
       const int wph = (L + rot) & int(P.kmask);
       int sw_d = 0;   // segment switch by this rotation jump (placement only, stored once the lane is taken)
       if (take && n && wph != ph) {
         const uint32_t d = uint32_t(ph - wph) & P.kmask;
         df |= d <= P.K ? 8u : 16u;
         bool sw = false;
-        if (P.KP > P.K && d <= P.K) {
-          const int sbo = at(P.gsb, g);
-          sw = sbo <= 1 || sbo <= L - int(P.K) + 1;   // the previous segment holds no readable entry
-        }
+        if (P.KP > P.K && d <= P.K) sw = sbo <= 1 || sbo <= L - int(P.K) + 1;   // the previous segment holds no readable entry
         if (sw) sw_d = int(d);
         else w_slot = wph;
       }
@@ -1112,12 +1268,23 @@ static void launch_two_pass_t(const DevPlanes& P, const Trace& T, unsigned long 
                               int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
                               uint32_t* next_count, hipStream_t s, hipEvent_t a, hipEvent_t b, hipEvent_t c,
                               hipEvent_t d) {
+  static const bool stage = [] {
+    const char* v = getenv("RAFTSTEP_LIST_STAGE");
+    return !v || atoi(v) != 0;
+  }();
   hipExtLaunchKernelGGL(tick_lean_kernel<R, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, list,
                         count);
-  const unsigned blocks =
-      unsigned(std::min<uint64_t>((P.G + 255) / 256, resident_blocks_fast(tick_list_kernel<R, false, CRC, SEM>)));
-  hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats,
-                        work, work_tick, work_count, list, count, next_count);
+  if (stage) {
+    const unsigned blocks =
+        unsigned(std::min<uint64_t>((P.G + 255) / 256, resident_blocks_fast(tick_list_kernel<R, false, CRC, SEM>)));
+    hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats,
+                          work, work_tick, work_count, list, count, next_count);
+  } else {
+    const unsigned blocks = unsigned(
+        std::min<uint64_t>((P.G + 255) / 256, resident_blocks_fast(tick_list_plain_kernel<R, false, CRC, SEM>)));
+    hipExtLaunchKernelGGL(tick_list_plain_kernel<R, false, CRC, SEM>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T,
+                          stats, work, work_tick, work_count, list, count, next_count);
+  }
 }
 hipError_t launch_tick_two_pass(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats,
                                 uint32_t* work, int32_t* work_tick, uint32_t* work_count, uint32_t* list,

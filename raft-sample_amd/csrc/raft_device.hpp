@@ -175,20 +175,24 @@ template <typename T>
 __device__ __forceinline__ T* prow(T* plane, int r, uint64_t Gp) {   // [..][Gp] row r (xmatch / xnext)
   return plane + uint64_t(r) * Gp;
 }
-// Per-replica rows live in one record per group, [Gp][NPL][R] int32: row k
-// of group g is R contiguous words at (g*NPL + k)*R, and the plane pointers
-// term, last, ... are rec + k*R, so replica r of group g of any of them is
-// element rix(g, r) = g*NPL*R + r. A group's whole per-replica state is then
+// Per-replica rows live in one record per group, [Gp][NPL][R] int32 padded to
+// recw(R) = NPL*R rounded up to 16 B: row k of group g is R contiguous words
+// at g*recw + k*R, and the plane pointers term, last, ... are rec + k*R, so
+// replica r of group g of any of them is element rix(g, r) = g*recw + r. A group's whole per-replica state is then
 // NPL*R*4 contiguous bytes (252 B at R=7): a scattered group (the list and
 // general kernels) costs 2-3 lines instead of one line per row, and a
 // block stages its groups' records into LDS with coalesced loads. A lane's
 // loads of one row still share one VGPR offset with immediate offsets r*4.
-// raft_engine_create keeps Gp*NPL*R*4 < 2^32.
+// raft_engine_create keeps Gp*recw*4 < 2^32.
 constexpr int NPL = 9;   // rows per record
 enum : int { PL_TERM = 0, PL_LAST, PL_COMMIT, PL_TSTART, PL_LTERM, PL_RS, PL_LMATCH, PL_LNEXT, PL_HWM };
+// record pitch in words: NPL*R rounded up to 16 B (records stay 16-B aligned)
+__host__ __device__ constexpr uint32_t recw_of(uint32_t R) { return (uint32_t(NPL) * R + 3u) & ~3u; }
+template <int R>
+__host__ __device__ constexpr uint32_t recw() { return recw_of(uint32_t(R)); }
 template <int R>
 __device__ __forceinline__ uint32_t rix(uint32_t g, int r) {
-  return g * uint32_t(NPL * R) + uint32_t(r);
+  return g * recw<R>() + uint32_t(r);
 }
 template <typename T>
 __device__ __forceinline__ T& at(T* base, uint32_t idx) {

@@ -92,7 +92,7 @@ def test_engine_create_rejects_bad_configs_before_touching_a_gpu(field, value, m
     assert msg in lib.raft_last_error().decode()
 
 
-NPL = 9   # int32 rows per group record (raft_device.hpp): padded groups * NPL * R * 4 must stay below 2^32
+NPL = 9   # int32 rows per group record (raft_device.hpp), padded to 16 B: groups * recw * 4 < 2^32
 
 
 def test_largest_engine_size_is_accepted_by_validation():
@@ -101,7 +101,8 @@ def test_largest_engine_size_is_accepted_by_validation():
     256 groups is refused."""
     lib = engine.load_library()
     for R in (1, 5, 7):
-        top = ((1 << 32) - 1) // (NPL * R * 4) // 256 * 256
+        recw = (NPL * R + 3) & ~3
+        top = ((1 << 32) - 1) // (recw * 4) // 256 * 256
         c = abi.default_config(replicas=R, groups=top)
         h = C.c_void_p()
         rc = lib.raft_engine_create(C.byref(c), C.byref(h))
