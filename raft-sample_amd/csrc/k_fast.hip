@@ -317,14 +317,25 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     // runs its own election timer. Its lagging MatchIndex stays implicit
     // (MSYNC: MatchIndex[xi] == LastApplied[xi], both unchanged).
     int xi = -1;
+    int giso_w = -1;   // giso to store (a window decided this tick), -1: unchanged
     bool lx = false;   // RAFT: the primary leader is the one isolated replica (see below)
     if (go && T.iso_p) {
       uint32_t act = 0, starting = 0;
       uint32_t im = iso_windows<R>(key, T, &act, &starting);
-      if (T.iso_leader) {   // leader mode: a window starting now is decided by the general kernel
-        if (starting) bail = true;
+      if (T.iso_leader) {
+        // leader mode: a window starting now takes the lowest-id Leader as the
+        // tick begins (tick_iso_mask, decide); in a STEADY group that is the
+        // primary, recorded in giso with the tick's stores. Other groups with
+        // a window starting go to the general kernel.
         uint32_t gi = act ? uint32_t(GW.iso()) : 0u;
-        im = leader_iso_mask(act, 0u, gi, 0u, false);
+        if (starting && (meta & M_STEADY)) {
+          const uint32_t g0 = gi;
+          im = leader_iso_mask(act, starting, gi, 1u << c, true);
+          if (gi != g0) giso_w = int(gi);
+        } else {
+          if (starting) bail = true;
+          im = leader_iso_mask(act, 0u, gi, 0u, false);
+        }
       }
       if (RAFT && R >= 3 && im && (im & (im - 1u)) == 0u && int(__builtin_ctz(im)) != c) xi = int(__builtin_ctz(im));
       else if (RAFT && R >= 3 && im == (1u << c) && (meta & M_STEADY)) lx = true;
@@ -718,6 +729,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       }
     }
     if (bail) GW.meta() = uint16_t(meta | M_DEFER);
+    else if (giso_w >= 0) GW.iso() = uint8_t(giso_w);   // a leader-isolation window decided this tick
     stored = !skip && !bail;
   }
   // ---- this tick's log entries into the rings (all lanes of the wave) ----
