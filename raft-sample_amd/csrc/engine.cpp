@@ -423,6 +423,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* wt = getenv("RAFTSTEP_WRITE_THROUGH")) e->write_through = atoi(wt) != 0;
   if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
+  if (const char* dl = getenv("RAFTSTEP_DIAG_LEAN")) e->P.diag = uint32_t(atoi(dl));
   if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
     if (rc == RAFT_OK) rc = dev_alloc(e, reinterpret_cast<void**>(&e->P.dbg), 32 * 8);
     if (rc == RAFT_OK && hipMemset(e->P.dbg, 0, 32 * 8) != hipSuccess) rc = fail(RAFT_EHIP, "hipMemset failed");

@@ -1143,8 +1143,12 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   // this tick's entries: the taken lanes at the global phase as whole ring
   // rows, all R replicas (the cooperative row stores of fast_group); a
   // drifted lane its own R-contiguous segment
-  const bool wr = take && n && w_slot < 0;
-  const bool wd = take && n && w_slot >= 0;
+  bool wr = take && n && w_slot < 0;
+  bool wd = take && n && w_slot >= 0;
+  if (P.diag) {   // timing-only diagnostics (wrong results): drifted lanes skip / write the common row
+    if (P.diag & 2u) wr |= wd;
+    wd = false;
+  }
   if (__ballot(wr || wd)) {
     const int lane = threadIdx.x & 63;
     const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g), P.KP, R);

@@ -88,6 +88,8 @@ struct DevPlanes {
   unsigned long long* dbg;  // diagnostics (RAFTSTEP_DEBUG_FAST): fast-kernel lane class counters, else null
   int32_t* rec;        // [Gp][NPL][R] group records holding every per-replica row above (see rix)
   uint32_t scap;       // capacity of one shard of a sharded group list (see below)
+  uint32_t diag;       // timing-only diagnostics (RAFTSTEP_DIAG_LEAN; results are wrong when set): 1 = drifted
+                       // lanes of the lean kernel skip their ring writes, 2 = they write the wave's common row
 };
 
 // Sharded group lists (the general kernel's worklist, the two-pass tick's
