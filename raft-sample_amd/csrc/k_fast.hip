@@ -229,7 +229,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
                                            int32_t* work_tick, uint32_t* work_count, int force_slow, const uint32_t g,
                                            const uint32_t* tab, const Rows& RW, const Words& GW) {
   constexpr bool RAFT = SEM == SEM_RAFT;
-  int sv[5] = {0, 0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups, term bumps
+  int sv[7] = {0, 0, 0, 0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups, term bumps, votes, won
   bool bail = false;
   const int n = int(T.client_entries());   // entries per leader this tick (wave-uniform)
   // this lane's ring writes, issued after the per-group code (wave-converged)
@@ -258,6 +258,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     }
     int term[R], last[R], commit[R], lt[R], m[R];
     uint32_t rowbad = 0;   // RAFT explicit rows out of step (replica bits)
+    uint32_t fresh = 0;    // RAFT: a new leader's rows (MatchIndex 0, NextIndex = its length + 1)
     uint32_t hwup = 0;     // RAFT: replicas whose high-water mark is above their log length (truncated)
     bool empty = true;   // every log of the group empty before this tick
     const bool go = !skip && !bail && c != NO_PRIMARY;
@@ -293,9 +294,16 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         if constexpr (RAFT) {
           // RAFT rows kept explicitly: NextIndex must be MatchIndex+1 and no
           // log may be shorter than its high-water mark (no pending truncation)
+          const int lc1 = sel(last, c) + 1;
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            if (r != c && RW.at(PL_LNEXT, r) != m[r] + 1) rowbad |= 1u << r;
+            const int nxr = RW.at(PL_LNEXT, r);
+            if (r != c && nxr != m[r] + 1) {
+              // the rows a leader starts its term with (r_candidate_round):
+              // in step for a follower holding the leader's log (checked below)
+              if (m[r] == 0 && nxr == lc1) fresh |= 1u << r;
+              else rowbad |= 1u << r;
+            }
             // a log truncated below its high-water mark stays in step as long as
             // the entry this tick's AppendEntries checks (its last) is still
             // inside the ring window (hwm-K, last] (Group::r_deliver_ae's evicted rule)
@@ -319,9 +327,10 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     int xi = -1;
     int giso_w = -1;   // giso to store (a window decided this tick), -1: unchanged
     bool lx = false;   // RAFT: the primary leader is the one isolated replica (see below)
+    uint32_t im = 0;   // replicas cut off this tick
     if (go && T.iso_p) {
       uint32_t act = 0, starting = 0;
-      uint32_t im = iso_windows<R>(key, T, &act, &starting);
+      im = iso_windows<R>(key, T, &act, &starting);
       if (T.iso_leader) {
         // leader mode: a window starting now takes the lowest-id Leader as the
         // tick begins (tick_iso_mask, decide); in a STEADY group that is the
@@ -343,7 +352,16 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       if (im) df |= 4u;
     }
     DIAG_REASON(if (bail && !(df & (2048u | 16384u))) df |= 4096u;);   // reason: leader or >1 replica isolated
-    if (go && !xi_ok<RAFT>(meta, xi)) bail = true;   // ONECAND needs its candidate isolated (role checked below)
+    // RAFT ONESTALE with nobody cut off this tick: the stale leader is
+    // reachable again (its window ended) — the return tick, taken below when
+    // it is a plain catch-up (sr: the returning stale leader)
+    int sr = -1;
+    if (RAFT && go && !bail && (meta & M_ONESTALE) && im == 0u && !P.crc_on) {
+#pragma unroll
+      for (int p = 0; p < R; ++p)
+        if (p != c && (RW.at(PL_RS, p) & 3) == ROLE_L) sr = p;
+    }
+    if (go && !xi_ok<RAFT>(meta, xi) && sr < 0) bail = true;   // ONECAND needs its candidate isolated (role checked below)
     // RAFT ONESTALE: the one non-follower besides the primary is a leader of a
     // lower term, cut off this tick (xi). It appends this tick's client entries
     // to its own log and every AppendEntries it sends is dropped; its commit
@@ -351,7 +369,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     // off and its own log only grows past it). Its row in the primary's
     // planes stays explicit, so the group keeps explicit rows (no MSYNC).
     const bool stale = RAFT && (meta & M_ONESTALE) && xi >= 0;
-    if (RAFT && (meta & M_ONESTALE)) bail |= (rowbad & ~(stale ? 1u << xi : 0u)) != 0u;
+    if (RAFT && (meta & M_ONESTALE))
+      bail |= (rowbad & ~(stale ? 1u << xi : 0u) & ~(sr >= 0 ? 1u << sr : 0u)) != 0u;
     // leader view
     const int Lt = sel(term, c), Ll = sel(last, c), Lc = sel(commit, c), Llt = sel(lt, c);
     // RAFT: the leader itself cut off (leader isolation), every other replica
@@ -365,16 +384,34 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     // stand still, so the rows become implicit (MSYNC).
     if (go && !bail && lx) {
       // (a truncated log, high-water mark above its length, would break MSYNC's hwm == last)
-      bail = int64_t(Ll) + n > I32MAX || n >= int(P.K) || Ll == 0 || hwup != 0u;
+      // (fresh rows are in step only for a follower that accepts this tick; here nobody does)
+      bail = int64_t(Ll) + n > I32MAX || n >= int(P.K) || Ll == 0 || hwup != 0u || fresh != 0u;
 #pragma unroll
       for (int p = 0; p < R; ++p) bail |= p != c && m[p] != last[p];
       int ts[R], rsv[R];
       RW.load(PL_TSTART, ts);
       const int hbt = GW.hb();
+      int w = -1, wdl = 0;   // the first follower, in (deadline, id) order, whose election timeout is due
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         rsv[p] = RW.at(PL_RS, p);
-        if (p != c) bail |= max(ts[p], hbt) + (rsv[p] >> 6) <= T.now;   // a follower's election timeout is due
+        const int dl = max(ts[p], hbt) + (rsv[p] >> 6);
+        if (p != c && dl <= T.now && (w < 0 || dl < wdl)) { w = p; wdl = dl; }
+      }
+      // Election (step 3 of the tick, after the cut-off leader's round):
+      // w times out (r_timeout_fire: Term+1, votes for itself, candidate
+      // timer) and runs its vote round at once (r_candidate_round,
+      // main.go:253-284 -> 157-170 with Raft's up-to-date check). Every other
+      // follower holds w's log and term, so each adopts Term+1 and grants
+      // (its timer reset), the cut-off leader is never reached: w wins with
+      // R-1 > R/2 votes; no other timer is still due. Taken when every
+      // follower's log and term equal w's; anything else: general path.
+      if (w >= 0) {
+        const int fl = sel(last, w), flt = sel(lt, w);
+        bail |= Lt >= I32MAX;
+#pragma unroll
+        for (int p = 0; p < R; ++p)
+          if (p != c) bail |= term[p] != Lt || last[p] != fl || (fl > 0 && lt[p] != flt);
       }
       // commitIndex: the largest N held by a majority (leader included), if
       // log[N].term == currentTerm (Group::r_commit_rule); MatchIndex = LastApplied (MSYNC)
@@ -419,7 +456,35 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
         }
         if (cm != Lc) RW.template st<WT>(PL_COMMIT, c, cm);
-        const int nm = (meta | M_MSYNC) & ~M_SSYNC;
+        int nm = (meta | M_MSYNC) & ~M_SSYNC;
+        if (w >= 0) {   // the election (see above)
+          const int nt = Lt + 1, fl = sel(last, w);
+          const int dc = T.c_min + int(uint32_t(rng_k(key, uint32_t(w), ST_TIMER_C, uint64_t(T.tick)) >> 32) %
+                                       uint32_t(T.c_span));
+          int hwr[R], mz[R], nx[R];
+#pragma unroll
+          for (int p = 0; p < R; ++p) {
+            hwr[p] = p == c ? Ll + n : last[p];   // high-water marks become explicit (MSYNC ends)
+            mz[p] = 0;                            // w's rows: MatchIndex 0, NextIndex = its length + 1
+            nx[p] = fl + 1;
+            if (p == c) continue;
+            RW.template st<WT>(PL_TERM, p, nt);
+            RW.template st<WT>(PL_TSTART, p, T.now);   // candidate timer start / vote granted: timer reset
+            RW.template st<WT>(PL_RS, p, p == w ? int32_t(ROLE_L | (uint32_t(w + 1) << 2) | (uint32_t(dc) << 6))
+                                                : int32_t((rsv[p] & ~0x3F) | ROLE_F | ((w + 1) << 2)));
+            // the cut-off leader's rows (implicit: MatchIndex = LastApplied) move to its xmatch / xnext rows
+            st<WT>(prow(P.xmatch, c * R + p, P.Gp), g, last[p]);
+            st<WT>(prow(P.xnext, c * R + p, P.Gp), g, last[p] + 1);
+          }
+          RW.store(PL_HWM, hwr);
+          RW.store(PL_LMATCH, mz);
+          RW.store(PL_LNEXT, nx);
+          // w (the highest term) becomes the primary; the cut-off leader is a stale one
+          nm = (meta & ~(0xF | M_MSYNC | M_SSYNC | M_STEADY | M_ONECAND)) | w | M_ONESTALE;
+          sv[4] = 1;       // term bumps: w's timeout
+          sv[5] = R - 2;   // votes granted
+          sv[6] = 1;       // elections won
+        }
         if (nm != meta) GW.meta() = uint16_t(nm);
       }
     }
@@ -428,11 +493,12 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     if (gom) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
-        if (p == xi) {   // MSYNC stays exact for an isolated follower / candidate
-          if (!stale) bail |= m[p] != last[p] || m[p] > Ll;
+        if (p == sr) continue;   // the returning stale leader: checked with its AppendEntries below
+        if (p == xi) {   // MSYNC stays exact for an isolated follower / candidate (not a fresh row: unchanged, explicit)
+          if (!stale) bail |= m[p] != last[p] || m[p] > Ll || ((fresh >> p) & 1u);
           continue;
         }
-        bail |= (p != c) && m[p] != Ll;
+        bail |= (p != c) && m[p] != Ll && !((fresh >> p) & 1u);
         // RAFT: a follower with extra entries or another term takes the general path
         if constexpr (RAFT) bail |= (p != c) && (last[p] != Ll || term[p] != Lt);
       }
@@ -493,7 +559,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     if (gom && !bail) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
-        if (p == c || p == xi) continue;   // xi: dropped (sender sees false, receiver unchanged)
+        if (p == c || p == xi || p == sr) continue;   // xi: dropped (sender sees false, receiver unchanged)
         const int l = last[p];
         bool ok;
         if constexpr (RAFT) {
@@ -526,9 +592,87 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         }
       }
     }
+    // The return tick (sr >= 0, see above). sr is still a Leader at step 1 and
+    // appends its own client entries; at step 2 it learns the primary's higher
+    // term — from the first peer its own round reaches when its id is lower
+    // (one failed AppendEntries), else from the primary's AppendEntries — and
+    // steps down (r_observe_term: Term, votedFor none, a new follower timer).
+    // The primary's AppendEntries carries prevLogIndex NextIndex[sr]-1 = L0,
+    // its length when it was elected (sr's row never moved while sr's
+    // messages were dropped), so the entries it holds after L0 are of its own
+    // term, above every term in sr's log. Taken when sr's entry L0 has the
+    // primary's term (accepted) and the two logs differ at L0+1 (checked, one
+    // ring read each): r_deliver_ae then truncates sr's log at L0 and appends
+    // everything, so sr's log becomes the primary's — entries L0+1..Ll copied
+    // from the primary's ring, this tick's written with everyone's.
+    int sr_hw = 0, sr_dur = 0;
+    if (RAFT && sr >= 0 && gom && !bail) {
+      const int L0 = RW.at(PL_LNEXT, sr) - 1;
+      const int ls = sel(last, sr), hws = RW.at(PL_HWM, sr), hwc = RW.at(PL_HWM, c);
+      sr_hw = max(hws, ls + n);   // its high-water mark after its own client append
+      const int Kd = int(P.K);
+      // (n == 0 would leave sr's LastApplied out of the row stores below: general path)
+      bail |= n == 0 || sel(term, sr) >= Lt || L0 < 0 || L0 > ls || L0 > Ll || int64_t(ls) + n > I32MAX ||
+              hwc < Ll || (L0 >= 1 ? L0 : 1) <= max(hwc, Ll + n) - Kd ||   // NextIndex / prevLogTerm in the ring
+              (L0 >= 1 ? L0 : 1) <= sr_hw - Kd;   // sr's entries L0 (prevLogTerm) and L0+1 (conflict) are read
+      // every read this needs is issued at once (one round trip for the lane,
+      // whose wave waits on it): sr's NextIndex for p0 and the terms of both
+      // logs at L0 and L0+1 (the ring addresses are valid whatever the values)
+      const uint64_t tb = ring_tile(g, P.KP, R);
+      const uint32_t rot = GW.rot(), rota = GW.rota();
+      const int sbo = GW.sb();
+      const int p0 = sr == 0 ? 1 : 0;   // the lowest-id peer: where sr's own round goes first
+      const uint32_t o0 = ring_in_tile(g, R, ring_slot(L0, rot, rota, sbo, P.kmask), 0u);
+      const uint32_t o1 = ring_in_tile(g, R, ring_slot(L0 + 1, rot, rota, sbo, P.kmask), 0u);
+      const int32_t* const rt = P.log_term + tb;
+      const int nx0 = at(prow(P.xnext, sr * R + p0, P.Gp), g);
+      const int tc0 = at(rt, o0 + uint32_t(c)), ts0 = at(rt, o0 + uint32_t(sr));
+      const int tc1 = at(rt, o1 + uint32_t(c)), ts1 = at(rt, o1 + uint32_t(sr));
+      // sr's own round (sr < c) reaches p0 before it learns the higher term:
+      // r_leader_round's NextIndex / prevLogTerm checks on sr's row must not fault
+      if (sr < c) bail |= nx0 < 1 || nx0 > ls + n + 1 || (nx0 >= 2 ? nx0 - 1 : 1) <= sr_hw - Kd;
+      // prevLogTerm: the primary's entry L0 against sr's (cached last-entry terms where they apply)
+      if (L0 >= 1) bail |= (L0 == Ll ? Llt : tc0) != (L0 == ls ? sel(lt, sr) : ts0);
+      // the first conflict must be at L0+1 (else r_deliver_ae skips the entries present);
+      // sr's entry L0+1 is from its ring or the one its own client append adds this tick
+      bail |= (L0 + 1 <= Ll ? tc1 : Lt) == (L0 + 1 <= ls ? ts1 : sel(term, sr));
+      if (!bail) {
+        // the primary's entries after L0 (at most K), 8 loads in flight per batch
+        for (int i0 = L0 + 1; i0 <= Ll; i0 += 8) {
+          int32_t bt[8];
+          int64_t bv[8];
+          uint32_t bo[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            bo[j] = ring_in_tile(g, R, ring_slot(i0 + j, rot, rota, sbo, P.kmask), uint32_t(c));
+            bt[j] = at(rt, bo[j]);
+            bv[j] = at(P.log_value + tb, bo[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if (i0 + j > Ll) break;
+            st<WT>(P.log_term + tb, bo[j] + uint32_t(sr - c), bt[j]);
+            st<WT>(P.log_value + tb, bo[j] + uint32_t(sr - c), bv[j]);
+          }
+        }
+        sr_dur = T.f_min + int(uint32_t(rng_k(key, uint32_t(sr), ST_TIMER_F, uint64_t(T.tick)) >> 32) %
+                               uint32_t(T.f_span));
+        const int nl = Ll + n;
+        put(last, sr, nl);
+        const int cs = sel(commit, sr);
+        if (Lc > cs) {   // min(leaderCommit, index of the last new entry)
+          const int nc = Lc < nl ? Lc : nl;
+          if (nc != cs) { put(commit, sr, nc); cch |= 1u << sr; }
+        }
+        ltch |= 1u << sr;   // its last entry is now one of the primary's term
+        put(m, sr, nl);
+        mch |= 1u << sr;
+        okm |= 1u << sr;
+      }
+    }
     if (gom && !bail) {
       int cm = Lc;
-      bool sync = !stale;   // ONESTALE: the stale leader's row is explicit
+      bool sync = !stale && sr < 0;   // ONESTALE: the stale leader's row is explicit; a returning one's hwm too
       if constexpr (RAFT) {  // MSYNC also means high-water mark == length for everyone
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -556,7 +700,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       }
       sv[0] = cm - Lc;
       sv[1] = __builtin_popcount(okm);
-      sv[2] = (R - 1) - sv[1] + (stale ? R - 1 : 0);   // + every AppendEntries of the cut-off stale leader
+      sv[2] = (R - 1) - sv[1] + (stale ? R - 1 : 0) + (sr >= 0 && sr < c ? 1 : 0);   // + every AppendEntries of the
+      // cut-off stale leader; a returning one with a lower id sends one (rejected) before stepping down
       sv[3] = 1;
       sv[4] = x_fire;
       // ---- stores (no bail past this point) ----
@@ -653,12 +798,19 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           RW.template st<WT>(PL_RS, xi, int32_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
           RW.template st<WT>(PL_TSTART, xi, T.now);
         }
+        if (sr >= 0) {   // the returning stale leader stepped down: a follower of the primary's term
+          RW.template st<WT>(PL_TERM, sr, Lt);
+          RW.template st<WT>(PL_RS, sr, int32_t(ROLE_F | (uint32_t(sr_dur) << 6)));   // votedFor none
+          RW.template st<WT>(PL_TSTART, sr, T.now);
+          RW.template st<WT>(PL_HWM, sr, sr_hw);
+        }
       }
       }   // !keep_ss
       // RAFT: MSYNC also makes NextIndex (= match+1) and the high-water marks (= last) implicit
       int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
       nm = keep_ss ? (nm | M_SSYNC) : (nm & ~M_SSYNC);
       if (x_fire) nm = (nm & ~M_STEADY) | M_ONECAND;
+      if (sr >= 0) nm = (nm & ~M_ONESTALE) | M_STEADY;   // one leader, every other replica a follower
       if (nm != meta) GW.meta() = uint16_t(nm);
       // this tick's entries go to the leader log + every follower that accepted
       if (n) {
@@ -685,7 +837,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           const uint32_t d = uint32_t(ph - w_ph) & P.kmask;
           if (d != 0u) df |= d <= P.K ? 8u : 16u;
           // (not with a stale leader appending elsewhere in the ring this tick)
-          if (P.KP > P.K && d != 0u && d <= P.K && Ll > 0 && !stale) {
+          if (P.KP > P.K && d != 0u && d <= P.K && Ll > 0 && !stale && sr < 0) {
             int lo = Ll, hi = Ll;   // log lengths before this tick (== high-water marks on this path)
 #pragma unroll
             for (int p = 0; p < R; ++p) {
@@ -883,8 +1035,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   }
   if (stats) {
     if constexpr (RAFT) {
-      const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
-      block_stats<5>(sv, idx, stats);
+      const int idx[7] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS, S_VOTES, S_WON};
+      block_stats<7>(sv, idx, stats);
     } else {
       const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
       const int v4[4] = {sv[0], sv[1], sv[2], sv[3]};
