@@ -576,7 +576,8 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
       if (v->deadline) v->deadline[c] = (role == ROLE_L ? ts[d] : std::max(ts[d], hb[g])) + int32_t(rs[d] >> 6);
       if (v->timeout) v->timeout[c] = int32_t(rs[d] >> 6);
       // RAFT + MSYNC: high-water marks and the primary's NextIndex row are implicit too
-      const int32_t hwm = (raft && !msync) ? hw[d] : last[d];
+      // (MSYNC: max(plane, LastApplied), raft_device.hpp M_HWX)
+      const int32_t hwm = raft ? (msync ? std::max(hw[d], last[d]) : hw[d]) : last[d];
       if (v->hwm) v->hwm[c] = hwm;
       if (v->match)
         for (uint64_t p = 0; p < R; ++p) {

@@ -236,6 +236,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   uint32_t wr = 0;      // replicas that append this tick's entries (leader + accepting followers)
   int w_term = 0, w_ph = 0;    // their term and the ring slot of the first entry
   uint64_t w_vb = 0;    // value stream base of this tick's entries
+  int cp_n = 0, cp_from = 0, cp_sb = 0;   // RAFT: a returning stale leader's catch-up copy (see the ring writes)
+  uint32_t cp_cs = 0, cp_rot = 0;
   uint32_t df = 0;      // diagnostics: lane class bits (P.dbg)
   bool stored = false;  // the group's rows may have been written (returned)
   // deferral-reason bits 11-15 only in a diagnostics build (make DIAG=1),
@@ -288,6 +290,16 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       if (meta & M_MSYNC) {
 #pragma unroll
         for (int r = 0; r < R; ++r) m[r] = (r != c) ? last[r] : 0;
+        if constexpr (RAFT) {
+          if (meta & M_HWX) {   // high-water marks max(plane, LastApplied): truncated logs in step
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              const int hwd = RW.at(PL_HWM, r) - last[r];
+              if (hwd >= int(P.K)) rowbad |= 1u << r;
+              if (hwd > 0) hwup |= 1u << r;
+            }
+          }
+        }
       } else {
 #pragma unroll
         for (int r = 0; r < R; ++r) m[r] = (r != c) ? RW.at(PL_LMATCH, r) : 0;
@@ -456,7 +468,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
         }
         if (cm != Lc) RW.template st<WT>(PL_COMMIT, c, cm);
-        int nm = (meta | M_MSYNC) & ~M_SSYNC;
+        int nm = (meta | M_MSYNC) & ~(M_SSYNC | M_HWX);   // (no truncated log here: hwup == 0)
         if (w >= 0) {   // the election (see above)
           const int nt = Lt + 1, fl = sel(last, w);
           const int dc = T.c_min + int(uint32_t(rng_k(key, uint32_t(w), ST_TIMER_C, uint64_t(T.tick)) >> 32) %
@@ -480,7 +492,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           RW.store(PL_LMATCH, mz);
           RW.store(PL_LNEXT, nx);
           // w (the highest term) becomes the primary; the cut-off leader is a stale one
-          nm = (meta & ~(0xF | M_MSYNC | M_SSYNC | M_STEADY | M_ONECAND)) | w | M_ONESTALE;
+          nm = (meta & ~(0xF | M_MSYNC | M_SSYNC | M_HWX | M_STEADY | M_ONECAND)) | w | M_ONESTALE;
           sv[4] = 1;       // term bumps: w's timeout
           sv[5] = R - 2;   // votes granted
           sv[6] = 1;       // elections won
@@ -637,24 +649,12 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       // sr's entry L0+1 is from its ring or the one its own client append adds this tick
       bail |= (L0 + 1 <= Ll ? tc1 : Lt) == (L0 + 1 <= ls ? ts1 : sel(term, sr));
       if (!bail) {
-        // the primary's entries after L0 (at most K), 8 loads in flight per batch
-        for (int i0 = L0 + 1; i0 <= Ll; i0 += 8) {
-          int32_t bt[8];
-          int64_t bv[8];
-          uint32_t bo[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            bo[j] = ring_in_tile(g, R, ring_slot(i0 + j, rot, rota, sbo, P.kmask), uint32_t(c));
-            bt[j] = at(rt, bo[j]);
-            bv[j] = at(P.log_value + tb, bo[j]);
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            if (i0 + j > Ll) break;
-            st<WT>(P.log_term + tb, bo[j] + uint32_t(sr - c), bt[j]);
-            st<WT>(P.log_value + tb, bo[j] + uint32_t(sr - c), bv[j]);
-          }
-        }
+        // the primary's entries after L0 (at most K): copied below by the whole wave
+        cp_n = Ll - L0;
+        cp_from = L0 + 1;
+        cp_cs = uint32_t(c) | (uint32_t(sr) << 4);
+        cp_rot = rot | (rota << 16);
+        cp_sb = sbo;
         sr_dur = T.f_min + int(uint32_t(rng_k(key, uint32_t(sr), ST_TIMER_F, uint64_t(T.tick)) >> 32) %
                                uint32_t(T.f_span));
         const int nl = Ll + n;
@@ -673,12 +673,13 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     if (gom && !bail) {
       int cm = Lc;
       bool sync = !stale && sr < 0;   // ONESTALE: the stale leader's row is explicit; a returning one's hwm too
-      if constexpr (RAFT) {  // MSYNC also means high-water mark == length for everyone
+      bool hwx = false;               // RAFT: MSYNC with a high-water mark above its log's length (M_HWX)
+      if constexpr (RAFT) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           if (!((hwup >> r) & 1u)) continue;
           const int la = r == c ? Ll + n : last[r];   // (accepting followers' last already moved)
-          if (RW.at(PL_HWM, r) > la) sync = false;
+          if (RW.at(PL_HWM, r) > la) hwx = true;      // the plane holds it (exact: rows were explicit or HWX)
         }
       }
       if constexpr (RAFT) {
@@ -808,6 +809,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       }   // !keep_ss
       // RAFT: MSYNC also makes NextIndex (= match+1) and the high-water marks (= last) implicit
       int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
+      nm = (sync && hwx) ? (nm | M_HWX) : (nm & ~M_HWX);
       nm = keep_ss ? (nm | M_SSYNC) : (nm & ~M_SSYNC);
       if (x_fire) nm = (nm & ~M_STEADY) | M_ONECAND;
       if (sr >= 0) nm = (nm & ~M_ONESTALE) | M_STEADY;   // one leader, every other replica a follower
@@ -921,6 +923,30 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
                 if constexpr (CRC) st<WT>(rc, o + p, stamp);
               }
             }
+      }
+    }
+  }
+  // a returning stale leader's catch-up (entries L0+1..Ll of the primary's
+  // log into its own, same slots): the wave copies one lane's entries at a
+  // time, one entry per lane, so each costs one round trip instead of a
+  // serial loop in the lane whose wave waits on it
+  if constexpr (RAFT) {
+    uint64_t pend = __ballot(cp_n > 0);
+    const int lane = threadIdx.x & 63;
+    while (pend) {
+      const int src = int(__builtin_ctzll(pend));
+      pend &= pend - 1ull;
+      const int cnt = __shfl(cp_n, src), from = __shfl(cp_from, src), sb_ = __shfl(cp_sb, src);
+      const uint32_t cs = uint32_t(__shfl(int(cp_cs), src)), rr = uint32_t(__shfl(int(cp_rot), src));
+      const uint32_t gg = uint32_t(__shfl(int(g), src));
+      const uint64_t tb = ring_tile(gg, P.KP, R);
+      const uint32_t cc = cs & 15u, ss = cs >> 4;
+      for (int j = lane; j < cnt; j += 64) {
+        const uint32_t o = ring_in_tile(gg, R, ring_slot(from + j, rr & 0xFFFFu, rr >> 16, sb_, P.kmask), 0u);
+        const int32_t t = at(P.log_term + tb, o + cc);
+        const int64_t v = at(P.log_value + tb, o + cc);
+        st<WT>(P.log_term + tb, o + ss, t);
+        st<WT>(P.log_value + tb, o + ss, v);
       }
     }
   }
@@ -1230,7 +1256,24 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         if (T.iso_leader ? act != 0u : im != 0u) take = false;
       }
       const int L = s.last;
-      take &= L > 0 && int64_t(L) + n <= I32MAX && n < int(P.K);
+      // (the followers' CommitIndex min(LeaderCommit, last new entry) is the
+      // leader's only while that is at most L+n: a leader's CommitIndex above
+      // its log, left by a truncation, goes to the list kernel)
+      take &= L > 0 && int64_t(L) + n <= I32MAX && n < int(P.K) && s.cl <= L + n;
+      int hwx_clear = 0;   // RAFT HWX: a truncated log in step (high-water marks in the hwm plane)
+      if (RAFT && take && (meta & M_HWX)) {
+        // every AppendEntries' prevLogIndex (L) and NextIndex (L+1) must stay
+        // inside the ring window of every log: max hwm < L+K (r_deliver_ae /
+        // r_leader_round's evicted rules); the flag clears once every log has
+        // grown to its mark (the marks are then LastApplied again)
+        int hw[R];
+        load_row_p<R>(&at(P.hwm, rix<R>(g, 0)), hw);
+        int mx = hw[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) mx = max(mx, hw[r]);
+        take &= mx - L < int(P.K);
+        hwx_clear = mx <= L + n ? 1 : 0;
+      }
       // ring phase: a group whose logs stood still under churn appends out of
       // the global phase (drifted); it switches its ring segment in place
       // when that is safe (ring_slot; as fast_group), else writes its own
@@ -1277,6 +1320,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         const int cf2 = s.cl > s.cf ? s.cl : s.cf;
         P.gss[g] = SsRec{nl, s.term, cl2, cf2};
         at(P.hb, g) = T.now;                               // timer.Reset(d) of every follower
+        if (hwx_clear) at(P.gmeta, g) = uint16_t(meta & ~M_HWX);
         if (sw_d) {   // the new segment starts at this tick's first entry
           at(P.grota, g) = uint16_t(rot);
           at(P.gsb, g) = L + 1;

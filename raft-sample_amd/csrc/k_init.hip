@@ -95,7 +95,8 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
       const int l = sel(last, r);
       const int ts = at(P.tstart, rix<R>(g, r));
       const int dl = (role == ROLE_L ? ts : max(ts, hb)) + dur;
-      const int hwm = (raft && !msync) ? at(P.hwm, rix<R>(g, r)) : l;
+      // MSYNC: max(plane, LastApplied) (HWX; the plane is at most LastApplied without it)
+      const int hwm = raft ? (msync ? max(at(P.hwm, rix<R>(g, r)), l) : at(P.hwm, rix<R>(g, r))) : l;
       h = dg_mix(h, uint64_t(role) | (uint64_t((x >> 2) & 15u) << 8) | (uint64_t(r) << 16));
       const int tm = ssync ? ss.term : at(P.term, rix<R>(g, r));
       const int cm = ssync ? (r == primary ? ss.cl : ss.cf) : at(P.commit, rix<R>(g, r));

@@ -46,6 +46,13 @@ constexpr int M_ONESTALE = 1 << 12; // as STEADY, except that exactly one other 
 // followers' CommitIndex} is the state (the steady-state kernel reads and
 // writes only it); every other reader materialises the planes from it.
 constexpr int M_SSYNC = 1 << 13;
+// HWX (RAFT, with MSYNC): some replica's log was truncated below its
+// high-water mark, which the hwm plane holds. Under MSYNC every replica's
+// high-water mark is max(hwm plane, LastApplied) (the plane is exact when
+// MSYNC is entered and no log is truncated while it holds); without HWX the
+// plane is at most LastApplied everywhere, so readers that only need the
+// steady case (the lean kernel) skip the plane.
+constexpr int M_HWX = 1 << 14;
 struct __attribute__((aligned(16))) SsRec { int32_t last, term, cl, cf; };
 constexpr int HB_NONE = -2147483647 - 1;
 constexpr int I32MAX = 2147483647;
@@ -462,8 +469,8 @@ struct Group {
           pm[p] = last[p];
           if constexpr (SEM == SEM_RAFT) pn[p] = last[p] + 1;
         }
-        if constexpr (SEM == SEM_RAFT) {
-          if (hw[p] != last[p]) { hw[p] = last[p]; d_hw |= 1u << p; }
+        if constexpr (SEM == SEM_RAFT) {   // max(plane, LastApplied) (HWX)
+          if (hw[p] < last[p]) { hw[p] = last[p]; d_hw |= 1u << p; }
         }
       }
     }

@@ -162,7 +162,7 @@ struct Seg {
         if constexpr (SEM == SEM_RAFT) { pn = last + 1; dirty |= SD_PN; }
       }
       if constexpr (SEM == SEM_RAFT) {
-        if (hw != last) { hw = last; dirty |= SD_HW; }
+        if (hw < last) { hw = last; dirty |= SD_HW; }   // max(plane, LastApplied) (HWX)
       }
     }
   }
