@@ -385,6 +385,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.grot), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.grota), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.gsb), Gp * 4);
+  A(reinterpret_cast<void**>(&e->P.grotb), Gp * 2);
+  A(reinterpret_cast<void**>(&e->P.gsb2), Gp * 4);
   // sharded group lists (raft_device.hpp): NSHARD shards of scap entries
   const uint64_t scap = ((Gp / 256 + NSHARD - 1) / NSHARD) * 256;
   A(reinterpret_cast<void**>(&e->work), NSHARD * scap * 4);
@@ -447,6 +449,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetAsync(e->P.grot, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grota, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gsb, 0, Gp * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.grotb, 0, Gp * 2, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.gsb2, 0, Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, 4 * SHARD_WORDS * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_value, 0, R * K * Gp * 8, e->stream) : z;
@@ -512,9 +516,9 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
   const bool raft = e->cfg.semantics == RAFT_SEM_RAFT;
   std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt, ln, xn, hw, rs, blk;
-  std::vector<uint16_t> meta, rot, rota;
+  std::vector<uint16_t> meta, rot, rota, rotb;
   std::vector<uint8_t> giso;
-  std::vector<int32_t> sb;
+  std::vector<int32_t> sb, sb2;
   std::vector<int64_t> lv;
   std::vector<uint32_t> lcrc;
   int rc = RAFT_OK;
@@ -530,6 +534,8 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!rc && logs) rc = d2h(e, rot, e->P.grot, Gp);
   if (!rc && logs) rc = d2h(e, rota, e->P.grota, Gp);
   if (!rc && logs) rc = d2h(e, sb, e->P.gsb, Gp);
+  if (!rc && logs) rc = d2h(e, rotb, e->P.grotb, Gp);
+  if (!rc && logs) rc = d2h(e, sb2, e->P.gsb2, Gp);
   std::vector<SsRec> gss;
   if (!rc) rc = d2h(e, gss, e->P.gss, Gp);
   if (!rc && logs) rc = d2h(e, lt, e->P.log_term, R * KP * Gp);
@@ -597,7 +603,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
         }
       // physical slot of entry idx (raft_device.hpp ring_slot)
       auto pslot = [&](int64_t idx) {
-        return uint64_t((idx - 1 + (idx >= sb[g] ? rot[g] : rota[g])) & int64_t(KP - 1));
+        return uint64_t((idx - 1 + (idx >= sb[g] ? rot[g] : (idx >= sb2[g] ? rota[g] : rotb[g]))) & int64_t(KP - 1));
       };
       if (logs && last[d] > 0) {
         const int32_t want = lt[ring_index(r, g, pslot(last[d]), KP, R)];
@@ -734,6 +740,8 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.grot, rot);
   if (!rc) rc = h2d(e, e->P.grota, rot);
   if (!rc) rc = h2d(e, e->P.gsb, sb0);
+  if (!rc) rc = h2d(e, e->P.grotb, rot);
+  if (!rc) rc = h2d(e, e->P.gsb2, sb0);
   if (!rc && raft) rc = h2d(e, e->P.xnext, xn);
   if (!rc && e->cfg.payload_crc) rc = h2d(e, e->P.log_crc, lcrc);
   if (!rc) rc = h2d(e, e->P.log_term, lt);

@@ -125,6 +125,8 @@ struct WordAcc {
   int32_t* hb_;
   int32_t* sb_;
   SsRec* ss_;
+  uint16_t* rotb_;
+  int32_t* sb2_;
   uint32_t g;
   __device__ __forceinline__ uint16_t& meta() const { if constexpr (LDS) return *meta_; else return raftstep::at(meta_, g); }
   __device__ __forceinline__ uint16_t& rot() const { if constexpr (LDS) return *rot_; else return raftstep::at(rot_, g); }
@@ -132,6 +134,8 @@ struct WordAcc {
   __device__ __forceinline__ uint8_t& iso() const { if constexpr (LDS) return *iso_; else return raftstep::at(iso_, g); }
   __device__ __forceinline__ int32_t& hb() const { if constexpr (LDS) return *hb_; else return raftstep::at(hb_, g); }
   __device__ __forceinline__ int32_t& sb() const { if constexpr (LDS) return *sb_; else return raftstep::at(sb_, g); }
+  __device__ __forceinline__ uint16_t& rotb() const { if constexpr (LDS) return *rotb_; else return raftstep::at(rotb_, g); }
+  __device__ __forceinline__ int32_t& sb2() const { if constexpr (LDS) return *sb2_; else return raftstep::at(sb2_, g); }
   __device__ __forceinline__ SsRec& ss() const { if constexpr (LDS) return *ss_; else return ss_[g]; }
   template <bool WT>
   __device__ __forceinline__ void st_hb(int32_t v) const {
@@ -144,7 +148,7 @@ __device__ __forceinline__ RowAcc<R, false> rows_global(const DevPlanes& P, uint
   return RowAcc<R, false>{P.rec, rix<R>(g, 0)};
 }
 __device__ __forceinline__ WordAcc<false> words_global(const DevPlanes& P, uint32_t g) {
-  return WordAcc<false>{P.gmeta, P.grot, P.grota, P.giso, P.hb, P.gsb, P.gss, g};
+  return WordAcc<false>{P.gmeta, P.grot, P.grota, P.giso, P.hb, P.gsb, P.gss, P.grotb, P.gsb2, g};
 }
 
 // A ONECAND group is taken only when a replica is isolated this tick (its
@@ -236,8 +240,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   uint32_t wr = 0;      // replicas that append this tick's entries (leader + accepting followers)
   int w_term = 0, w_ph = 0;    // their term and the ring slot of the first entry
   uint64_t w_vb = 0;    // value stream base of this tick's entries
-  int cp_n = 0, cp_from = 0, cp_sb = 0;   // RAFT: a returning stale leader's catch-up copy (see the ring writes)
-  uint32_t cp_cs = 0, cp_rot = 0;
+  int cp_n = 0, cp_from = 0, cp_sb = 0, cp_sb2 = 0;   // RAFT: a returning stale leader's catch-up copy (ring writes)
+  uint32_t cp_cs = 0, cp_rot = 0, cp_rotb = 0;
   uint32_t df = 0;      // diagnostics: lane class bits (P.dbg)
   bool stored = false;  // the group's rows may have been written (returned)
   // deferral-reason bits 11-15 only in a diagnostics build (make DIAG=1),
@@ -631,11 +635,11 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       // whose wave waits on it): sr's NextIndex for p0 and the terms of both
       // logs at L0 and L0+1 (the ring addresses are valid whatever the values)
       const uint64_t tb = ring_tile(g, P.KP, R);
-      const uint32_t rot = GW.rot(), rota = GW.rota();
-      const int sbo = GW.sb();
+      const uint32_t rot = GW.rot(), rota = GW.rota(), rotb = GW.rotb();
+      const int sbo = GW.sb(), sb2 = GW.sb2();
       const int p0 = sr == 0 ? 1 : 0;   // the lowest-id peer: where sr's own round goes first
-      const uint32_t o0 = ring_in_tile(g, R, ring_slot(L0, rot, rota, sbo, P.kmask), 0u);
-      const uint32_t o1 = ring_in_tile(g, R, ring_slot(L0 + 1, rot, rota, sbo, P.kmask), 0u);
+      const uint32_t o0 = ring_in_tile(g, R, ring_slot(L0, rot, rota, rotb, sbo, sb2, P.kmask), 0u);
+      const uint32_t o1 = ring_in_tile(g, R, ring_slot(L0 + 1, rot, rota, rotb, sbo, sb2, P.kmask), 0u);
       const int32_t* const rt = P.log_term + tb;
       const int nx0 = at(prow(P.xnext, sr * R + p0, P.Gp), g);
       const int tc0 = at(rt, o0 + uint32_t(c)), ts0 = at(rt, o0 + uint32_t(sr));
@@ -654,7 +658,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         cp_from = L0 + 1;
         cp_cs = uint32_t(c) | (uint32_t(sr) << 4);
         cp_rot = rot | (rota << 16);
+        cp_rotb = rotb;
         cp_sb = sbo;
+        cp_sb2 = sb2;
         sr_dur = T.f_min + int(uint32_t(rng_k(key, uint32_t(sr), ST_TIMER_F, uint64_t(T.tick)) >> 32) %
                                uint32_t(T.f_span));
         const int nl = Ll + n;
@@ -778,13 +784,13 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           if (n) {
             const uint64_t xvb = rng_k(key, uint32_t(xi), ST_VALUE, uint64_t(T.tick));
             const uint64_t tb = ring_tile(g, P.KP, R);
-            const uint32_t xrot = GW.rot(), xrota = GW.rota();
-            const int xsb = GW.sb();
+            const uint32_t xrot = GW.rot(), xrota = GW.rota(), xrotb = GW.rotb();
+            const int xsb = GW.sb(), xsb2 = GW.sb2();
             uint32_t cs = 0;
             if constexpr (CRC) cs = crc_term_state(tab, x_term);
             for (int e = 0; e < n; ++e) {
               const int64_t v = int64_t(sm64(xvb ^ uint64_t(uint32_t(e))) >> 1);
-              const uint32_t o = ring_in_tile(g, R, ring_slot(xl + 1 + e, xrot, xrota, xsb, P.kmask), uint32_t(xi));
+              const uint32_t o = ring_in_tile(g, R, ring_slot(xl + 1 + e, xrot, xrota, xrotb, xsb, xsb2, P.kmask), uint32_t(xi));
               st<WT>(P.log_term + tb, o, x_term);
               st<WT>(P.log_value + tb, o, v);
               if constexpr (CRC) st<WT>(P.log_crc + tb, o, crc_value_final(tab, cs, v));
@@ -848,10 +854,14 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
               hi = max(hi, pre);
             }
             const int sbo = GW.sb();
+            const uint32_t rota = GW.rota();
+            const bool ok = ring_switch_ok(d, uint32_t(rot), rota, sbo, GW.sb2(), lo, P.K, P.kmask);
             df |= hi > Ll ? 64u : 0u;
-            df |= (sbo <= 1 || sbo <= lo - int(P.K) + 1) ? 0u : 128u;
-            if (hi <= Ll && (sbo <= 1 || sbo <= lo - int(P.K) + 1)) {
+            df |= ok ? 0u : 128u;
+            if (hi <= Ll && ok) {
               df |= 32u;
+              GW.rotb() = uint16_t(rota);   // the three segments shift
+              GW.sb2() = sbo;
               GW.rota() = uint16_t(rot);
               GW.sb() = Ll + 1;
               rot = (rot + int(d)) & int(P.kmask);
@@ -861,8 +871,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           }
         } else {   // rare: write here, each replica at its own LastApplied+1+e
           const uint64_t tb = ring_tile(g, P.KP, R);
-          const uint32_t rota = GW.rota();
-          const int sb = GW.sb();
+          const uint32_t rota = GW.rota(), rotb = GW.rotb();
+          const int sb = GW.sb(), sb2 = GW.sb2();
           uint32_t cs = 0;
           if constexpr (CRC) cs = crc_term_state(tab, Lt);
           for (int e = 0; e < n; ++e) {
@@ -873,7 +883,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             for (int p = 0; p < R; ++p) {
               if (p != c && !((okm >> p) & 1u)) continue;
               const int i0 = p == c ? Ll : last[p] - n;
-              const uint32_t o = ring_in_tile(g, R, ring_slot(i0 + e + 1, uint32_t(rot), rota, sb, P.kmask), uint32_t(p));
+              const uint32_t o = ring_in_tile(g, R, ring_slot(i0 + e + 1, uint32_t(rot), rota, rotb, sb, sb2, P.kmask), uint32_t(p));
               st<WT>(P.log_term + tb, o, Lt);
               st<WT>(P.log_value + tb, o, v);
               if constexpr (CRC) st<WT>(P.log_crc + tb, o, stamp);
@@ -937,12 +947,14 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       const int src = int(__builtin_ctzll(pend));
       pend &= pend - 1ull;
       const int cnt = __shfl(cp_n, src), from = __shfl(cp_from, src), sb_ = __shfl(cp_sb, src);
+      const int sb2_ = __shfl(cp_sb2, src);
       const uint32_t cs = uint32_t(__shfl(int(cp_cs), src)), rr = uint32_t(__shfl(int(cp_rot), src));
+      const uint32_t rb = uint32_t(__shfl(int(cp_rotb), src));
       const uint32_t gg = uint32_t(__shfl(int(g), src));
       const uint64_t tb = ring_tile(gg, P.KP, R);
       const uint32_t cc = cs & 15u, ss = cs >> 4;
       for (int j = lane; j < cnt; j += 64) {
-        const uint32_t o = ring_in_tile(gg, R, ring_slot(from + j, rr & 0xFFFFu, rr >> 16, sb_, P.kmask), 0u);
+        const uint32_t o = ring_in_tile(gg, R, ring_slot(from + j, rr & 0xFFFFu, rr >> 16, rb, sb_, sb2_, P.kmask), 0u);
         const int32_t t = at(P.log_term + tb, o + cc);
         const int64_t v = at(P.log_value + tb, o + cc);
         st<WT>(P.log_term + tb, o + ss, t);
@@ -1122,7 +1134,8 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
   __shared__ uint32_t sg[256];
   __shared__ SsRec sgss[256];
   __shared__ int32_t shb[256], sgsb[256];
-  __shared__ uint16_t smeta[256], sgrot[256], sgrota[256];
+  __shared__ uint16_t smeta[256], sgrot[256], sgrota[256], sgrotb[256];
+  __shared__ int32_t sgsb2[256];
   __shared__ uint8_t sgiso[256], sdirty[256];
   shard_zero(next_count);
   const uint32_t n = shard_prefix(count, pre);
@@ -1134,15 +1147,17 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
     const uint32_t g = i < n ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
     const bool valid = g < P.G;
     sg[t] = g;
-    uint16_t m0 = 0, r0 = 0, ra0 = 0;
+    uint16_t m0 = 0, r0 = 0, ra0 = 0, rb0 = 0;
     uint8_t gi0 = 0;
-    int32_t hb0 = 0, sb0 = 0;
+    int32_t hb0 = 0, sb0 = 0, sb20 = 0;
     SsRec ss0{0, 0, 0, 0};
     if (valid) {
       m0 = at(P.gmeta, g); r0 = at(P.grot, g); ra0 = at(P.grota, g); gi0 = at(P.giso, g);
       hb0 = at(P.hb, g); sb0 = at(P.gsb, g); ss0 = P.gss[g];
+      rb0 = at(P.grotb, g); sb20 = at(P.gsb2, g);
     }
     smeta[t] = m0; sgrot[t] = r0; sgrota[t] = ra0; sgiso[t] = gi0; shb[t] = hb0; sgsb[t] = sb0; sgss[t] = ss0;
+    sgrotb[t] = rb0; sgsb2[t] = sb20;
     __syncthreads();
     {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
       const int4* grec = reinterpret_cast<const int4*>(P.rec);
@@ -1157,7 +1172,7 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
     }
     __syncthreads();
     const RowAcc<R, true> rw{&srec[t * RW], 0u};
-    const WordAcc<true> gw{&smeta[t], &sgrot[t], &sgrota[t], &sgiso[t], &shb[t], &sgsb[t], &sgss[t], g};
+    const WordAcc<true> gw{&smeta[t], &sgrot[t], &sgrota[t], &sgiso[t], &shb[t], &sgsb[t], &sgss[t], &sgrotb[t], &sgsb2[t], g};
     const bool wrote = fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab, rw, gw);
     sdirty[t] = valid && wrote;
     __syncthreads();
@@ -1176,6 +1191,8 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
       if (sgiso[t] != gi0) at(P.giso, g) = sgiso[t];
       if (shb[t] != hb0) at(P.hb, g) = shb[t];
       if (sgsb[t] != sb0) at(P.gsb, g) = sgsb[t];
+      if (sgrotb[t] != rb0) at(P.grotb, g) = sgrotb[t];
+      if (sgsb2[t] != sb20) at(P.gsb2, g) = sgsb2[t];
       const SsRec s1 = sgss[t];
       if (s1.last != ss0.last || s1.term != ss0.term || s1.cl != ss0.cl || s1.cf != ss0.cf) P.gss[g] = s1;
     }
@@ -1282,11 +1299,19 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       const int sbo = P.KP > P.K ? at(P.gsb, g) : 0;   // (loaded with the rest: no dependent round trip for drifted lanes)
       const int wph = (L + rot) & int(P.kmask);
       int sw_d = 0;   // segment switch by this rotation jump (placement only, stored once the lane is taken)
+      int sw_rota = -1;   // the previous segment's rotation when it stays live (a third segment)
       if (take && n && wph != ph) {
         const uint32_t d = uint32_t(ph - wph) & P.kmask;
         df |= d <= P.K ? 8u : 16u;
         bool sw = false;
-        if (P.KP > P.K && d <= P.K) sw = sbo <= 1 || sbo <= L - int(P.K) + 1;   // the previous segment holds no readable entry
+        if (P.KP > P.K && d <= P.K) {
+          sw = sbo <= 1 || sbo <= L - int(P.K) + 1;   // the previous segment holds no readable entry
+          if (!sw) {   // it does: the segments shift when the oldest is dead and both jumps fit (ring_switch_ok)
+            const uint32_t rota = at(P.grota, g);
+            sw = ring_switch_ok(d, uint32_t(rot), rota, sbo, at(P.gsb2, g), L, P.K, P.kmask);
+            sw_rota = int(rota);
+          }
+        }
         if (sw) sw_d = int(d);
         else w_slot = wph;
       }
@@ -1322,6 +1347,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         at(P.hb, g) = T.now;                               // timer.Reset(d) of every follower
         if (hwx_clear) at(P.gmeta, g) = uint16_t(meta & ~M_HWX);
         if (sw_d) {   // the new segment starts at this tick's first entry
+          if (sw_rota >= 0) at(P.grotb, g) = uint16_t(sw_rota);   // (else the older segments are dead)
+          at(P.gsb2, g) = sbo;
           at(P.grota, g) = uint16_t(rot);
           at(P.gsb, g) = L + 1;
           at(P.grot, g) = uint16_t((rot + sw_d) & int(P.kmask));

@@ -27,6 +27,8 @@ __global__ __launch_bounds__(256) void init_new_kernel(DevPlanes P, Trace T) {
   P.grot[g] = 0;   // empty logs: the phase is chosen at the first append
   P.grota[g] = 0;
   P.gsb[g] = 0;
+  P.grotb[g] = 0;
+  P.gsb2[g] = 0;
 }
 
 // Post-election state (KAT-1 generalised).
@@ -62,6 +64,8 @@ __global__ __launch_bounds__(256) void init_steady_kernel(DevPlanes P, Trace T, 
   P.grot[g] = uint16_t(T.entries_before(T.tick + 1) & P.kmask);   // entry 1 lands in the global phase
   P.grota[g] = 0;
   P.gsb[g] = 0;
+  P.grotb[g] = 0;
+  P.gsb2[g] = 0;
 }
 
 // State digest (raft_state_digest): one lane per group derives the canonical
@@ -117,11 +121,11 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
         h = dg_mix(h, lo32(m) | (lo32(nx) << 32));
       }
       const uint64_t rb = ring_tile(g, P.KP, R);
-      const uint32_t rot = at(P.grot, g), rota = at(P.grota, g);
-      const int sb = at(P.gsb, g);
+      const uint32_t rot = at(P.grot, g), rota = at(P.grota, g), rotb = at(P.grotb, g);
+      const int sb = at(P.gsb, g), sb2 = at(P.gsb2, g);
 #pragma unroll 1
       for (int idx = hwm > int(P.K) ? hwm - int(P.K) + 1 : 1; idx <= l; ++idx) {
-        const uint32_t o = ring_in_tile(g, R, ring_slot(idx, rot, rota, sb, P.kmask), uint32_t(r));
+        const uint32_t o = ring_in_tile(g, R, ring_slot(idx, rot, rota, rotb, sb, sb2, P.kmask), uint32_t(r));
         h = dg_mix(h, lo32(at(P.log_term + rb, o)) | (lo32(idx) << 32));
         h = dg_mix(h, uint64_t(at(P.log_value + rb, o)));
         h = dg_mix(h, P.crc_on ? uint64_t(at(P.log_crc + rb, o)) : 0ull);

@@ -79,6 +79,8 @@ struct DevPlanes {
   uint16_t* grot;      // ring rotation of the current segment: entry idx >= gsb sits at slot (idx-1+grot) mod KP
   uint16_t* grota;     // rotation of the previous segment (entries idx < gsb)
   int32_t* gsb;        // first index of the current segment (0: one segment)
+  uint16_t* grotb;     // rotation of the segment before the previous one (entries idx < gsb2)
+  int32_t* gsb2;       // first index of the previous segment (0: none older)
   int32_t* lterm;      // [Gp][R] Log[len-1].Term: cached term of each replica's last entry
   int32_t* log_term;   // Log.Term  ring, tiles [Gp/64][KP][64][R] (ring_tile / ring_in_tile)
   int64_t* log_value;  // Log.Value ring
@@ -147,13 +149,25 @@ __device__ __forceinline__ void shard_zero(uint32_t* cnt) {   // block 0, thread
 // entries_before(t) mod KP that every steady wave writes, and would write
 // partial ring lines from then on. With KP = 2K its rotation can instead be
 // switched without moving a single entry: entries idx >= gsb use the new
-// rotation, older ones the previous one (grota). Safe when the jump
-// d = new - old rotation is in [1, K] (the new segment's slots then only
-// reach an old slot once the entry there is more than K behind every log
-// that writes it), no log holds an entry at or above gsb yet, and the
-// previous segment holds no readable entry (the last K of any log).
-__device__ __forceinline__ uint32_t ring_slot(int idx, uint32_t rot, uint32_t rota, int sb, uint32_t kmask) {
-  return uint32_t(idx - 1 + int(idx >= sb ? rot : rota)) & kmask;
+// rotation, entries in [gsb2, gsb) the previous one (grota), older ones the
+// one before (grotb). A switch shifts the three (grotb = grota, gsb2 = gsb,
+// grota = grot, gsb = first new index) and is safe when no log holds an
+// entry at or above the new gsb yet, the oldest segment (idx < gsb2) holds
+// no readable entry (the last K of any log), and the live entries still fit
+// KP = 2K slots: in unwrapped slot positions they span K-1 plus the jumps
+// between live segments, so the new jump d plus the previous one (when the
+// previous segment is still live) must be at most K (ring_switch_ok).
+__device__ __forceinline__ uint32_t ring_slot(int idx, uint32_t rot, uint32_t rota, uint32_t rotb, int sb, int sb2,
+                                              uint32_t kmask) {
+  return uint32_t(idx - 1 + int(idx >= sb ? rot : (idx >= sb2 ? rota : rotb))) & kmask;
+}
+// lo: the shortest log (before this tick); d: the jump to the global phase
+__device__ __forceinline__ bool ring_switch_ok(uint32_t d, uint32_t rot, uint32_t rota, int sb, int sb2, int lo,
+                                               uint32_t K, uint32_t kmask) {
+  const int first = lo - int(K) + 1;   // oldest readable index of any log
+  if (d == 0u || d > K || !(sb2 <= 1 || sb2 <= first)) return false;
+  if (sb <= 1 || sb <= first) return true;                    // the previous segment is dead too
+  return ((rot - rota) & kmask) + d <= K;                      // it stays live: both jumps inside the window
 }
 
 // Ring layout: the log rings of all R replicas are tiled by waves of 64
@@ -348,6 +362,8 @@ struct Group {
   uint32_t rot, rot0;        // ring rotation (grot) now / as loaded
   uint32_t rota, rota0;      // previous segment's rotation (grota) now / as loaded
   int sb, sb0;               // segment boundary (gsb) now / as loaded
+  uint32_t rotb;             // the segment before (grotb, gsb2; never changed by the general path)
+  int sb2;
   uint32_t d_pm, d_pn, d_lt;
   uint32_t roles;       // 2 bits per replica
   uint32_t votes;       // 4 bits per replica: REF Voted (0/1), RAFT votedFor+1
@@ -414,6 +430,8 @@ struct Group {
     rot = rot0 = at(P.grot, g);
     rota = rota0 = at(P.grota, g);
     sb = sb0 = at(P.gsb, g);
+    rotb = at(P.grotb, g);
+    sb2 = at(P.gsb2, g);
     giso = giso0 = at(P.giso, g);
   }
   // Per-tick reset of a group whose state stays resident across ticks
@@ -548,7 +566,7 @@ struct Group {
 
   // Log ring of replica r: entry idx (1-based) at slot (idx-1) mod K.
   __device__ __forceinline__ uint32_t ring_off(const DevPlanes& P, int r, int idx) const {
-    return ring_in_tile(g, R, ring_slot(idx, rot, rota, sb, P.kmask), uint32_t(r));
+    return ring_in_tile(g, R, ring_slot(idx, rot, rota, rotb, sb, sb2, P.kmask), uint32_t(r));
   }
   // Every log of the group is empty (RAFT: nothing above LastApplied either):
   // the ring holds no entry, so its rotation is free. Chosen so that the
@@ -1197,8 +1215,8 @@ struct TickSrc {
   const uint32_t* tab;
   uint32_t crc_on;
   uint32_t R;          // replicas (ring layout)
-  uint32_t g, KP, kmask, rot, rota;
-  int sb;
+  uint32_t g, KP, kmask, rot, rota, rotb;
+  int sb, sb2;
   int leader, from;
   int cache_leader, cache_from, cache_term;
   uint64_t cache_vbase;
@@ -1211,7 +1229,7 @@ struct TickSrc {
       if (crc_on) c = crc_entry(tab, t, v);   // the leader's stamp of its own fresh entry
     } else {
       const uint64_t tb = ring_tile(g, KP, R);
-      const uint32_t o = ring_in_tile(g, R, ring_slot(idx, rot, rota, sb, kmask), uint32_t(leader));
+      const uint32_t o = ring_in_tile(g, R, ring_slot(idx, rot, rota, rotb, sb, sb2, kmask), uint32_t(leader));
       t = at(lt + tb, o);
       v = at(lv + tb, o);
       if (crc_on) c = at(lc + tb, o);

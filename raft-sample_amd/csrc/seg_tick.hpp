@@ -50,8 +50,8 @@ struct Seg {
   int64_t tick;
   int32_t now;
   int primary, fault, meta0;
-  uint32_t rot, rota;
-  int sbd;         // ring segment boundary (gsb)
+  uint32_t rot, rota, rotb;
+  int sbd, sb2;    // ring segment boundaries (gsb, gsb2)
   bool rot_dirty;  // rot / sbd changed (align_ring)
   uint32_t iso;
   uint32_t giso;   // EXT leader-isolation victims (giso plane)
@@ -123,6 +123,8 @@ struct Seg {
     rot = at(P.grot, g);
     rota = at(P.grota, g);
     sbd = at(P.gsb, g);
+    rotb = at(P.grotb, g);
+    sb2 = at(P.gsb2, g);
     rot_dirty = false;
     giso = at(P.giso, g);
     giso_dirty = false;
@@ -232,7 +234,7 @@ struct Seg {
 
   // ---------------------------------------------------------------- ring --
   __device__ __forceinline__ uint32_t ring_off(const DevPlanes& P, int r, int idx) const {
-    return ring_in_tile(g, R, ring_slot(idx, rot, rota, sbd, P.kmask), uint32_t(r));
+    return ring_in_tile(g, R, ring_slot(idx, rot, rota, rotb, sbd, sb2, P.kmask), uint32_t(r));
   }
   __device__ __forceinline__ int32_t& ring_term(const DevPlanes& P, int r, int idx) const {
     return at(P.log_term + ring_tile(g, P.KP, R), ring_off(P, r, idx));

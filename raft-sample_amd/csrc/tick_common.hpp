@@ -125,7 +125,7 @@ __device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, c
   }
 
   // 2. rounds in ascending replica id, against the roles as they are now.
-  const TickSrc base{P.log_term, P.log_value, P.log_crc, P.crc_tab, P.crc_on, uint32_t(R), G.g, P.KP, P.kmask, G.rot, G.rota, G.sb, 0, 1,
+  const TickSrc base{P.log_term, P.log_value, P.log_crc, P.crc_tab, P.crc_on, uint32_t(R), G.g, P.KP, P.kmask, G.rot, G.rota, G.rotb, G.sb, G.sb2, 0, 1,
                      G.cache_leader, G.cache_from, G.cache_term, G.cache_vbase};
   auto make_src = [base](int c) {
     TickSrc s = base;

@@ -43,6 +43,15 @@ DIGEST_CASES = {
     "raft_leader_iso_r7": (dict(replicas=7, groups=1024, client_period=1, ring_depth=64, semantics=abi.SEM_RAFT,
                                 seed=0x45, isolate_per_65536=20000, isolate_min_ticks=4, isolate_max_ticks=32,
                                 isolate_leader=1), "new", 0, 200),
+    # small ring, frequent leader-isolation windows, long run: elections, stale
+    # leaders, returns and truncations in the fast path, ring phase segments
+    # switching again while the previous segment is still live (three segments)
+    "raft_leader_iso_k16_long": (dict(replicas=5, groups=2048, client_period=1, ring_depth=16, semantics=abi.SEM_RAFT,
+                                      seed=0x46, isolate_per_65536=30000, isolate_min_ticks=4, isolate_max_ticks=16,
+                                      isolate_leader=1), "new", 0, 600),
+    "raft_hashed_iso_k32_long": (dict(replicas=7, groups=1024, client_period=1, ring_depth=32, semantics=abi.SEM_RAFT,
+                                      seed=0x47, isolate_per_65536=30000, isolate_min_ticks=4, isolate_max_ticks=24),
+                                 "new", 0, 500),
     "crc_e16_r5": (dict(replicas=5, groups=512, client_period=1, entries_per_tick=16, ring_depth=64, payload_crc=1,
                         corrupt_per_65536=3000, seed=0x5EED0005), "steady", 1, 20),
 }
