@@ -382,6 +382,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.gmeta), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.giso), Gp);
   A(reinterpret_cast<void**>(&e->P.gss), Gp * sizeof(SsRec));
+  A(reinterpret_cast<void**>(&e->P.glx), Gp * sizeof(LxRec));
   A(reinterpret_cast<void**>(&e->P.grot), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.grota), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.gsb), Gp * 4);
@@ -446,6 +447,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
                                            e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.giso, 0, Gp, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gss, 0, Gp * sizeof(SsRec), e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.glx, 0, Gp * sizeof(LxRec), e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grot, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grota, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gsb, 0, Gp * 4, e->stream) : z;
@@ -538,6 +540,8 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!rc && logs) rc = d2h(e, sb2, e->P.gsb2, Gp);
   std::vector<SsRec> gss;
   if (!rc) rc = d2h(e, gss, e->P.gss, Gp);
+  std::vector<LxRec> glx;
+  if (!rc) rc = d2h(e, glx, e->P.glx, Gp);
   if (!rc && logs) rc = d2h(e, lt, e->P.log_term, R * KP * Gp);
   if (!rc && logs) rc = d2h(e, lv, e->P.log_value, R * KP * Gp);
   const bool crcs = v->log_crc && e->cfg.payload_crc;
@@ -560,7 +564,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
     if (!(meta[g] & M_SSYNC) || pr >= int(R)) continue;
     for (uint64_t r = 0; r < R; ++r) {
       term[g * R + r] = gss[g].term;
-      last[g * R + r] = gss[g].last;
+      last[g * R + r] = ss_last(gss[g], int(r), pr, meta[g], glx[g]);
       commit[g * R + r] = int(r) == pr ? gss[g].cl : gss[g].cf;
       if (!ltm.empty()) ltm[g * R + r] = gss[g].term;
     }
@@ -1108,8 +1112,10 @@ int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap) {
   std::string out;
   uint16_t meta = 0;
   SsRec ss{};
+  LxRec lx{};
   HIPCHK(hipMemcpyAsync(&meta, e->P.gmeta + group, 2, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipMemcpyAsync(&ss, e->P.gss + group, sizeof ss, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&lx, e->P.glx + group, sizeof lx, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   const int pr = meta & 0xF;
   const bool ssync = (meta & M_SSYNC) && pr < int(e->cfg.replicas);   // compressed state
@@ -1121,7 +1127,7 @@ int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap) {
     HIPCHK(hipMemcpyAsync(&last, e->P.last + d, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&rs, e->P.rs + d, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    if (ssync) { term = ss.term; last = ss.last; commit = int(r) == pr ? ss.cl : ss.cf; }
+    if (ssync) { term = ss.term; last = ss_last(ss, int(r), pr, meta, lx); commit = int(r) == pr ? ss.cl : ss.cf; }
     char line[128];
     snprintf(line, sizeof line, "[Server%u:%d:%d:%d][%s]\n", r, term, commit, last, names[rs & 3]);
     out += line;

@@ -127,6 +127,7 @@ struct WordAcc {
   SsRec* ss_;
   uint16_t* rotb_;
   int32_t* sb2_;
+  LxRec* lx_;
   uint32_t g;
   __device__ __forceinline__ uint16_t& meta() const { if constexpr (LDS) return *meta_; else return raftstep::at(meta_, g); }
   __device__ __forceinline__ uint16_t& rot() const { if constexpr (LDS) return *rot_; else return raftstep::at(rot_, g); }
@@ -136,6 +137,7 @@ struct WordAcc {
   __device__ __forceinline__ int32_t& sb() const { if constexpr (LDS) return *sb_; else return raftstep::at(sb_, g); }
   __device__ __forceinline__ uint16_t& rotb() const { if constexpr (LDS) return *rotb_; else return raftstep::at(rotb_, g); }
   __device__ __forceinline__ int32_t& sb2() const { if constexpr (LDS) return *sb2_; else return raftstep::at(sb2_, g); }
+  __device__ __forceinline__ LxRec& lx() const { if constexpr (LDS) return *lx_; else return lx_[g]; }
   __device__ __forceinline__ SsRec& ss() const { if constexpr (LDS) return *ss_; else return ss_[g]; }
   template <bool WT>
   __device__ __forceinline__ void st_hb(int32_t v) const {
@@ -148,7 +150,7 @@ __device__ __forceinline__ RowAcc<R, false> rows_global(const DevPlanes& P, uint
   return RowAcc<R, false>{P.rec, rix<R>(g, 0)};
 }
 __device__ __forceinline__ WordAcc<false> words_global(const DevPlanes& P, uint32_t g) {
-  return WordAcc<false>{P.gmeta, P.grot, P.grota, P.giso, P.hb, P.gsb, P.gss, P.grotb, P.gsb2, g};
+  return WordAcc<false>{P.gmeta, P.grot, P.grota, P.giso, P.hb, P.gsb, P.gss, P.grotb, P.gsb2, P.glx, g};
 }
 
 // A ONECAND group is taken only when a replica is isolated this tick (its
@@ -279,9 +281,11 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     if (go) {
       if (ss) {
         const SsRec ss_rec = GW.ss();
+        const LxRec lxr = (RAFT && (meta & M_LXS)) ? GW.lx() : LxRec{0, 0};   // LXS: the leader is k ahead
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          term[r] = ss_rec.term; last[r] = ss_rec.last; commit[r] = r == c ? ss_rec.cl : ss_rec.cf; lt[r] = ss_rec.term;
+          term[r] = ss_rec.term; last[r] = ss_last(ss_rec, r, c, meta, lxr); commit[r] = r == c ? ss_rec.cl : ss_rec.cf;
+          lt[r] = ss_rec.term;
         }
       } else {
         RW.load(PL_TERM, term);
@@ -448,11 +452,14 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       }
       if (!bail) {
         df |= 131072u;
-        if (ss) {   // the record's rows become explicit (the leader's elements change below)
-          const SsRec ss_rec = GW.ss();   // (re-read: rare, keeps it out of the live registers)
+        // a compressed group stays compressed (LXS: the record holds the
+        // followers, glx the leader's lead and the earliest follower deadline,
+        // and the lean kernel takes the following ticks of the window)
+        const bool to_lxs = ss && w < 0 && T.iso_leader && Llt == Lt;
+        if (ss && !to_lxs) {   // the record's rows become explicit (the leader's elements change below)
           int trow[R], lrow[R], crow[R];
 #pragma unroll
-          for (int p = 0; p < R; ++p) { trow[p] = ss_rec.term; lrow[p] = ss_rec.last; crow[p] = p == c ? ss_rec.cl : ss_rec.cf; }
+          for (int p = 0; p < R; ++p) { trow[p] = term[p]; lrow[p] = last[p]; crow[p] = commit[p]; }
           RW.store(PL_TERM, trow);
           RW.store(PL_LAST, lrow);
           RW.store(PL_COMMIT, crow);
@@ -464,15 +471,27 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         sv[3] = 1;
         sv[4] = 0;
         if (n) {
-          RW.template st<WT>(PL_LAST, c, Ll + n);
-          if (Llt != Lt) RW.template st<WT>(PL_LTERM, c, Lt);
+          if (!to_lxs) {
+            RW.template st<WT>(PL_LAST, c, Ll + n);
+            if (Llt != Lt) RW.template st<WT>(PL_LTERM, c, Lt);
+          }
           wr = 1u << c;                                   // only the leader's log grows
           w_term = Lt;
           w_ph = int((uint32_t(Ll) + uint32_t(GW.rot())) & P.kmask);
           w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
         }
-        if (cm != Lc) RW.template st<WT>(PL_COMMIT, c, cm);
-        int nm = (meta | M_MSYNC) & ~(M_SSYNC | M_HWX);   // (no truncated log here: hwup == 0)
+        if (cm != Lc && !to_lxs) RW.template st<WT>(PL_COMMIT, c, cm);
+        int nm = (meta | M_MSYNC) & ~(M_SSYNC | M_HWX | M_LXS);   // (no truncated log here: hwup == 0)
+        if (to_lxs) {
+          const int f = c == 0 ? 1 : 0;   // any follower (SSYNC: one length, term, CommitIndex)
+          int dmin = I32MAX;
+#pragma unroll
+          for (int p = 0; p < R; ++p)
+            if (p != c) dmin = min(dmin, max(ts[p], hbt) + (rsv[p] >> 6));
+          GW.ss() = SsRec{sel(last, f), Lt, cm, sel(commit, f)};
+          GW.lx() = LxRec{Ll + n - sel(last, f), dmin};
+          nm |= M_SSYNC | M_LXS;
+        }
         if (w >= 0) {   // the election (see above)
           const int nt = Lt + 1, fl = sel(last, w);
           const int dc = T.c_min + int(uint32_t(rng_k(key, uint32_t(w), ST_TIMER_C, uint64_t(T.tick)) >> 32) %
@@ -496,7 +515,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           RW.store(PL_LMATCH, mz);
           RW.store(PL_LNEXT, nx);
           // w (the highest term) becomes the primary; the cut-off leader is a stale one
-          nm = (meta & ~(0xF | M_MSYNC | M_SSYNC | M_HWX | M_STEADY | M_ONECAND)) | w | M_ONESTALE;
+          nm = (meta & ~(0xF | M_MSYNC | M_SSYNC | M_HWX | M_LXS | M_STEADY | M_ONECAND)) | w | M_ONESTALE;
           sv[4] = 1;       // term bumps: w's timeout
           sv[5] = R - 2;   // votes granted
           sv[6] = 1;       // elections won
@@ -732,9 +751,12 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       } else {
       if (ss) {   // leaving the compressed form: the rows as they stood, then the element stores below
         const SsRec ss_rec = GW.ss();   // (re-read: rare, keeps it out of the live registers)
+        const LxRec lxr = (RAFT && (meta & M_LXS)) ? GW.lx() : LxRec{0, 0};
         int trow[R], lrow[R], crow[R];
 #pragma unroll
-        for (int p = 0; p < R; ++p) { trow[p] = ss_rec.term; lrow[p] = ss_rec.last; crow[p] = p == c ? ss_rec.cl : ss_rec.cf; }
+        for (int p = 0; p < R; ++p) {
+          trow[p] = ss_rec.term; lrow[p] = ss_last(ss_rec, p, c, meta, lxr); crow[p] = p == c ? ss_rec.cl : ss_rec.cf;
+        }
         RW.store(PL_TERM, trow);
         RW.store(PL_LAST, lrow);
         RW.store(PL_COMMIT, crow);
@@ -816,6 +838,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       // RAFT: MSYNC also makes NextIndex (= match+1) and the high-water marks (= last) implicit
       int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
       nm = (sync && hwx) ? (nm | M_HWX) : (nm & ~M_HWX);
+      nm &= ~M_LXS;   // (a fresh record when compressed: every log at Ll+n)
       nm = keep_ss ? (nm | M_SSYNC) : (nm & ~M_SSYNC);
       if (x_fire) nm = (nm & ~M_STEADY) | M_ONECAND;
       if (sr >= 0) nm = (nm & ~M_ONESTALE) | M_STEADY;   // one leader, every other replica a follower
@@ -1136,6 +1159,7 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
   __shared__ int32_t shb[256], sgsb[256];
   __shared__ uint16_t smeta[256], sgrot[256], sgrota[256], sgrotb[256];
   __shared__ int32_t sgsb2[256];
+  __shared__ LxRec sglx[256];
   __shared__ uint8_t sgiso[256], sdirty[256];
   shard_zero(next_count);
   const uint32_t n = shard_prefix(count, pre);
@@ -1151,13 +1175,15 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
     uint8_t gi0 = 0;
     int32_t hb0 = 0, sb0 = 0, sb20 = 0;
     SsRec ss0{0, 0, 0, 0};
+    LxRec lx0{0, 0};
     if (valid) {
       m0 = at(P.gmeta, g); r0 = at(P.grot, g); ra0 = at(P.grota, g); gi0 = at(P.giso, g);
       hb0 = at(P.hb, g); sb0 = at(P.gsb, g); ss0 = P.gss[g];
       rb0 = at(P.grotb, g); sb20 = at(P.gsb2, g);
+      if (m0 & M_LXS) lx0 = P.glx[g];
     }
     smeta[t] = m0; sgrot[t] = r0; sgrota[t] = ra0; sgiso[t] = gi0; shb[t] = hb0; sgsb[t] = sb0; sgss[t] = ss0;
-    sgrotb[t] = rb0; sgsb2[t] = sb20;
+    sgrotb[t] = rb0; sgsb2[t] = sb20; sglx[t] = lx0;
     __syncthreads();
     {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
       const int4* grec = reinterpret_cast<const int4*>(P.rec);
@@ -1172,7 +1198,7 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
     }
     __syncthreads();
     const RowAcc<R, true> rw{&srec[t * RW], 0u};
-    const WordAcc<true> gw{&smeta[t], &sgrot[t], &sgrota[t], &sgiso[t], &shb[t], &sgsb[t], &sgss[t], &sgrotb[t], &sgsb2[t], g};
+    const WordAcc<true> gw{&smeta[t], &sgrot[t], &sgrota[t], &sgiso[t], &shb[t], &sgsb[t], &sgss[t], &sgrotb[t], &sgsb2[t], &sglx[t], g};
     const bool wrote = fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab, rw, gw);
     sdirty[t] = valid && wrote;
     __syncthreads();
@@ -1193,6 +1219,8 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
       if (sgsb[t] != sb0) at(P.gsb, g) = sgsb[t];
       if (sgrotb[t] != rb0) at(P.grotb, g) = sgrotb[t];
       if (sgsb2[t] != sb20) at(P.gsb2, g) = sgsb2[t];
+      const LxRec x1 = sglx[t];
+      if (x1.k != lx0.k || x1.dl != lx0.dl) P.glx[g] = x1;
       const SsRec s1 = sgss[t];
       if (s1.last != ss0.last || s1.term != ss0.term || s1.cl != ss0.cl || s1.cf != ss0.cf) P.gss[g] = s1;
     }
@@ -1253,8 +1281,9 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   stage_crc_tab<CRC>(P, tab);
   const int n = int(T.client_entries());
   const int ph = int(T.entries_before(T.tick) & P.kmask);   // global ring phase of this tick's first entry
-  bool take = false, pass = false;
+  bool take = false, pass = false, lxs = false;   // lxs: an LXS tick (the cut-off leader appends alone)
   int committed = 0, w_term = 0, w_slot = -1;   // w_slot >= 0: drifted lane, its own segment from that slot
+  uint32_t wmask = 0;                           // replicas whose ring column gets this tick's entries
   uint64_t w_vb = 0;
   uint32_t df = 0;
   if (g < P.G) {
@@ -1267,11 +1296,45 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     if (take) {
       const SsRec s = P.gss[g];
       const uint64_t key = group_key(T.seed, P.gbase + g);
-      if (T.iso_p) {   // any window over this group this tick (either mode): the list kernel
+      if (T.iso_p) {   // any window over this group this tick (either mode): the list kernel ...
         uint32_t act = 0, starting = 0;
         const uint32_t im = iso_windows<R>(key, T, &act, &starting);
-        if (T.iso_leader ? act != 0u : im != 0u) take = false;
+        if (RAFT && (meta & M_LXS)) {
+          // ... except an LXS group whose window still cuts off exactly its primary
+          uint32_t gi = act ? uint32_t(at(P.giso, g)) : 0u;
+          lxs = T.iso_leader && !starting && leader_iso_mask(act, 0u, gi, 0u, false) == (1u << c);
+          take = lxs;
+        } else if (T.iso_leader ? act != 0u : im != 0u) {
+          take = false;
+        }
+      } else if (meta & M_LXS) {
+        take = false;
       }
+      if (RAFT && lxs) {
+        // LXS tick (fast_group's isolated-leader tick in closed form): the
+        // leader appends its client entries alone (main.go:327-329), every
+        // AppendEntries it sends is dropped (EXT), nobody's timer is reset;
+        // taken while no follower's election deadline is due (an election is
+        // the list kernel's) and the leader's log is in the global ring
+        // phase. Commit (r_leader_commit): the majority order statistic is the
+        // followers' length L, an entry of the current term (SSYNC).
+        const LxRec x = P.glx[g];
+        const int L = s.last, Lc = L + x.k;
+        const int rot = at(P.grot, g);
+        take = x.dl > T.now && n < int(P.K) && int64_t(Lc) + n <= I32MAX && (n == 0 || ((Lc + rot) & int(P.kmask)) == ph);
+        if (take) {
+          const int cl2 = L > s.cl ? L : s.cl;
+          if (cl2 != s.cl) P.gss[g] = SsRec{L, s.term, cl2, s.cf};
+          P.glx[g] = LxRec{x.k + n, x.dl};
+          committed = cl2 - s.cl;
+          w_term = s.term;
+          w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+          wmask = 1u << c;
+          df |= 131072u | 256u;
+        } else {
+          pass = true;
+        }
+      } else {
       const int L = s.last;
       // (the followers' CommitIndex min(LeaderCommit, last new entry) is the
       // leader's only while that is at most L+n: a leader's CommitIndex above
@@ -1357,10 +1420,12 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         committed = cl2 - s.cl;
         w_term = s.term;
         w_vb = vb;
+        wmask = (1u << R) - 1u;
         df |= 262144u | (w_slot < 0 ? 256u : 512u);
       } else {
         pass = true;
       }
+      }   // !lxs
     }
   }
   // this tick's entries: the taken lanes at the global phase as whole ring
@@ -1384,10 +1449,10 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     bool k_on[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-      const int src = (k * 64 + lane) / R;
+      const int src = (k * 64 + lane) / R, rr = (k * 64 + lane) - src * R;
       k_src[k] = src;
       k_term[k] = __shfl(w_term, src);
-      k_on[k] = __shfl(int(wr), src) != 0;
+      k_on[k] = ((uint32_t(__shfl(int(wr ? wmask : 0u), src)) >> rr) & 1u) != 0u;   // (LXS: the leader's column)
     }
     for (int e = 0; e < n; ++e) {
       const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
@@ -1444,7 +1509,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   if (stats) {
     const int t = take ? 1 : 0;
     if constexpr (RAFT) {
-      const int v[5] = {committed, t * (R - 1), 0, t, 0};
+      // (an LXS tick: every AppendEntries of the cut-off leader dropped)
+      const int v[5] = {committed, (take && !lxs) ? R - 1 : 0, (take && lxs) ? R - 1 : 0, t, 0};
       const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
       block_stats<5>(v, idx, stats);
     } else {

@@ -87,10 +87,11 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
     const bool msync = (meta & M_MSYNC) && primary < R;
     const bool ssync = (meta & M_SSYNC) && primary < R;   // compressed state: the gss record
     const SsRec ss = ssync ? P.gss[g] : SsRec{0, 0, 0, 0};
+    const LxRec lx = (ssync && (meta & M_LXS)) ? P.glx[g] : LxRec{0, 0};
     const int hb = at(P.hb, g);
     int last[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) last[r] = ssync ? ss.last : at(P.last, rix<R>(g, r));
+    for (int r = 0; r < R; ++r) last[r] = ssync ? ss_last(ss, r, primary, meta, lx) : at(P.last, rix<R>(g, r));
     h = sm64(0x5241465444494721ULL ^ (P.gbase + g));
 #pragma unroll 1
     for (int r = 0; r < R; ++r) {

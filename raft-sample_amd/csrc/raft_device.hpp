@@ -53,7 +53,18 @@ constexpr int M_SSYNC = 1 << 13;
 // plane is at most LastApplied everywhere, so readers that only need the
 // steady case (the lean kernel) skip the plane.
 constexpr int M_HWX = 1 << 14;
+// LXS (RAFT, with SSYNC, MSYNC and STEADY): the primary leader is cut off
+// (leader isolation) and appends alone; the gss record holds the followers
+// (and the shared term / commit fields), the leader's log is k entries longer,
+// glx[g] = {k, D} with D the earliest follower election deadline (no
+// follower timer moves while the leader is cut off).
+constexpr int M_LXS = 1 << 15;
+struct __attribute__((aligned(8))) LxRec { int32_t k, dl; };
 struct __attribute__((aligned(16))) SsRec { int32_t last, term, cl, cf; };
+// LastApplied of replica r of an SSYNC group (LXS: the primary is k ahead)
+__device__ __host__ __forceinline__ int32_t ss_last(const SsRec& s, int r, int primary, int meta, const LxRec& x) {
+  return s.last + ((meta & M_LXS) && r == primary ? x.k : 0);
+}
 constexpr int HB_NONE = -2147483647 - 1;
 constexpr int I32MAX = 2147483647;
 constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to cut atomic contention
@@ -76,6 +87,7 @@ struct DevPlanes {
   uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
   uint8_t* giso;       // [Gp] EXT leader-isolation victims, nibble per epoch parity: 8 | replica (0 = none)
   SsRec* gss;          // [Gp] the compressed state of an SSYNC group
+  LxRec* glx;          // [Gp] LXS: the cut-off leader's extra entries and the earliest follower deadline
   uint16_t* grot;      // ring rotation of the current segment: entry idx >= gsb sits at slot (idx-1+grot) mod KP
   uint16_t* grota;     // rotation of the previous segment (entries idx < gsb)
   int32_t* gsb;        // first index of the current segment (0: one segment)
@@ -469,9 +481,11 @@ struct Group {
     // materialise the compressed state of an SSYNC group (written back by store)
     if ((meta0 & M_SSYNC) && primary < R) {
       const SsRec s = P.gss[g];
+      const LxRec x = (meta0 & M_LXS) ? P.glx[g] : LxRec{0, 0};
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        term[r] = s.term; last[r] = s.last; commit[r] = r == primary ? s.cl : s.cf; ltm[r] = s.term;
+        term[r] = s.term; last[r] = ss_last(s, r, primary, meta0, x); commit[r] = r == primary ? s.cl : s.cf;
+        ltm[r] = s.term;
       }
       d_term = d_last = d_commit = d_lt = (1u << R) - 1u;
     }

@@ -151,7 +151,8 @@ struct Seg {
     dl = (role == ROLE_L ? ts : max(ts, hbt)) + dur;   // effective timer start counts the heartbeat
     if ((meta0 & M_SSYNC) && primary < R && act) {     // compressed state (Group::load)
       const SsRec s = P.gss[g];
-      term = s.term; last = s.last; commit = me == primary ? s.cl : s.cf; ltm = s.term;
+      const LxRec x = (meta0 & M_LXS) ? P.glx[g] : LxRec{0, 0};
+      term = s.term; last = ss_last(s, me, primary, meta0, x); commit = me == primary ? s.cl : s.cf; ltm = s.term;
       dirty |= SD_TERM | SD_LAST | SD_COMMIT | SD_LT;
     }
     if (!act) { role = ROLE_F; dl = I32MAX; last = 0; hw = 0; }
