@@ -1113,8 +1113,7 @@ __device__ __forceinline__ void stage_crc_tab(const DevPlanes& P, uint32_t* tab)
   if constexpr (CRC) {
     const uint4* src = reinterpret_cast<const uint4*>(P.crc_tab);
     uint4* dst = reinterpret_cast<uint4*>(tab);
-    dst[threadIdx.x] = src[threadIdx.x];
-    dst[threadIdx.x + 256] = src[threadIdx.x + 256];
+    for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) dst[i] = src[i];   // (blocks of 64..256 lanes)
     __syncthreads();
   }
 }
@@ -1143,8 +1142,8 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
 // (RowAcc / WordAcc over the __shared__ arrays: ds_ instructions), and
 // writes back the records
 // it may have changed (coalesced) and the per-group words that did change.
-template <int R, bool WT, bool CRC, int SEM>
-__global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, unsigned long long* stats,
+template <int R, bool WT, bool CRC, int SEM, int LB>
+__global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, unsigned long long* stats,
                                                         uint32_t* work, int32_t* work_tick, uint32_t* work_count,
                                                         const uint32_t* list, const uint32_t* count,
                                                         uint32_t* next_count) {
@@ -1152,21 +1151,21 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
   constexpr uint32_t RQ = RW / 4;      // 16-B pieces per record
   __shared__ uint32_t tab[CRC ? 2048 : 1];
   __shared__ uint32_t pre[NSHARD + 1];
-  __shared__ int4 srec4[256 * RQ];
+  __shared__ int4 srec4[LB * RQ];
   int32_t* const srec = reinterpret_cast<int32_t*>(srec4);
-  __shared__ uint32_t sg[256];
-  __shared__ SsRec sgss[256];
-  __shared__ int32_t shb[256], sgsb[256];
-  __shared__ uint16_t smeta[256], sgrot[256], sgrota[256], sgrotb[256];
-  __shared__ int32_t sgsb2[256];
-  __shared__ LxRec sglx[256];
-  __shared__ uint8_t sgiso[256], sdirty[256];
+  __shared__ uint32_t sg[LB];
+  __shared__ SsRec sgss[LB];
+  __shared__ int32_t shb[LB], sgsb[LB];
+  __shared__ uint16_t smeta[LB], sgrot[LB], sgrota[LB], sgrotb[LB];
+  __shared__ int32_t sgsb2[LB];
+  __shared__ LxRec sglx[LB];
+  __shared__ uint8_t sgiso[LB], sdirty[LB];
   shard_zero(next_count);
   const uint32_t n = shard_prefix(count, pre);
-  if (blockIdx.x * 256u >= n) return;
+  if (blockIdx.x * uint32_t(LB) >= n) return;
   stage_crc_tab<CRC>(P, tab);
   const uint32_t t = threadIdx.x;
-  for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+  for (uint32_t base = blockIdx.x * uint32_t(LB); base < n; base += gridDim.x * uint32_t(LB)) {
     const uint32_t i = base + t;
     const uint32_t g = i < n ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
     const bool valid = g < P.G;
@@ -1190,11 +1189,11 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
       int4 v[RQ];
 #pragma unroll
       for (uint32_t k = 0; k < RQ; ++k) {
-        const uint32_t w = t + 256u * k, j = w / RQ, gj = sg[j];
+        const uint32_t w = t + uint32_t(LB) * k, j = w / RQ, gj = sg[j];
         v[k] = gj < P.G ? grec[uint64_t(gj) * RQ + (w - j * RQ)] : int4{0, 0, 0, 0};
       }
 #pragma unroll
-      for (uint32_t k = 0; k < RQ; ++k) srec4[t + 256u * k] = v[k];
+      for (uint32_t k = 0; k < RQ; ++k) srec4[t + uint32_t(LB) * k] = v[k];
     }
     __syncthreads();
     const RowAcc<R, true> rw{&srec[t * RW], 0u};
@@ -1206,7 +1205,7 @@ __global__ __launch_bounds__(256) void tick_list_kernel(DevPlanes P, Trace T, un
       int4* grec = reinterpret_cast<int4*>(P.rec);
 #pragma unroll
       for (uint32_t k = 0; k < RQ; ++k) {
-        const uint32_t w = t + 256u * k, j = w / RQ;
+        const uint32_t w = t + uint32_t(LB) * k, j = w / RQ;
         if (sdirty[j]) grec[uint64_t(sg[j]) * RQ + (w - j * RQ)] = srec4[w];
       }
     }
@@ -1551,7 +1550,7 @@ hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, 
 
 // Resident blocks of a kernel (CUs x blocks per CU at its occupancy), per device.
 template <typename Kern>
-static unsigned resident_blocks_fast(Kern k) {
+static unsigned resident_blocks_fast(Kern k, int block = 256) {
   constexpr int MAXDEV = 64;
   static unsigned resident_of[MAXDEV] = {};
   int dev = 0;
@@ -1560,7 +1559,7 @@ static unsigned resident_blocks_fast(Kern k) {
   if (!resident) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 256, 0) == hipSuccess && cus > 0 && per > 0)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, block, 0) == hipSuccess && cus > 0 && per > 0)
       resident = unsigned(cus) * unsigned(per);
     else
       resident = 2048;
@@ -1579,10 +1578,23 @@ static void launch_two_pass_t(const DevPlanes& P, const Trace& T, unsigned long 
   }();
   hipExtLaunchKernelGGL(tick_lean_kernel<R, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, list,
                         count);
-  if (stage) {
-    const unsigned blocks =
-        unsigned(std::min<uint64_t>((P.G + 255) / 256, resident_blocks_fast(tick_list_kernel<R, false, CRC, SEM>)));
-    hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats,
+  // list blocks of four waves (default); RAFTSTEP_LIST_BLOCK=64 for one-wave
+  // blocks (no block barrier waits on another wave): the same list kernel
+  // time on C4, but the following lean kernel measured 15% slower (A/B in
+  // tools/gpu_r2_lb.sh)
+  static const int lb = [] {
+    const char* v = getenv("RAFTSTEP_LIST_BLOCK");
+    return (v && atoi(v) == 64) ? 64 : 256;
+  }();
+  if (stage && lb == 64) {
+    const unsigned blocks = unsigned(
+        std::min<uint64_t>((P.G + 63) / 64, resident_blocks_fast(tick_list_kernel<R, false, CRC, SEM, 64>, 64)));
+    hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM, 64>, dim3(blocks), dim3(64), 0, s, c, d, 0, P, T, stats,
+                          work, work_tick, work_count, list, count, next_count);
+  } else if (stage) {
+    const unsigned blocks = unsigned(
+        std::min<uint64_t>((P.G + 255) / 256, resident_blocks_fast(tick_list_kernel<R, false, CRC, SEM, 256>, 256)));
+    hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM, 256>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats,
                           work, work_tick, work_count, list, count, next_count);
   } else {
     const unsigned blocks = unsigned(

@@ -188,7 +188,8 @@ __device__ __forceinline__ void block_stats(const int (&v)[N], const int (&idx)[
   __syncthreads();
   if (threadIdx.x < N) {
     const int s = threadIdx.x;
-    const long long x = red[s][0] + red[s][1] + red[s][2] + red[s][3];
+    long long x = red[s][0];   // (blocks of 64..256 lanes)
+    for (int w = 1; w < int(blockDim.x >> 6); ++w) x += red[s][w];
     int which = 0;
 #pragma unroll
     for (int k = 0; k < N; ++k) which = (s == k) ? idx[k] : which;
