@@ -1155,9 +1155,8 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
   int32_t* const srec = reinterpret_cast<int32_t*>(srec4);
   __shared__ uint32_t sg[LB];
   __shared__ SsRec sgss[LB];
-  __shared__ int32_t shb[LB], sgsb[LB];
-  __shared__ uint16_t smeta[LB], sgrot[LB], sgrota[LB], sgrotb[LB];
-  __shared__ int32_t sgsb2[LB];
+  __shared__ int32_t shb[LB];
+  __shared__ uint16_t smeta[LB], sgrot[LB];
   __shared__ LxRec sglx[LB];
   __shared__ uint8_t sgiso[LB], sdirty[LB];
   shard_zero(next_count);
@@ -1170,19 +1169,20 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     const uint32_t g = i < n ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
     const bool valid = g < P.G;
     sg[t] = g;
-    uint16_t m0 = 0, r0 = 0, ra0 = 0, rb0 = 0;
+    // (each is a separate scattered line per group: only the words most
+    // ticks use are staged; the ring segment words, needed on rare paths —
+    // ring reads, segment switches — stay in HBM, read and written there)
+    uint16_t m0 = 0, r0 = 0;
     uint8_t gi0 = 0;
-    int32_t hb0 = 0, sb0 = 0, sb20 = 0;
+    int32_t hb0 = 0;
     SsRec ss0{0, 0, 0, 0};
     LxRec lx0{0, 0};
     if (valid) {
-      m0 = at(P.gmeta, g); r0 = at(P.grot, g); ra0 = at(P.grota, g); gi0 = at(P.giso, g);
-      hb0 = at(P.hb, g); sb0 = at(P.gsb, g); ss0 = P.gss[g];
-      rb0 = at(P.grotb, g); sb20 = at(P.gsb2, g);
+      m0 = at(P.gmeta, g); r0 = at(P.grot, g); hb0 = at(P.hb, g); ss0 = P.gss[g];
+      if (T.iso_p) gi0 = at(P.giso, g);
       if (m0 & M_LXS) lx0 = P.glx[g];
     }
-    smeta[t] = m0; sgrot[t] = r0; sgrota[t] = ra0; sgiso[t] = gi0; shb[t] = hb0; sgsb[t] = sb0; sgss[t] = ss0;
-    sgrotb[t] = rb0; sgsb2[t] = sb20; sglx[t] = lx0;
+    smeta[t] = m0; sgrot[t] = r0; sgiso[t] = gi0; shb[t] = hb0; sgss[t] = ss0; sglx[t] = lx0;
     __syncthreads();
     {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
       const int4* grec = reinterpret_cast<const int4*>(P.rec);
@@ -1197,7 +1197,9 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     }
     __syncthreads();
     const RowAcc<R, true> rw{&srec[t * RW], 0u};
-    const WordAcc<true> gw{&smeta[t], &sgrot[t], &sgrota[t], &sgiso[t], &shb[t], &sgsb[t], &sgss[t], &sgrotb[t], &sgsb2[t], &sglx[t], g};
+    const uint32_t gs = valid ? g : 0u;   // (invalid lanes never touch their words)
+    const WordAcc<true> gw{&smeta[t], &sgrot[t], &P.grota[gs], &sgiso[t], &shb[t], &P.gsb[gs], &sgss[t], &P.grotb[gs],
+                           &P.gsb2[gs], &sglx[t], g};
     const bool wrote = fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab, rw, gw);
     sdirty[t] = valid && wrote;
     __syncthreads();
@@ -1212,12 +1214,8 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     if (valid) {   // per-group words that changed
       if (smeta[t] != m0) at(P.gmeta, g) = smeta[t];
       if (sgrot[t] != r0) at(P.grot, g) = sgrot[t];
-      if (sgrota[t] != ra0) at(P.grota, g) = sgrota[t];
       if (sgiso[t] != gi0) at(P.giso, g) = sgiso[t];
       if (shb[t] != hb0) at(P.hb, g) = shb[t];
-      if (sgsb[t] != sb0) at(P.gsb, g) = sgsb[t];
-      if (sgrotb[t] != rb0) at(P.grotb, g) = sgrotb[t];
-      if (sgsb2[t] != sb20) at(P.gsb2, g) = sgsb2[t];
       const LxRec x1 = sglx[t];
       if (x1.k != lx0.k || x1.dl != lx0.dl) P.glx[g] = x1;
       const SsRec s1 = sgss[t];
