@@ -89,13 +89,14 @@ template <int R, bool LDS>
 struct RowAcc {
   int32_t* base;   // global: P.rec; LDS: the lane's record copy
   uint32_t o;      // global: g * recw (element offset); LDS: 0
+  uint32_t* dm;    // LDS: the lane's dirty-row mask (the list kernel writes back only those rows' pieces)
   __device__ __forceinline__ int32_t& at(int k, int r) const {
     if constexpr (LDS) return base[k * R + r];
     else return raftstep::at(base, o + uint32_t(k * R + r));
   }
   template <bool WT>
   __device__ __forceinline__ void st(int k, int r, int32_t v) const {
-    if constexpr (LDS) base[k * R + r] = v;
+    if constexpr (LDS) { base[k * R + r] = v; *dm |= 1u << k; }
     else raftstep::st<WT>(base, o + uint32_t(k * R + r), v);
   }
   __device__ __forceinline__ void load(int k, int (&a)[R]) const {
@@ -110,6 +111,7 @@ struct RowAcc {
     if constexpr (LDS) {
 #pragma unroll
       for (int r = 0; r < R; ++r) base[k * R + r] = a[r];
+      *dm |= 1u << k;
     } else {
       store_row_p<R>(&raftstep::at(base, o + uint32_t(k * R)), a);
     }
@@ -147,7 +149,7 @@ struct WordAcc {
 };
 template <int R>
 __device__ __forceinline__ RowAcc<R, false> rows_global(const DevPlanes& P, uint32_t g) {
-  return RowAcc<R, false>{P.rec, rix<R>(g, 0)};
+  return RowAcc<R, false>{P.rec, rix<R>(g, 0), nullptr};
 }
 __device__ __forceinline__ WordAcc<false> words_global(const DevPlanes& P, uint32_t g) {
   return WordAcc<false>{P.gmeta, P.grot, P.grota, P.giso, P.hb, P.gsb, P.gss, P.grotb, P.gsb2, P.glx, g};
@@ -1158,7 +1160,8 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
   __shared__ int32_t shb[LB];
   __shared__ uint16_t smeta[LB], sgrot[LB];
   __shared__ LxRec sglx[LB];
-  __shared__ uint8_t sgiso[LB], sdirty[LB];
+  __shared__ uint8_t sgiso[LB];
+  __shared__ uint32_t sdm[LB];   // dirty rows, then dirty 16-B pieces, of each lane's record
   shard_zero(next_count);
   const uint32_t n = shard_prefix(count, pre);
   if (blockIdx.x * uint32_t(LB) >= n) return;
@@ -1196,19 +1199,30 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       for (uint32_t k = 0; k < RQ; ++k) srec4[t + uint32_t(LB) * k] = v[k];
     }
     __syncthreads();
-    const RowAcc<R, true> rw{&srec[t * RW], 0u};
+    sdm[t] = 0u;
+    const RowAcc<R, true> rw{&srec[t * RW], 0u, &sdm[t]};
     const uint32_t gs = valid ? g : 0u;   // (invalid lanes never touch their words)
     const WordAcc<true> gw{&smeta[t], &sgrot[t], &P.grota[gs], &sgiso[t], &shb[t], &P.gsb[gs], &sgss[t], &P.grotb[gs],
                            &P.gsb2[gs], &sglx[t], g};
     const bool wrote = fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab, rw, gw);
-    sdirty[t] = valid && wrote;
+    {   // dirty rows -> the 16-B pieces of the record they touch
+      const uint32_t rows = (valid && wrote) ? sdm[t] : 0u;
+      uint32_t pm = 0;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k)
+        if ((rows >> k) & 1u) {
+          const uint32_t q0 = uint32_t(k * R) / 4u, q1 = uint32_t(k * R + R - 1) / 4u;
+          pm |= ((2u << q1) - 1u) & ~((1u << q0) - 1u);
+        }
+      sdm[t] = pm;
+    }
     __syncthreads();
     {   // coalesced write-back of the records that may have changed
       int4* grec = reinterpret_cast<int4*>(P.rec);
 #pragma unroll
       for (uint32_t k = 0; k < RQ; ++k) {
         const uint32_t w = t + uint32_t(LB) * k, j = w / RQ;
-        if (sdirty[j]) grec[uint64_t(sg[j]) * RQ + (w - j * RQ)] = srec4[w];
+        if ((sdm[j] >> (w - j * RQ)) & 1u) grec[uint64_t(sg[j]) * RQ + (w - j * RQ)] = srec4[w];
       }
     }
     if (valid) {   // per-group words that changed
