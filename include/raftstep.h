@@ -63,6 +63,7 @@ enum raft_semantics { RAFT_SEM_REF = 0, RAFT_SEM_RAFT = 1 };
 #define RAFT_ENODEV (-19)
 #define RAFT_EHIP (-1000)
 #define RAFT_ERCCL (-2000)
+#define RAFT_EINTERNAL (-3000)  /* an engine invariant failed its run-time check (a bug: report it) */
 
 /* Statistics of one or more ticks (summed over groups, and over GPUs once a
  * communicator is attached). Index names: */

@@ -115,6 +115,19 @@ struct raft_engine {
   int two_pass = 1;
   uint32_t* blist = nullptr;    // [Gp] groups the lean kernel passed on
   uint32_t lpar = 0;            // parity of the two-pass list's shard counters
+  // Steady-state list skip. After init_steady (every log empty, entries
+  // appended from there only) and no host mutation since, once a call ends
+  // with nothing deferred in its last window and an empty list at its last
+  // tick, every live group is in the compressed steady state and the lean
+  // kernel takes it; without isolation or corruption it then takes it again
+  // every tick (its conditions only need LastApplied+E < 2^31 and E < K,
+  // both checked here), so the list kernel's launch — about 5 us per tick
+  // whatever its list holds — is skipped. raft_tick re-checks at the end of
+  // every call with statistics: the list counters of a call that skipped are
+  // never zeroed, so any group passed during it would show (RAFT_EINTERNAL).
+  bool steady_origin = false;
+  bool steady_ok = false;
+  bool skipped_list = false;    // the current call skipped the list kernel
   // handler-batch staging
   void* stage = nullptr;
   size_t stage_cap = 0;
@@ -496,6 +509,7 @@ int raft_engine_info(const raft_engine* e, raft_config* cfg_out, uint64_t* devic
 
 int raft_init_new_nodes(raft_engine* e, int64_t tick0) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
+  e->steady_origin = e->steady_ok = false;
   if (int rc = check_ticks(e, tick0, 1)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   HIPCHK(launch_init_new(e->R, e->P, make_trace(e, tick0), e->stream));
@@ -505,6 +519,8 @@ int raft_init_new_nodes(raft_engine* e, int64_t tick0) {
 
 int raft_init_steady(raft_engine* e, int32_t leader, int64_t tick0) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
+  e->steady_origin = true;   // empty logs; the list skip still needs a call that proves the list empty
+  e->steady_ok = false;
   if (int rc = check_ticks(e, tick0, 1)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   HIPCHK(launch_init_steady(e->R, e->P, make_trace(e, tick0), leader, e->stream));
@@ -633,6 +649,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
 }
 
 int raft_load_state(raft_engine* e, const raft_state_view* v) {
+  if (e) e->steady_origin = e->steady_ok = false;
   if (!e || !v) return fail(RAFT_EINVAL, "null argument");
   if (!v->role || !v->voted || !v->term || !v->last || !v->commit || !v->deadline || !v->timeout ||
       !v->match || !v->fault || !v->log_term || !v->log_value)
@@ -783,6 +800,12 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     if (int rc = ensure_hist(e, nticks)) return rc;
   const Trace T0 = make_trace(e, first_tick);
   int64_t win_first = first_tick;   // first tick of the current general-kernel window
+  // steady-state list skip (see raft_engine): entries per tick at most E, so
+  // LastApplied + E stays below 2^31 while E * (last tick + 2) does
+  const bool skip_list = e->steady_ok && e->steady_origin && T0.iso_p == 0 && e->P.corrupt_p == 0 &&
+                         !e->force_general && uint64_t(e->cfg.entries_per_tick) < e->cfg.ring_depth &&
+                         double(e->cfg.entries_per_tick) * double(first_tick + int64_t(nticks) + 2) < 2.0e9;
+  e->skipped_list = skip_list;
   hipEvent_t ra = nullptr, rb = nullptr;
   if (e->prof == 2) {
     ra = next_event(e);
@@ -807,7 +830,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     if (e->two_pass && !force && !e->write_through) {
       // lean pass appends to list counter lpar, the list pass zeroes the other one
       hipEvent_t c = nullptr, d = nullptr;
-      if (e->prof == 3) {
+      if (e->prof == 3 && !skip_list) {
         c = next_event(e);
         d = next_event(e);
         if (!c || !d) return fail(RAFT_EHIP, "hipEventCreate failed");
@@ -815,7 +838,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       HIPCHK(launch_tick_two_pass(e->R, int(e->cfg.semantics), e->P, T, st, e->work, e->work_tick, cnt, e->blist,
                                   e->wcount + (2 + (e->lpar & 1)) * SHARD_WORDS,
                                   e->wcount + (2 + ((e->lpar + 1) & 1)) * SHARD_WORDS, e->stream, a, b,
-                                  c, d));
+                                  c, d, skip_list));
       ++e->lpar;
     } else {
       HIPCHK(launch_tick_fast(e->R, int(e->cfg.semantics), e->P, T, st, e->work, e->work_tick, cnt, force,
@@ -877,6 +900,25 @@ int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_sta
     HIPCHK(hipStreamSynchronize(e->stream));
     std::memset(out, 0, sizeof *out);
     for (size_t i = 0; i < h.size(); ++i) out->v[i % NSTAT] += int64_t(h[i]);
+    // steady-state list skip: both list counters (a call that skipped never
+    // zeroed them) and the last general window's worklist counter
+    if (e->two_pass && !e->write_through && e->steady_origin) {
+      uint32_t c[4 * SHARD_WORDS];
+      HIPCHK(hipMemcpyAsync(c, e->wcount, sizeof c, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
+      uint64_t listed = 0, deferred = 0;
+      const uint32_t wlast = (e->wpar + 1) & 1;   // the window the last general kernel consumed
+      for (int k = 0; k < NSHARD; ++k) {
+        listed += c[(2 * SHARD_WORDS) + k * SHARD_STRIDE] + c[(3 * SHARD_WORDS) + k * SHARD_STRIDE];
+        deferred += c[wlast * SHARD_WORDS + k * SHARD_STRIDE];
+      }
+      if (e->skipped_list && listed) {
+        e->steady_ok = false;
+        return fail(RAFT_EINTERNAL, "steady-state list skip: %llu groups were passed to a list kernel that did not run",
+                    (unsigned long long)listed);
+      }
+      e->steady_ok = listed == 0 && deferred == 0;
+    }
   }
   return RAFT_OK;
 }
@@ -902,6 +944,7 @@ int raft_sync(raft_engine* e) {
 
 int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_req* reqs, size_t n,
                               const raft_log_entry* entries, size_t n_entries_total, raft_ae_resp* out) {
+  if (e) e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &reqs[0].group, sizeof(raft_ae_req), n)) return rc;
@@ -953,6 +996,7 @@ int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_re
 
 int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_req* reqs, size_t n,
                             raft_vote_resp* out) {
+  if (e) e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &reqs[0].group, sizeof(raft_vote_req), n)) return rc;
@@ -982,6 +1026,7 @@ int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_re
 
 int raft_group_ops_batch(raft_engine* e, int64_t now_tick, const raft_group_op* ops_in, size_t n,
                          raft_op_result* out) {
+  if (e) e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (!e || (n && (!ops_in || !out))) return fail(RAFT_EINVAL, "null argument");
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &ops_in[0].group, sizeof(raft_group_op), n)) return rc;
@@ -1259,6 +1304,7 @@ int raft_checkpoint_save(raft_engine* e, const char* path) {
 }
 
 int raft_checkpoint_load(raft_engine* e, const char* path) {
+  if (e) e->steady_origin = e->steady_ok = false;
   if (!e || !path) return fail(RAFT_EINVAL, "null argument");
   const uint64_t G = e->cfg.groups, R = e->cfg.replicas, K = e->cfg.ring_depth;
   File f;

@@ -1583,13 +1583,14 @@ template <int R, bool CRC, int SEM>
 static void launch_two_pass_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                               int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
                               uint32_t* next_count, hipStream_t s, hipEvent_t a, hipEvent_t b, hipEvent_t c,
-                              hipEvent_t d) {
+                              hipEvent_t d, bool skip_list) {
   static const bool stage = [] {
     const char* v = getenv("RAFTSTEP_LIST_STAGE");
     return !v || atoi(v) != 0;
   }();
   hipExtLaunchKernelGGL(tick_lean_kernel<R, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, list,
                         count);
+  if (skip_list) return;   // the engine proved the list empty (engine.cpp, steady-state list skip)
   // list blocks of four waves (default); RAFTSTEP_LIST_BLOCK=64 for one-wave
   // blocks (no block barrier waits on another wave): the same list kernel
   // time on C4, but the following lean kernel measured 15% slower (A/B in
@@ -1618,17 +1619,17 @@ static void launch_two_pass_t(const DevPlanes& P, const Trace& T, unsigned long 
 hipError_t launch_tick_two_pass(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats,
                                 uint32_t* work, int32_t* work_tick, uint32_t* work_count, uint32_t* list,
                                 uint32_t* count, uint32_t* next_count, hipStream_t s, hipEvent_t lean_start,
-                                hipEvent_t lean_stop, hipEvent_t list_start, hipEvent_t list_stop) {
+                                hipEvent_t lean_stop, hipEvent_t list_start, hipEvent_t list_stop, bool skip_list) {
   const bool crc = P.crc_on != 0;
 #define RAFT_TWO(CRC_)                                                                                            \
   if (sem == SEM_RAFT) {                                                                                           \
     RAFT_DISPATCH_R(R, (launch_two_pass_t<RR, CRC_, SEM_RAFT>(P, T, stats, work, work_tick, work_count, list, count, \
                                                               next_count, s, lean_start, lean_stop, list_start,      \
-                                                              list_stop)))                                           \
+                                                              list_stop, skip_list)))                                           \
   } else {                                                                                                         \
     RAFT_DISPATCH_R(R, (launch_two_pass_t<RR, CRC_, SEM_REF>(P, T, stats, work, work_tick, work_count, list, count,  \
                                                              next_count, s, lean_start, lean_stop, list_start,       \
-                                                             list_stop)))                                            \
+                                                             list_stop, skip_list)))                                            \
   }
   if (crc) { RAFT_TWO(true); } else { RAFT_TWO(false); }
 #undef RAFT_TWO

@@ -50,7 +50,7 @@ hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, 
 hipError_t launch_tick_two_pass(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats,
                                 uint32_t* work, int32_t* work_tick, uint32_t* work_count, uint32_t* list,
                                 uint32_t* count, uint32_t* next_count, hipStream_t s, hipEvent_t lean_start,
-                                hipEvent_t lean_stop, hipEvent_t list_start, hipEvent_t list_stop);
+                                hipEvent_t lean_stop, hipEvent_t list_start, hipEvent_t list_stop, bool skip_list);
 // General kernel: catches every worklisted group up to last_tick; zeroes
 // `next_count`. lane_per_group: the one-lane-per-group form (tick_slow_kernel)
 // instead of the replica-parallel one (tick_seg_kernel).

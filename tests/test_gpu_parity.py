@@ -221,3 +221,29 @@ def test_handler_batches_on_compressed_steady_groups(sem):
         se, so = e.tick(8 + 2 * rnd, 1), o.tick(8 + 2 * rnd, 1)
         assert list(se) == list(so), f"round {rnd}: tick stats differ"
         compare(e, o, f"round {rnd} tick")
+
+
+@pytest.mark.parametrize("sem", [abi.SEM_REF, abi.SEM_RAFT])
+def test_steady_state_list_skip(sem):
+    """The engine's steady-state list skip (engine.cpp): after init_steady a
+    call with statistics proves the list empty, the following calls run the
+    lean kernel alone; a host mutation (here load_state of a state where one
+    follower's CommitIndex lags, so the group is not compressed) must bring
+    the list kernel back. Every step against the oracle, the whole state."""
+    kw = dict(replicas=5, groups=3000, ring_depth=16, client_period=1, seed=0x5EED0002, semantics=sem)
+    e, o = pair(**kw)
+    e.init_steady(0, 0)
+    o.init_steady(0, 0)
+    t = 1
+    for k in (6, 10, 13):   # establishes the skip, then skipped calls (and a ring wrap at K=16)
+        assert list(e.tick(t, k)) == list(o.tick(t, k)), f"stats at {t}"
+        compare(e, o, f"after tick {t + k - 1}")
+        t += k
+    st = o.store_state()
+    st["commit"][7, 2] -= 1   # group 7, follower 2: one entry behind on CommitIndex
+    e.load_state(st)
+    o.load_state(st)
+    for k in (1, 5, 8):
+        assert list(e.tick(t, k)) == list(o.tick(t, k)), f"stats at {t} after the mutation"
+        compare(e, o, f"after tick {t + k - 1} (mutated)")
+        t += k
