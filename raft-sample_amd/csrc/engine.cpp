@@ -853,9 +853,13 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         for (int k = 0; k < NSHARD; ++k) nw += sh[k * SHARD_STRIDE];
         fprintf(stderr, "raftstep: general kernel ticks %lld..%lld worklist %u\n", (long long)win_first, (long long)t, nw);
       }
-      HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t, stats ? e->hist : nullptr,
-                              e->work, e->work_tick, cnt, e->wcount + ((e->wpar + 1) & 1) * SHARD_WORDS, e->lane_general,
-                              e->stream));
+      // (with the list skipped nothing can be deferred — only the list kernel
+      // defers — so both worklist counters stay zero and the general kernel
+      // has nothing to do)
+      if (!skip_list)
+        HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t,
+                                stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
+                                e->wcount + ((e->wpar + 1) & 1) * SHARD_WORDS, e->lane_general, e->stream));
       ++e->wpar;
       if (stats)
         if (int rc = flush_window_stats(e, uint32_t(win_first - first_tick), i)) return rc;
