@@ -806,6 +806,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
                          !e->force_general && uint64_t(e->cfg.entries_per_tick) < e->cfg.ring_depth &&
                          double(e->cfg.entries_per_tick) * double(first_tick + int64_t(nticks) + 2) < 2.0e9;
   e->skipped_list = skip_list;
+  uint32_t stats_first = 0;   // first tick (index in this call) whose records are not reduced yet
   hipEvent_t ra = nullptr, rb = nullptr;
   if (e->prof == 2) {
     ra = next_event(e);
@@ -861,8 +862,12 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
                                 stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
                                 e->wcount + ((e->wpar + 1) & 1) * SHARD_WORDS, e->lane_general, e->stream));
       ++e->wpar;
-      if (stats)
-        if (int rc = flush_window_stats(e, uint32_t(win_first - first_tick), i)) return rc;
+      // per-tick records: reduced (and all-reduced) per window; with the list
+      // skipped on one GPU nothing overlaps them, so one reduce at the end of
+      // the call covers every tick
+      if (stats && (!skip_list || e->comm || i + 1 == nticks))
+        if (int rc = flush_window_stats(e, stats_first, i)) return rc;
+      if (!skip_list || e->comm || i + 1 == nticks) stats_first = i + 1;
       win_first = t + 1;
     }
   }
