@@ -1340,7 +1340,15 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
           committed = cl2 - s.cl;
           w_term = s.term;
           w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
-          wmask = 1u << c;
+          // The whole row, not only the leader's column, when every
+          // follower's slot there is dead: with KP = 2K slots, all of a
+          // follower's live entries (L-K, L] in the current segment (gsb at
+          // most L-K+1, no segment gap) and the lead k+n at most K, the slot
+          // of leader index L+k+e last held follower index L+k+e-2K <= L-K;
+          // the follower rewrites it before its log reaches it. No partial
+          // lines then; otherwise the leader's column alone.
+          const bool whole = P.KP >= 2u * P.K && x.k + n <= int(P.K) && at(P.gsb, g) <= L - int(P.K) + 1;
+          wmask = whole ? (1u << R) - 1u : (1u << c);
           df |= 131072u | 256u;
         } else {
           pass = true;
