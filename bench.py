@@ -236,6 +236,10 @@ def main():
     # timed regions: exactly K fused ticks each (+ the per-tick stats, reduced
     # on the device and, at N>1, all-reduced by RCCL on the engine's side stream)
     times, stats = [], np.zeros(len(STAT_NAMES), np.int64)
+    # groups frozen by a fault before each tick (REF prefix: a frozen group does
+    # no work, so C4REF's value counts only the live group-steps)
+    frozen = int(untimed[STAT_NAMES.index("faults")])
+    live_steps = []
     eng.profile(2)   # one HIP event pair on the engine stream around each timed call
     for _ in range(max(1, args.repeats)):
         barrier()
@@ -243,6 +247,11 @@ def main():
         s = eng.tick(tick, args.steps, stats=True)
         barrier()
         el = time.perf_counter() - t0
+        if wl.get("allow_faults"):   # (outside the timed region) per-tick fault counts of this rank
+            f = eng.tick_records(args.steps)[:, STAT_NAMES.index("faults")]
+            before = frozen + np.concatenate([[0], np.cumsum(f)[:-1]])
+            live_steps.append(int(G * args.steps - before.sum()))
+            frozen += int(f.sum())
         if dist is not None:
             from raftstep import dist as rdist
             el = rdist.max_over_ranks(dist, el, device=None if same_dev else "cuda")
@@ -269,6 +278,15 @@ def main():
     reps = len(times)
     total_steps = G * world * args.steps
     value = total_steps / elapsed
+    live_value = None
+    if wl.get("allow_faults"):   # C4REF: only the group-steps of groups not frozen by a fault count
+        mid = sorted(range(reps), key=lambda i: times[i])[reps // 2]
+        live = live_steps[mid]
+        if dist is not None:
+            from raftstep import dist as rdist
+            live = int(sum(rdist.sum_over_ranks(dist, [live])))
+        live_value = live / times[mid]
+        value = live_value
     # correctness guard on the timed runs: the steady state commits exactly one
     # entry per group per tick and never faults; under churn nothing faults
     # and most groups have a leader (REF prefix: faults are the point)
@@ -279,6 +297,12 @@ def main():
             (wl.get("allow_faults") or stats[STAT_NAMES.index("leader_groups")] > 0.5 * G * world * args.steps * reps)
     else:
         ok = stats[STAT_NAMES.index("committed")] == expect_commit and faults == 0
+    if world > 1 and not same_dev:
+        # the engine communicator must span every rank, and every window's
+        # stats must have gone through it (ncclAllReduce on the side stream)
+        if nranks != world:
+            raise SystemExit(f"bench: RCCL communicator has {nranks} ranks, WORLD_SIZE is {world}")
+        ok = ok and allreduces > 0
 
     B_survey = algorithmic_bytes(R, E, crc)
     # the dominant kernel's algorithmic bytes in its own layout: the lean
@@ -287,7 +311,10 @@ def main():
     B = lean_bytes(R, E, crc, segmented="iso" in wl and wl["iso"][0] > 0) if two_pass else B_survey
     avg_kernel_s = kernel_ms / 1e3 / max(kernel_launches, 1)    # steady-state kernel, kernel-exact
     avg_region_s = region_ms / 1e3 / max(region_launches, 1)    # all launches of a tick + gaps
-    achieved = B * G / avg_kernel_s / 1e9
+    # C4REF: the lean kernel's algorithmic bytes are those of the live groups it
+    # takes (a frozen group is read as 2 B of gmeta and skipped)
+    units = G if live_value is None else live_value * elapsed / world / args.steps
+    achieved = B * units / avg_kernel_s / 1e9
     workload = f"{wl_key}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}, K={K}"
     traffic, traffic_src = load_pmc(workload, "tick_lean_kernel" if two_pass else "tick_fast_kernel")
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -298,12 +325,12 @@ def main():
             "bytes_accounting": ("tick_lean_kernel, compressed steady state (bench.py lean_bytes), every group "
                                  "counted as taken by the lean pass" if two_pass else
                                  "SURVEY.md §8(d) B(R,E), per-replica SoA"),
-            "units_per_launch": G,
+            "units_per_launch": units,
             "kernel": "tick_lean_kernel" if two_pass else "tick_fast_kernel",
             "avg_kernel_us": avg_kernel_s * 1e6, "kernel_launches": kernel_launches,
             "list_kernel_us": (list_ms * 1e3 / max(list_launches, 1)) if two_pass else None,
             "avg_region_us_per_tick": avg_region_s * 1e6,
-            "achieved_region": B * G / avg_region_s / 1e9,
+            "achieved_region": B * units / avg_region_s / 1e9,
             # SURVEY §8(d)'s per-replica SoA figure at the measured tick rate:
             # the bandwidth an uncompressed SoA engine would need for this
             # throughput (above the HBM peak = beyond any per-replica layout)
@@ -337,7 +364,10 @@ def main():
         fi = STAT_NAMES.index("faults")
         result["faults_prefix"] = {"groups": G * world, "faulted_before_timed": int(untimed[fi]),
                                    "faulted_in_timed": int(stats[fi]),
-                                   "frozen_fraction": (int(untimed[fi]) + int(stats[fi])) / (G * world)}
+                                   "frozen_fraction": (int(untimed[fi]) + int(stats[fi])) / (G * world),
+                                   "value_counts": "live (not frozen) group-steps only",
+                                   "live_group_steps_median_repeat": int(round(live_value * elapsed)),
+                                   "all_group_steps_per_s": total_steps / elapsed}
     if world > 1:
         from raftstep import dist as rdist
         ranks = [None] * world

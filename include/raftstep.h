@@ -155,6 +155,12 @@ int raft_init_steady(raft_engine* e, int32_t leader, int64_t tick0);
 
 int raft_load_state(raft_engine* e, const raft_state_view* v);
 int raft_store_state(raft_engine* e, raft_state_view* v);
+/* The canonical view of groups [first_group, first_group + n_groups) only,
+ * indexed by the local group (g - first_group) with the same per-group shapes
+ * as raft_store_state; copies out only that slice of the device state, so a
+ * slice of a multi-million-group engine can be compared with a CPU run of the
+ * same groups (RAFT_ERANGE when the range leaves the engine). */
+int raft_store_state_range(raft_engine* e, uint64_t first_group, uint64_t n_groups, raft_state_view* v);
 
 /* ---- audit: digests, nodelog, checkpoints ---------------------------------
  * raft_state_digest: per-group 64-bit digest of the canonical view that
@@ -295,6 +301,58 @@ int raft_comm_info(raft_engine* e, int32_t* nranks, int32_t* rank, uint64_t* all
  * and the number of tick launches covered. */
 int raft_profile_enable(raft_engine* e, int mode);
 int raft_profile_read(raft_engine* e, double* total_ms, uint64_t* launches);
+
+/* ---- diagnostics: tick-class coverage ------------------------------------
+ * raft_diag_enable(e, 1) zeroes and starts the device lane-class counters:
+ * for every tick, the lanes (groups) of the steady-state (lean) kernel and of
+ * the full fast-path body (the list kernel, or the one-pass kernel) that took
+ * each class of tick. raft_diag_read copies out n <= RAFT_DIAG_COUNTERS
+ * counters (indices below) and zeroes them. Counting costs one ballot and
+ * atomic per wave and class; off by default. */
+#define RAFT_DIAG_DEVICE_COUNTERS 64u
+#define RAFT_DIAG_COUNTERS 72u
+enum raft_diag_counter {
+  /* lean kernel (first pass of the two-pass tick) */
+  RAFT_DIAG_LEAN_LANES = 10,          /* groups looked at */
+  RAFT_DIAG_LEAN_SKIPPED = 0,         /* deferred to the general kernel or frozen by a fault */
+  RAFT_DIAG_LEAN_SSYNC = 18,          /* compressed steady ticks taken */
+  RAFT_DIAG_LEAN_LXS = 19,            /* cut-off leader appending alone (LXS) taken */
+  RAFT_DIAG_LEAN_THREE_SEG = 20,      /* ring segment switch while the previous segment stays live */
+  RAFT_DIAG_LEAN_LXS_WHOLE_ROW = 21,  /* LXS ticks written as whole ring rows */
+  RAFT_DIAG_LEAN_HWX = 22,            /* steady ticks of a group with a truncated log in step (HWX) */
+  RAFT_DIAG_LEAN_PASSED = 23,         /* groups passed on to the list kernel */
+  RAFT_DIAG_LEAN_FORCED = 24,         /* groups passed by raft_debug_force_pass */
+  RAFT_DIAG_LEAN_SWITCH = 5,          /* ring segment switches */
+  /* full fast-path body (list kernel / one-pass kernel): 32 + bit */
+  RAFT_DIAG_LIST_LANES = 42,          /* groups looked at */
+  RAFT_DIAG_LIST_DEFERRED = 33,       /* deferred to the general kernel this tick */
+  RAFT_DIAG_LIST_ISOLATION = 34,      /* an isolation window over the group */
+  RAFT_DIAG_LIST_SWITCH = 37,         /* ring segment switches */
+  RAFT_DIAG_LIST_QUIET = 48,          /* quiet leaderless ticks */
+  RAFT_DIAG_LIST_ISOLATED_LEADER = 49,/* cut-off leader appending alone */
+  RAFT_DIAG_LIST_SSYNC = 50,          /* ticks ending in the compressed steady state */
+  RAFT_DIAG_LIST_ELECTION = 51,       /* a follower's election while the leader is cut off */
+  RAFT_DIAG_LIST_FIRST_ROUND = 52,    /* a new leader's first round (fresh rows) */
+  RAFT_DIAG_LIST_RETURN = 53,         /* the stale leader's return (step-down + catch-up) */
+  RAFT_DIAG_LIST_RETURN_TRUNC = 54,   /* ... with its log truncated */
+  RAFT_DIAG_LIST_STALE = 55,          /* new leader replicating while the stale one is cut off */
+  RAFT_DIAG_LIST_HWX = 56,            /* truncated logs in step */
+  RAFT_DIAG_LIST_THREE_SEG = 57,      /* ring segment switch while the previous segment stays live */
+  RAFT_DIAG_LIST_ISOLATED_REPLICA = 58,/* one isolated follower / candidate */
+  RAFT_DIAG_LIST_TIMER_FIRE = 59,     /* the isolated replica's election timer fired */
+  RAFT_DIAG_LIST_WINDOW_START = 60,   /* a leader-isolation window decided on the fast path */
+  /* host counters since the last read */
+  RAFT_DIAG_TICKS = 64,
+  RAFT_DIAG_TICKS_LIST_SKIPPED = 65,  /* ticks run by the lean kernel alone (steady-state list skip) */
+  RAFT_DIAG_GENERAL_LAUNCHES = 66
+};
+int raft_diag_enable(raft_engine* e, int on);
+int raft_diag_read(raft_engine* e, uint64_t* counters, uint32_t n);
+/* Test knob: the lean kernel passes `group` (< 0: none) to the list kernel at
+ * every tick instead of taking it. Results are unchanged while the list kernel
+ * runs; in a list-skipping call the group's tick is lost, which the engine
+ * detects (RAFT_EINTERNAL, engine poisoned until its state is replaced). */
+int raft_debug_force_pass(raft_engine* e, int64_t group);
 
 #ifdef __cplusplus
 }

@@ -97,8 +97,10 @@ struct raft_engine {
   // zero between calls by the reduce kernel) and the reduced per-tick records
   // [cap][NSTAT] (the 64 B per tick that RCCL sums across GPUs)
   unsigned long long* hist = nullptr;
-  unsigned long long* tstat = nullptr;
+  unsigned long long* tstat = nullptr;   // [hist_cap + 2][NSTAT]: per-tick records, then two check records
+  unsigned long long* hrb = nullptr;     // pinned host copy of tstat (one async readback per call)
   uint32_t hist_cap = 0;
+  uint32_t last_stats_n = 0;             // nticks of the last raft_tick call with statistics (0: none yet)
   unsigned long long* cstat = nullptr;   // raft_comm_allreduce_stats staging
   uint32_t wpar = 0;            // parity of the next worklist window (its counter was zeroed by the last general kernel)
   // worklist of groups the steady-state kernel hands to the general kernel
@@ -128,6 +130,20 @@ struct raft_engine {
   bool steady_origin = false;
   bool steady_ok = false;
   bool skipped_list = false;    // the current call skipped the list kernel
+  // A skipping call without statistics ends with the check record written to
+  // tstat[hist_cap + 1] and copied to the pinned buffer (event chk_ev); the
+  // next call on the engine waits for it and verifies that nothing was passed
+  // to the list kernel that did not run. If something was, ticks were lost:
+  // the engine is poisoned (every call fails with RAFT_EINTERNAL) until its
+  // state is replaced (init_*, load_state, checkpoint load).
+  bool pend_chk = false;
+  hipEvent_t chk_ev = nullptr;
+  bool poisoned = false;
+  std::string poison_msg;
+  // diagnostics: lane class counters on the device (raft_diag_enable), host counters
+  int diag_print = 0;
+  unsigned long long* dbg_buf = nullptr;   // the device counters (P.dbg while counting)           // RAFTSTEP_DEBUG_FAST: print the class counters after every call (synchronising)
+  uint64_t n_ticks = 0, n_skip_ticks = 0, n_general = 0;
   // handler-batch staging
   void* stage = nullptr;
   size_t stage_cap = 0;
@@ -205,15 +221,52 @@ int ensure_hist(raft_engine* e, uint32_t n) {
   if (e->comm_stream) HIPCHK(hipStreamSynchronize(e->comm_stream));
   if (e->hist) HIPCHK(hipFree(e->hist));
   if (e->tstat) HIPCHK(hipFree(e->tstat));
-  e->hist = e->tstat = nullptr;
+  if (e->hrb) HIPCHK(hipHostFree(e->hrb));
+  e->hist = e->tstat = e->hrb = nullptr;
   e->hist_cap = 0;
+  e->last_stats_n = 0;
   uint32_t cap = std::max<uint32_t>(n, 64);
   const size_t hb = size_t(cap) * STAT_SLOTS * NSTAT * 8;
+  const size_t tb = size_t(cap + 2) * NSTAT * 8;   // + the two check records (raft_engine::tstat)
   HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->hist), hb));
-  HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->tstat), size_t(cap) * NSTAT * 8));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->tstat), tb));
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&e->hrb), tb, hipHostMallocDefault));
   HIPCHK(hipMemsetAsync(e->hist, 0, hb, e->stream));   // once; the reduce kernel re-zeroes what it reads
+  HIPCHK(hipMemsetAsync(e->tstat, 0, tb, e->stream));
   e->hist_cap = cap;
   return RAFT_OK;
+}
+
+// The check of the last list-skipping call without statistics (see
+// raft_engine::pend_chk): waits for its record and poisons the engine if the
+// lean kernel passed any group on while the list kernel was skipped.
+int settle_check(raft_engine* e) {
+  if (e->pend_chk) {
+    e->pend_chk = false;
+    HIPCHK(hipEventSynchronize(e->chk_ev));
+    const unsigned long long* c = e->hrb + size_t(e->hist_cap + 1) * NSTAT;
+    if (c[CHK_MAGIC] != 0x5241465443484Bull) {
+      e->poisoned = true;
+      e->poison_msg = "steady-state list skip: the end-of-call check record was not written";
+    } else if (c[CHK_LISTED]) {
+      e->poisoned = true;
+      e->poison_msg = "steady-state list skip: " + std::to_string(c[CHK_LISTED]) +
+                      " groups were passed to a list kernel that did not run (ticks lost)";
+    }
+    if (e->poisoned) e->steady_ok = false;
+  }
+  if (e->poisoned)
+    return fail(RAFT_EINTERNAL, "%s; the engine state is invalid until init_*, load_state or a checkpoint load",
+                e->poison_msg.c_str());
+  return RAFT_OK;
+}
+
+// State replaced: the list-skip proof and any poison go
+void state_replaced(raft_engine* e) {
+  e->steady_origin = e->steady_ok = false;
+  e->pend_chk = false;
+  e->poisoned = false;
+  e->poison_msg.clear();
 }
 
 hipEvent_t next_event(raft_engine* e) {
@@ -440,9 +493,12 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
   if (const char* dl = getenv("RAFTSTEP_DIAG_LEAN")) e->P.diag = uint32_t(atoi(dl));
+  e->P.dbg_pass = 0xFFFFFFFFu;
   if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
-    if (rc == RAFT_OK) rc = dev_alloc(e, reinterpret_cast<void**>(&e->P.dbg), 32 * 8);
-    if (rc == RAFT_OK && hipMemset(e->P.dbg, 0, 32 * 8) != hipSuccess) rc = fail(RAFT_EHIP, "hipMemset failed");
+    e->diag_print = 1;
+    if (rc == RAFT_OK) rc = dev_alloc(e, reinterpret_cast<void**>(&e->P.dbg), RAFT_DIAG_DEVICE_COUNTERS * 8);
+    if (rc == RAFT_OK && hipMemset(e->P.dbg, 0, RAFT_DIAG_DEVICE_COUNTERS * 8) != hipSuccess)
+      rc = fail(RAFT_EHIP, "hipMemset failed");
     if (rc != RAFT_OK) {
       std::string keep = g_err;
       raft_engine_destroy(e);
@@ -493,6 +549,8 @@ int raft_engine_destroy(raft_engine* e) {
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->hist) (void)hipFree(e->hist);
   if (e->tstat) (void)hipFree(e->tstat);
+  if (e->hrb) (void)hipHostFree(e->hrb);
+  if (e->chk_ev) (void)hipEventDestroy(e->chk_ev);
   if (e->cstat) (void)hipFree(e->cstat);
   if (e->stage) (void)hipFree(e->stage);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -509,7 +567,7 @@ int raft_engine_info(const raft_engine* e, raft_config* cfg_out, uint64_t* devic
 
 int raft_init_new_nodes(raft_engine* e, int64_t tick0) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
-  e->steady_origin = e->steady_ok = false;
+  state_replaced(e);
   if (int rc = check_ticks(e, tick0, 1)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   HIPCHK(launch_init_new(e->R, e->P, make_trace(e, tick0), e->stream));
@@ -519,8 +577,8 @@ int raft_init_new_nodes(raft_engine* e, int64_t tick0) {
 
 int raft_init_steady(raft_engine* e, int32_t leader, int64_t tick0) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
+  state_replaced(e);
   e->steady_origin = true;   // empty logs; the list skip still needs a call that proves the list empty
-  e->steady_ok = false;
   if (int rc = check_ticks(e, tick0, 1)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   HIPCHK(launch_init_steady(e->R, e->P, make_trace(e, tick0), leader, e->stream));
@@ -528,10 +586,16 @@ int raft_init_steady(raft_engine* e, int32_t leader, int64_t tick0) {
   return RAFT_OK;
 }
 
-int raft_store_state(raft_engine* e, raft_state_view* v) {
-  if (!e || !v) return fail(RAFT_EINVAL, "null argument");
+}  // extern "C"
+
+namespace {
+
+// Canonical view of groups [g0, g0+n): only that slice of every plane (and
+// the ring tiles holding it) is copied out; the view is indexed by the
+// local group g - g0.
+int store_range(raft_engine* e, uint64_t g0, uint64_t n, raft_state_view* v) {
   HIPCHK(hipSetDevice(e->cfg.device));
-  const uint64_t R = e->cfg.replicas, G = e->cfg.groups, Gp = e->Gp, K = e->cfg.ring_depth;
+  const uint64_t R = e->cfg.replicas, Gp = e->Gp, K = e->cfg.ring_depth;
   const bool raft = e->cfg.semantics == RAFT_SEM_RAFT;
   std::vector<int32_t> term, last, commit, ts, hb, lm, xm, lt, ln, xn, hw, rs, blk;
   std::vector<uint16_t> meta, rot, rota, rotb;
@@ -539,43 +603,52 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   std::vector<int32_t> sb, sb2;
   std::vector<int64_t> lv;
   std::vector<uint32_t> lcrc;
+  const uint64_t W = recw_of(uint32_t(R));
   int rc = RAFT_OK;
-  if (!rc) rc = d2h(e, blk, e->P.rec, Gp * recw_of(R));   // group records (rows extracted below)
-  if (!rc) rc = d2h(e, hb, e->P.hb, Gp);
-  if (!rc) rc = d2h(e, xm, e->P.xmatch, R * R * Gp);
-  if (!rc) rc = d2h(e, meta, e->P.gmeta, Gp);
-  if (!rc && v->iso_victim) rc = d2h(e, giso, e->P.giso, Gp);
-  if (!rc && raft) rc = d2h(e, xn, e->P.xnext, R * R * Gp);
+  if (!rc) rc = d2h(e, blk, e->P.rec + g0 * W, n * W);   // group records (rows extracted below)
+  if (!rc) rc = d2h(e, hb, e->P.hb + g0, n);
+  // [R][R][Gp] rows of further leaders: R*R strided slices
+  auto rows2d = [&](std::vector<int32_t>& h, const int32_t* d) -> int {
+    h.resize(R * R * n);
+    HIPCHK(hipMemcpy2DAsync(h.data(), n * 4, d + g0, Gp * 4, n * 4, R * R, hipMemcpyDeviceToHost, e->stream));
+    return RAFT_OK;
+  };
+  if (!rc) rc = rows2d(xm, e->P.xmatch);
+  if (!rc) rc = d2h(e, meta, e->P.gmeta + g0, n);
+  if (!rc && v->iso_victim) rc = d2h(e, giso, e->P.giso + g0, n);
+  if (!rc && raft) rc = rows2d(xn, e->P.xnext);
   const bool logs = v->log_term || v->log_value || v->log_crc;
   std::vector<int32_t> ltm;
   const uint64_t KP = e->KP;
-  if (!rc && logs) rc = d2h(e, rot, e->P.grot, Gp);
-  if (!rc && logs) rc = d2h(e, rota, e->P.grota, Gp);
-  if (!rc && logs) rc = d2h(e, sb, e->P.gsb, Gp);
-  if (!rc && logs) rc = d2h(e, rotb, e->P.grotb, Gp);
-  if (!rc && logs) rc = d2h(e, sb2, e->P.gsb2, Gp);
+  const uint64_t t0 = g0 >> 6, nt = ((g0 + n - 1) >> 6) - t0 + 1;   // ring tiles [t0, t0+nt)
+  const uint64_t tile = KP * 64 * R;
+  if (!rc && logs) rc = d2h(e, rot, e->P.grot + g0, n);
+  if (!rc && logs) rc = d2h(e, rota, e->P.grota + g0, n);
+  if (!rc && logs) rc = d2h(e, sb, e->P.gsb + g0, n);
+  if (!rc && logs) rc = d2h(e, rotb, e->P.grotb + g0, n);
+  if (!rc && logs) rc = d2h(e, sb2, e->P.gsb2 + g0, n);
   std::vector<SsRec> gss;
-  if (!rc) rc = d2h(e, gss, e->P.gss, Gp);
+  if (!rc) rc = d2h(e, gss, e->P.gss + g0, n);
   std::vector<LxRec> glx;
-  if (!rc) rc = d2h(e, glx, e->P.glx, Gp);
-  if (!rc && logs) rc = d2h(e, lt, e->P.log_term, R * KP * Gp);
-  if (!rc && logs) rc = d2h(e, lv, e->P.log_value, R * KP * Gp);
+  if (!rc) rc = d2h(e, glx, e->P.glx + g0, n);
+  if (!rc && logs) rc = d2h(e, lt, e->P.log_term + t0 * tile, nt * tile);
+  if (!rc && logs) rc = d2h(e, lv, e->P.log_value + t0 * tile, nt * tile);
   const bool crcs = v->log_crc && e->cfg.payload_crc;
-  if (!rc && crcs) rc = d2h(e, lcrc, e->P.log_crc, R * KP * Gp);
+  if (!rc && crcs) rc = d2h(e, lcrc, e->P.log_crc + t0 * tile, nt * tile);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(e->stream));
-  rec_rows(blk, PL_TERM, R, Gp, term);
-  rec_rows(blk, PL_LAST, R, Gp, last);
-  rec_rows(blk, PL_COMMIT, R, Gp, commit);
-  rec_rows(blk, PL_TSTART, R, Gp, ts);
-  rec_rows(blk, PL_RS, R, Gp, rs);
-  rec_rows(blk, PL_LMATCH, R, Gp, lm);
-  if (raft) rec_rows(blk, PL_LNEXT, R, Gp, ln);
-  if (raft) rec_rows(blk, PL_HWM, R, Gp, hw);
-  if (logs) rec_rows(blk, PL_LTERM, R, Gp, ltm);
+  rec_rows(blk, PL_TERM, R, n, term);
+  rec_rows(blk, PL_LAST, R, n, last);
+  rec_rows(blk, PL_COMMIT, R, n, commit);
+  rec_rows(blk, PL_TSTART, R, n, ts);
+  rec_rows(blk, PL_RS, R, n, rs);
+  rec_rows(blk, PL_LMATCH, R, n, lm);
+  if (raft) rec_rows(blk, PL_LNEXT, R, n, ln);
+  if (raft) rec_rows(blk, PL_HWM, R, n, hw);
+  if (logs) rec_rows(blk, PL_LTERM, R, n, ltm);
   std::vector<int32_t>().swap(blk);
   // SSYNC groups: the planes are stale, the gss record is the state
-  for (uint64_t g = 0; g < G; ++g) {
+  for (uint64_t g = 0; g < n; ++g) {
     const int pr = meta[g] & 0xF;
     if (!(meta[g] & M_SSYNC) || pr >= int(R)) continue;
     for (uint64_t r = 0; r < R; ++r) {
@@ -585,9 +658,10 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
       if (!ltm.empty()) ltm[g * R + r] = gss[g].term;
     }
   }
-  for (uint64_t g = 0; g < G; ++g) {
+  for (uint64_t g = 0; g < n; ++g) {
     const int primary = meta[g] & 0xF;
     const bool msync = meta[g] & M_MSYNC;
+    const uint64_t gt = g0 + g - t0 * 64;   // group index inside the copied ring tiles
     if (v->fault) v->fault[g] = uint8_t((meta[g] >> 4) & 0xF);
     if (v->iso_victim) v->iso_victim[g] = giso[g];
     for (uint64_t r = 0; r < R; ++r) {
@@ -609,15 +683,15 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
         for (uint64_t p = 0; p < R; ++p) {
           int32_t m = 0;
           if (role == ROLE_L && p != r)
-            m = (int(r) == primary) ? (msync ? last[g * R + p] : lm[g * R + p]) : xm[(r * R + p) * Gp + g];
+            m = (int(r) == primary) ? (msync ? last[g * R + p] : lm[g * R + p]) : xm[(r * R + p) * n + g];
           v->match[c * R + p] = m;
         }
       if (v->next)
         for (uint64_t p = 0; p < R; ++p) {
           int32_t nx = 0;
           if (role == ROLE_L && p != r) {
-            if (raft) nx = (int(r) == primary) ? (msync ? last[g * R + p] + 1 : ln[g * R + p]) : xn[(r * R + p) * Gp + g];
-            else nx = ((int(r) == primary) ? (msync ? last[g * R + p] : lm[g * R + p]) : xm[(r * R + p) * Gp + g]) + 1;
+            if (raft) nx = (int(r) == primary) ? (msync ? last[g * R + p] + 1 : ln[g * R + p]) : xn[(r * R + p) * n + g];
+            else nx = ((int(r) == primary) ? (msync ? last[g * R + p] : lm[g * R + p]) : xm[(r * R + p) * n + g]) + 1;
           }
           v->next[c * R + p] = nx;
         }
@@ -626,10 +700,10 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
         return uint64_t((idx - 1 + (idx >= sb[g] ? rot[g] : (idx >= sb2[g] ? rota[g] : rotb[g]))) & int64_t(KP - 1));
       };
       if (logs && last[d] > 0) {
-        const int32_t want = lt[ring_index(r, g, pslot(last[d]), KP, R)];
+        const int32_t want = lt[ring_index(r, gt, pslot(last[d]), KP, R)];
         if (ltm[d] != want)
-          return fail(RAFT_EINVAL, "internal: last-entry term cache of group %llu replica %llu is %d, ring says %d",
-                      (unsigned long long)g, (unsigned long long)r, ltm[d], want);
+          return fail(RAFT_EINTERNAL, "last-entry term cache of group %llu replica %llu is %d, ring says %d",
+                      (unsigned long long)(g0 + g), (unsigned long long)r, ltm[d], want);
       }
       if (logs) {
         const int64_t l = last[d];
@@ -637,7 +711,7 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
           // slot s holds the largest index i <= l with (i-1) mod K == s
           int64_t idx = l >= 1 ? l - ((l - 1 - int64_t(s)) & int64_t(K - 1)) : 0;
           const bool live = idx >= 1 && idx <= l && idx > int64_t(hwm) - int64_t(K);
-          const uint64_t o = live ? ring_index(r, g, pslot(idx), KP, R) : 0;
+          const uint64_t o = live ? ring_index(r, gt, pslot(idx), KP, R) : 0;
           if (v->log_term) v->log_term[c * K + s] = live ? lt[o] : 0;
           if (v->log_value) v->log_value[c * K + s] = live ? lv[o] : 0;
           if (v->log_crc) v->log_crc[c * K + s] = (live && crcs) ? lcrc[o] : 0u;
@@ -648,8 +722,27 @@ int raft_store_state(raft_engine* e, raft_state_view* v) {
   return RAFT_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int raft_store_state(raft_engine* e, raft_state_view* v) {
+  if (!e || !v) return fail(RAFT_EINVAL, "null argument");
+  if (int rc = settle_check(e)) return rc;
+  return store_range(e, 0, e->cfg.groups, v);
+}
+
+int raft_store_state_range(raft_engine* e, uint64_t first_group, uint64_t n_groups, raft_state_view* v) {
+  if (!e || !v) return fail(RAFT_EINVAL, "null argument");
+  if (n_groups == 0 || first_group >= e->cfg.groups || n_groups > e->cfg.groups - first_group)
+    return fail(RAFT_ERANGE, "groups [%llu, +%llu) outside the engine's %llu", (unsigned long long)first_group,
+                (unsigned long long)n_groups, (unsigned long long)e->cfg.groups);
+  if (int rc = settle_check(e)) return rc;
+  return store_range(e, first_group, n_groups, v);
+}
+
 int raft_load_state(raft_engine* e, const raft_state_view* v) {
-  if (e) e->steady_origin = e->steady_ok = false;
+  if (e) state_replaced(e);
   if (!e || !v) return fail(RAFT_EINVAL, "null argument");
   if (!v->role || !v->voted || !v->term || !v->last || !v->commit || !v->deadline || !v->timeout ||
       !v->match || !v->fault || !v->log_term || !v->log_value)
@@ -775,10 +868,12 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
 // Stats of the window [w0, w1] (indices into this call's ticks) are final
 // once its general kernel has run: reduce them to per-tick records and, with
 // a communicator, sum those across GPUs on the comm stream (ordered by an
-// event, overlapping the following ticks on the engine stream).
-static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1) {
+// event, overlapping the following ticks on the engine stream). The call's
+// last flush also writes the end-of-call check record (chk).
+static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1, const CallCheck* chk) {
   const uint32_t n = w1 - w0 + 1;
-  HIPCHK(launch_stats_reduce(e->hist + size_t(w0) * STAT_SLOTS * NSTAT, e->tstat + size_t(w0) * NSTAT, n, e->stream));
+  HIPCHK(launch_stats_reduce(e->hist + size_t(w0) * STAT_SLOTS * NSTAT, e->tstat + size_t(w0) * NSTAT, n, e->stream,
+                             chk));
   if (!e->comm) return RAFT_OK;
   if (e->comm_ev.empty()) {
     hipEvent_t x;
@@ -794,10 +889,12 @@ static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1) {
 }
 
 static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool stats) {
+  if (int rc = settle_check(e)) return rc;
   if (int rc = check_ticks(e, first_tick, nticks)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
-  if (stats)
-    if (int rc = ensure_hist(e, nticks)) return rc;
+  // (the per-tick records need nticks slots; the check records exist at any capacity)
+  if (int rc = ensure_hist(e, stats ? std::max<uint32_t>(nticks, 1) : 1)) return rc;
+  if (!nticks) return RAFT_OK;
   const Trace T0 = make_trace(e, first_tick);
   int64_t win_first = first_tick;   // first tick of the current general-kernel window
   // steady-state list skip (see raft_engine): entries per tick at most E, so
@@ -806,6 +903,9 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
                          !e->force_general && uint64_t(e->cfg.entries_per_tick) < e->cfg.ring_depth &&
                          double(e->cfg.entries_per_tick) * double(first_tick + int64_t(nticks) + 2) < 2.0e9;
   e->skipped_list = skip_list;
+  e->n_ticks += nticks;
+  if (skip_list) e->n_skip_ticks += nticks;
+  const bool two = e->two_pass && !e->force_general && !e->write_through;
   uint32_t stats_first = 0;   // first tick (index in this call) whose records are not reduced yet
   hipEvent_t ra = nullptr, rb = nullptr;
   if (e->prof == 2) {
@@ -828,7 +928,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
     }
     const int force = e->force_general;
-    if (e->two_pass && !force && !e->write_through) {
+    if (two) {
       // lean pass appends to list counter lpar, the list pass zeroes the other one
       hipEvent_t c = nullptr, d = nullptr;
       if (e->prof == 3 && !skip_list) {
@@ -857,17 +957,21 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       // (with the list skipped nothing can be deferred — only the list kernel
       // defers — so both worklist counters stay zero and the general kernel
       // has nothing to do)
-      if (!skip_list)
+      if (!skip_list) {
         HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t,
                                 stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
                                 e->wcount + ((e->wpar + 1) & 1) * SHARD_WORDS, e->lane_general, e->stream));
+        ++e->n_general;
+      }
       ++e->wpar;
       // per-tick records: reduced (and all-reduced) per window; with the list
       // skipped on one GPU nothing overlaps them, so one reduce at the end of
-      // the call covers every tick
-      if (stats && (!skip_list || e->comm || i + 1 == nticks))
-        if (int rc = flush_window_stats(e, stats_first, i)) return rc;
-      if (!skip_list || e->comm || i + 1 == nticks) stats_first = i + 1;
+      // the call covers every tick. The last one carries the check record.
+      const bool last = i + 1 == nticks;
+      const CallCheck chk{e->wcount, int((e->wpar + 1) & 1), skip_list ? 1 : 0, e->tstat + size_t(nticks) * NSTAT};
+      if (stats && (!skip_list || e->comm || last))
+        if (int rc = flush_window_stats(e, stats_first, i, (last && two) ? &chk : nullptr)) return rc;
+      if (!skip_list || e->comm || last) stats_first = i + 1;
       win_first = t + 1;
     }
   }
@@ -880,21 +984,32 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     HIPCHK(hipEventRecord(e->comm_ev[1], e->comm_stream));
     HIPCHK(hipStreamWaitEvent(e->stream, e->comm_ev[1], 0));
   }
+  if (!stats && skip_list) {
+    // no readback in this call: the check record goes to tstat[cap + 1] and
+    // its pinned copy is verified by the next call (settle_check)
+    const CallCheck chk{e->wcount, int((e->wpar + 1) & 1), 1, e->tstat + size_t(e->hist_cap + 1) * NSTAT};
+    HIPCHK(launch_stats_reduce(nullptr, nullptr, 0, e->stream, &chk));
+    const size_t off = size_t(e->hist_cap + 1) * NSTAT;
+    HIPCHK(hipMemcpyAsync(e->hrb + off, e->tstat + off, NSTAT * 8, hipMemcpyDeviceToHost, e->stream));
+    if (!e->chk_ev) HIPCHK(hipEventCreateWithFlags(&e->chk_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(e->chk_ev, e->stream));
+    e->pend_chk = true;
+  }
   if (e->prof == 2) {
     HIPCHK(hipEventRecord(rb, e->stream));
     e->prof_n += nticks;
   }
-  if (e->P.dbg) {   // diagnostics: fast-kernel lane classes summed over this call's ticks (synchronising)
-    unsigned long long d[32];
+  if (e->P.dbg && e->diag_print) {   // diagnostics: lane classes summed over this call's ticks (synchronising)
+    unsigned long long d[64];
     HIPCHK(hipMemcpyAsync(d, e->P.dbg, sizeof d, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemsetAsync(e->P.dbg, 0, sizeof d, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    fprintf(stderr,
-            "raftstep: ticks %lld..%lld lanes %llu skip %llu bail %llu iso %llu drift<=K %llu drift>K %llu switch %llu "
-            "blk_hi %llu blk_seg %llu coop %llu drifted %llu | bail: not-steady %llu iso-leader/multi %llu "
-            "follower-out-of-step %llu raft-rows %llu other %llu | quiet-leaderless %llu isolated-leader %llu ssync %llu\n",
-            (long long)first_tick, (long long)(first_tick + nticks - 1), d[10], d[0], d[1], d[2], d[3], d[4], d[5], d[6],
-            d[7], d[8], d[9], d[11], d[12], d[13], d[14], d[15], d[16], d[17], d[18]);
+    fprintf(stderr, "raftstep: ticks %lld..%lld lean:", (long long)first_tick, (long long)(first_tick + nticks - 1));
+    for (int k = 0; k < 64; ++k) {
+      if (k == 32) fprintf(stderr, " | list:");
+      if (d[k]) fprintf(stderr, " %d=%llu", k & 31, d[k]);
+    }
+    fprintf(stderr, "\n");
   }
   return RAFT_OK;
 }
@@ -903,30 +1018,32 @@ int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_sta
   if (!e) return fail(RAFT_EINVAL, "null engine");
   if (int rc = tick_impl(e, first_tick, nticks, out != nullptr)) return rc;
   if (out) {
-    // per-tick records, already summed over slots (and over GPUs)
-    std::vector<unsigned long long> h(size_t(nticks) * NSTAT);
-    HIPCHK(hipMemcpyAsync(h.data(), e->tstat, h.size() * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
     std::memset(out, 0, sizeof *out);
-    for (size_t i = 0; i < h.size(); ++i) out->v[i % NSTAT] += int64_t(h[i]);
-    // steady-state list skip: both list counters (a call that skipped never
-    // zeroed them) and the last general window's worklist counter
-    if (e->two_pass && !e->write_through && e->steady_origin) {
-      uint32_t c[4 * SHARD_WORDS];
-      HIPCHK(hipMemcpyAsync(c, e->wcount, sizeof c, hipMemcpyDeviceToHost, e->stream));
-      HIPCHK(hipStreamSynchronize(e->stream));
-      uint64_t listed = 0, deferred = 0;
-      const uint32_t wlast = (e->wpar + 1) & 1;   // the window the last general kernel consumed
-      for (int k = 0; k < NSHARD; ++k) {
-        listed += c[(2 * SHARD_WORDS) + k * SHARD_STRIDE] + c[(3 * SHARD_WORDS) + k * SHARD_STRIDE];
-        deferred += c[wlast * SHARD_WORDS + k * SHARD_STRIDE];
-      }
-      if (e->skipped_list && listed) {
+    if (!nticks) return RAFT_OK;
+    // one readback per call: the per-tick records (already summed over slots,
+    // and over GPUs) and, behind them, the end-of-call check record
+    const bool two = e->two_pass && !e->force_general && !e->write_through;
+    const size_t words = size_t(nticks + (two ? 1 : 0)) * NSTAT;
+    HIPCHK(hipMemcpyAsync(e->hrb, e->tstat, words * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->last_stats_n = nticks;
+    for (size_t i = 0; i < size_t(nticks) * NSTAT; ++i) out->v[i % NSTAT] += int64_t(e->hrb[i]);
+    if (two) {
+      const unsigned long long* c = e->hrb + size_t(nticks) * NSTAT;
+      if (c[CHK_MAGIC] != 0x5241465443484Bull) {
         e->steady_ok = false;
-        return fail(RAFT_EINTERNAL, "steady-state list skip: %llu groups were passed to a list kernel that did not run",
-                    (unsigned long long)listed);
+        return fail(RAFT_EINTERNAL, "end-of-call check record missing");
       }
-      e->steady_ok = listed == 0 && deferred == 0;
+      if (e->skipped_list && c[CHK_LISTED]) {   // (the check block zeroed the list counters)
+        e->poisoned = true;
+        e->steady_ok = false;
+        e->poison_msg = "steady-state list skip: " + std::to_string(c[CHK_LISTED]) +
+                        " groups were passed to a list kernel that did not run (ticks lost)";
+        return fail(RAFT_EINTERNAL, "%s", e->poison_msg.c_str());
+      }
+      // steady-state list skip: proven for the next call when nothing was
+      // listed at the last tick and the last general window took nothing
+      if (e->steady_origin) e->steady_ok = c[CHK_LISTED] == 0 && c[CHK_DEFERRED] == 0;
     }
   }
   return RAFT_OK;
@@ -934,7 +1051,8 @@ int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_sta
 
 int raft_tick_records(raft_engine* e, uint32_t nticks, raft_tick_stats* per_tick) {
   if (!e || (nticks && !per_tick)) return fail(RAFT_EINVAL, "null argument");
-  if (nticks > e->hist_cap || !e->tstat) return fail(RAFT_ERANGE, "only %u per-tick records are held", e->hist_cap);
+  if (nticks > e->last_stats_n || !e->tstat)
+    return fail(RAFT_ERANGE, "the last raft_tick call with statistics produced %u per-tick records", e->last_stats_n);
   HIPCHK(hipSetDevice(e->cfg.device));
   std::vector<unsigned long long> h(size_t(nticks) * NSTAT);
   HIPCHK(hipMemcpyAsync(h.data(), e->tstat, h.size() * 8, hipMemcpyDeviceToHost, e->stream));
@@ -948,13 +1066,14 @@ int raft_sync(raft_engine* e) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
   HIPCHK(hipSetDevice(e->cfg.device));
   HIPCHK(hipStreamSynchronize(e->stream));
-  return RAFT_OK;
+  return settle_check(e);
 }
 
 int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_req* reqs, size_t n,
                               const raft_log_entry* entries, size_t n_entries_total, raft_ae_resp* out) {
-  if (e) e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
+  if (int rc = settle_check(e)) return rc;
+  e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &reqs[0].group, sizeof(raft_ae_req), n)) return rc;
   std::vector<DevOp> ops(n);
@@ -1005,8 +1124,9 @@ int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_re
 
 int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_req* reqs, size_t n,
                             raft_vote_resp* out) {
-  if (e) e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
+  if (int rc = settle_check(e)) return rc;
+  e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &reqs[0].group, sizeof(raft_vote_req), n)) return rc;
   std::vector<DevOp> ops(n);
@@ -1035,8 +1155,9 @@ int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_re
 
 int raft_group_ops_batch(raft_engine* e, int64_t now_tick, const raft_group_op* ops_in, size_t n,
                          raft_op_result* out) {
-  if (e) e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (!e || (n && (!ops_in || !out))) return fail(RAFT_EINVAL, "null argument");
+  if (int rc = settle_check(e)) return rc;
+  e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &ops_in[0].group, sizeof(raft_group_op), n)) return rc;
   std::vector<DevOp> ops(n);
@@ -1112,6 +1233,14 @@ int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats) {
 int raft_profile_enable(raft_engine* e, int mode) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
   if (mode < 0 || mode > 3) return fail(RAFT_EINVAL, "profile mode must be 0, 1, 2 or 3");
+  HIPCHK(hipSetDevice(e->cfg.device));
+  // events are created here, not inside the timed calls (hipEventCreate costs
+  // tens of microseconds); more are added on demand
+  while (mode && e->ev.size() < 128) {
+    hipEvent_t x;
+    HIPCHK(hipEventCreate(&x));
+    e->ev.push_back(x);
+  }
   e->prof = mode;
   e->ev_used = 0;
   e->prof_ms = 0.0;
@@ -1135,10 +1264,52 @@ int raft_profile_read(raft_engine* e, double* total_ms, uint64_t* launches) {
   return RAFT_OK;
 }
 
+// ---- diagnostics -----------------------------------------------------------
+
+int raft_diag_enable(raft_engine* e, int on) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  HIPCHK(hipSetDevice(e->cfg.device));
+  if (!e->dbg_buf && e->P.dbg) e->dbg_buf = e->P.dbg;   // (allocated at creation by RAFTSTEP_DEBUG_FAST)
+  if (on && !e->dbg_buf) {
+    if (int rc = dev_alloc(e, reinterpret_cast<void**>(&e->dbg_buf), RAFT_DIAG_DEVICE_COUNTERS * 8)) return rc;
+  }
+  if (e->dbg_buf) HIPCHK(hipMemsetAsync(e->dbg_buf, 0, RAFT_DIAG_DEVICE_COUNTERS * 8, e->stream));
+  e->P.dbg = on ? e->dbg_buf : nullptr;   // (the buffer stays allocated; counting stops)
+  e->n_ticks = e->n_skip_ticks = e->n_general = 0;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return RAFT_OK;
+}
+
+int raft_diag_read(raft_engine* e, uint64_t* counters, uint32_t n) {
+  if (!e || (n && !counters)) return fail(RAFT_EINVAL, "null argument");
+  if (n > RAFT_DIAG_COUNTERS) return fail(RAFT_ERANGE, "at most %u counters", RAFT_DIAG_COUNTERS);
+  HIPCHK(hipSetDevice(e->cfg.device));
+  uint64_t all[RAFT_DIAG_COUNTERS] = {};
+  if (e->P.dbg) {
+    HIPCHK(hipMemcpyAsync(all, e->P.dbg, RAFT_DIAG_DEVICE_COUNTERS * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemsetAsync(e->P.dbg, 0, RAFT_DIAG_DEVICE_COUNTERS * 8, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  all[RAFT_DIAG_TICKS] = e->n_ticks;
+  all[RAFT_DIAG_TICKS_LIST_SKIPPED] = e->n_skip_ticks;
+  all[RAFT_DIAG_GENERAL_LAUNCHES] = e->n_general;
+  e->n_ticks = e->n_skip_ticks = e->n_general = 0;
+  for (uint32_t i = 0; i < n; ++i) counters[i] = all[i];
+  return RAFT_OK;
+}
+
+int raft_debug_force_pass(raft_engine* e, int64_t group) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  if (group >= int64_t(e->cfg.groups)) return fail(RAFT_EINVAL, "group out of range");
+  e->P.dbg_pass = group < 0 ? 0xFFFFFFFFu : uint32_t(group);
+  return RAFT_OK;
+}
+
 // ---- audit: digest, nodelog, checkpoints ----------------------------------
 
 int raft_state_digest(raft_engine* e, uint64_t* per_group, uint64_t* total) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
+  if (int rc = settle_check(e)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   const uint64_t G = e->cfg.groups;
   uint64_t* d_pg = nullptr;
@@ -1161,6 +1332,7 @@ int raft_state_digest(raft_engine* e, uint64_t* per_group, uint64_t* total) {
 int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap) {
   if (!e || (!buf && cap)) return fail(RAFT_EINVAL, "null argument");
   if (group >= e->cfg.groups) return fail(RAFT_EINVAL, "group %llu out of range", (unsigned long long)group);
+  if (int rc = settle_check(e)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   static const char* names[] = {"follower", "candidate", "leader", "?"};   // State (main.go:51-57)
   std::string out;
@@ -1313,7 +1485,7 @@ int raft_checkpoint_save(raft_engine* e, const char* path) {
 }
 
 int raft_checkpoint_load(raft_engine* e, const char* path) {
-  if (e) e->steady_origin = e->steady_ok = false;
+  if (e) state_replaced(e);
   if (!e || !path) return fail(RAFT_EINVAL, "null argument");
   const uint64_t G = e->cfg.groups, R = e->cfg.replicas, K = e->cfg.ring_depth;
   File f;
@@ -1328,7 +1500,9 @@ int raft_checkpoint_load(raft_engine* e, const char* path) {
   CkptHeader h{};
   if (!get(&h, sizeof h) || std::memcmp(h.magic, CKPT_MAGIC, 8) != 0)
     return fail(RAFT_EINVAL, "%s: not a raftstep checkpoint", path);
-  if (h.version != CKPT_VERSION) return fail(RAFT_EINVAL, "%s: checkpoint version %u unsupported", path, h.version);
+  // version 1 (before leader isolation) has every field but iso_victim, the last one
+  if (h.version != CKPT_VERSION && h.version != 1)
+    return fail(RAFT_EINVAL, "%s: checkpoint version %u unsupported", path, h.version);
   if (h.cfg.replicas != e->cfg.replicas || h.cfg.groups != e->cfg.groups || h.cfg.ring_depth != e->cfg.ring_depth ||
       h.cfg.semantics != e->cfg.semantics || h.cfg.payload_crc != e->cfg.payload_crc)
     return fail(RAFT_EINVAL, "%s: checkpoint of R=%u G=%llu K=%u sem=%u crc=%u does not fit this engine", path,
@@ -1357,6 +1531,7 @@ int raft_checkpoint_load(raft_engine* e, const char* path) {
   }
   raft_state_view v{};
   auto fields = view_fields(v, G, R, K);
+  if (h.version == 1) fields.pop_back();   // iso_victim: absent (loads as 0)
   if (h.nfields != fields.size()) return fail(RAFT_EINVAL, "%s: %u fields, expected %zu", path, h.nfields, fields.size());
   std::vector<std::vector<uint8_t>> bufs(fields.size());
   for (size_t i = 0; i < fields.size(); ++i) {

@@ -521,6 +521,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           sv[4] = 1;       // term bumps: w's timeout
           sv[5] = R - 2;   // votes granted
           sv[6] = 1;       // elections won
+          df |= 1u << 19;  // class: the election tick of a cut-off leader's group
         }
         if (nm != meta) GW.meta() = uint16_t(nm);
       }
@@ -674,6 +675,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       // sr's entry L0+1 is from its ring or the one its own client append adds this tick
       bail |= (L0 + 1 <= Ll ? tc1 : Lt) == (L0 + 1 <= ls ? ts1 : sel(term, sr));
       if (!bail) {
+        df |= (1u << 21) | (ls > L0 ? 1u << 22 : 0u);   // class: stale leader's return (its log truncated at L0)
         // the primary's entries after L0 (at most K): copied below by the whole wave
         cp_n = Ll - L0;
         cp_from = L0 + 1;
@@ -726,6 +728,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           sync &= (p == c) || m[p] == last[p];
         }
       }
+      df |= (fresh ? 1u << 20 : 0u) | (stale ? 1u << 23 : 0u) | (xi >= 0 && !stale ? 1u << 26 : 0u) |
+            (x_fire ? 1u << 27 : 0u) | (hwx || hwup ? 1u << 24 : 0u);   // classes taken this tick
       sv[0] = cm - Lc;
       sv[1] = __builtin_popcount(okm);
       sv[2] = (R - 1) - sv[1] + (stale ? R - 1 : 0) + (sr >= 0 && sr < c ? 1 : 0);   // + every AppendEntries of the
@@ -884,7 +888,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             df |= hi > Ll ? 64u : 0u;
             df |= ok ? 0u : 128u;
             if (hi <= Ll && ok) {
-              df |= 32u;
+              df |= 32u | ((sbo <= 1 || sbo <= lo - int(P.K) + 1) ? 0u : 1u << 25);   // (+ the previous segment stays live)
               GW.rotb() = uint16_t(rota);   // the three segments shift
               GW.sb2() = sbo;
               GW.rota() = uint16_t(rot);
@@ -919,6 +923,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     }
     if (bail) GW.meta() = uint16_t(meta | M_DEFER);
     else if (giso_w >= 0) GW.iso() = uint8_t(giso_w);   // a leader-isolation window decided this tick
+    df |= (!bail && giso_w >= 0) ? 1u << 28 : 0u;
     stored = !skip && !bail;
   }
   // ---- this tick's log entries into the rings (all lanes of the wave) ----
@@ -1060,10 +1065,11 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     df |= (g < P.G) ? 1024u : 0u;
     DIAG_REASON(if (bail && !(df & (2048u | 4096u | 8192u | 16384u))) df |= 32768u;);   // reason: anything later
     DIAG_REASON(if (!bail) df &= ~(2048u | 4096u | 8192u | 16384u););
+    if (bail) df &= ~0x1FF80000u;   // the class bits 19-28 count taken ticks only
 #pragma unroll 1
-    for (int k = 0; k < 19; ++k) {
+    for (int k = 0; k < 32; ++k) {
       const uint64_t b = __ballot((df >> k) & 1u);
-      if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
+      if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[32 + k], (unsigned long long)__popcll(b));
     }
   }
   // groups that need the general path go to the sharded worklist: dense
@@ -1301,8 +1307,9 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     const int meta = at(P.gmeta, g);
     const int c = meta & 0xF;
     const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
-    take = !skip && (meta & M_SSYNC) && c < R;
+    take = !skip && (meta & M_SSYNC) && c < R && g != P.dbg_pass;   // (test knob: pass one group on)
     pass = !skip && !take;
+    df |= (!skip && g == P.dbg_pass) ? 1u << 24 : 0u;
     df |= skip ? 1u : 0u;
     if (take) {
       const SsRec s = P.gss[g];
@@ -1349,7 +1356,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
           // lines then; otherwise the leader's column alone.
           const bool whole = P.KP >= 2u * P.K && x.k + n <= int(P.K) && at(P.gsb, g) <= L - int(P.K) + 1;
           wmask = whole ? (1u << R) - 1u : (1u << c);
-          df |= 131072u | 256u;
+          df |= 131072u | 256u | (1u << 19) | (whole ? 1u << 21 : 0u);
         } else {
           pass = true;
         }
@@ -1392,6 +1399,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
             const uint32_t rota = at(P.grota, g);
             sw = ring_switch_ok(d, uint32_t(rot), rota, sbo, at(P.gsb2, g), L, P.K, P.kmask);
             sw_rota = int(rota);
+            df |= sw ? 1u << 20 : 0u;   // class: a switch while the previous segment stays live (three segments)
           }
         }
         if (sw) sw_d = int(d);
@@ -1428,6 +1436,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         P.gss[g] = SsRec{nl, s.term, cl2, cf2};
         at(P.hb, g) = T.now;                               // timer.Reset(d) of every follower
         if (hwx_clear) at(P.gmeta, g) = uint16_t(meta & ~M_HWX);
+        if (RAFT && (meta & M_HWX)) df |= 1u << 22;   // class: a truncated log in step (HWX)
         if (sw_d) {   // the new segment starts at this tick's first entry
           if (sw_rota >= 0) at(P.grotb, g) = uint16_t(sw_rota);   // (else the older segments are dead)
           at(P.gsb2, g) = sbo;
@@ -1501,8 +1510,10 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   }
   if (P.dbg) {   // diagnostics (same class bits as fast_group): lanes, skipped, taken by the lean pass
     df |= (g < P.G) ? 1024u : 0u;
+    df |= pass ? 1u << 23 : 0u;
+    if (!take) df &= ~0x780000u;   // the class bits 19-22 count taken ticks only
 #pragma unroll 1
-    for (int k = 0; k < 19; ++k) {
+    for (int k = 0; k < 25; ++k) {
       const uint64_t b = __ballot((df >> k) & 1u);
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
     }
@@ -1568,25 +1579,6 @@ hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, 
   return hipGetLastError();
 }
 
-// Resident blocks of a kernel (CUs x blocks per CU at its occupancy), per device.
-template <typename Kern>
-static unsigned resident_blocks_fast(Kern k, int block = 256) {
-  constexpr int MAXDEV = 64;
-  static unsigned resident_of[MAXDEV] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
-  unsigned& resident = resident_of[dev % MAXDEV];
-  if (!resident) {
-    int cus = 0, per = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, block, 0) == hipSuccess && cus > 0 && per > 0)
-      resident = unsigned(cus) * unsigned(per);
-    else
-      resident = 2048;
-  }
-  return resident;
-}
-
 template <int R, bool CRC, int SEM>
 static void launch_two_pass_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                               int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
@@ -1609,17 +1601,17 @@ static void launch_two_pass_t(const DevPlanes& P, const Trace& T, unsigned long 
   }();
   if (stage && lb == 64) {
     const unsigned blocks = unsigned(
-        std::min<uint64_t>((P.G + 63) / 64, resident_blocks_fast(tick_list_kernel<R, false, CRC, SEM, 64>, 64)));
+        std::min<uint64_t>((P.G + 63) / 64, resident_blocks(tick_list_kernel<R, false, CRC, SEM, 64>, 64)));
     hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM, 64>, dim3(blocks), dim3(64), 0, s, c, d, 0, P, T, stats,
                           work, work_tick, work_count, list, count, next_count);
   } else if (stage) {
     const unsigned blocks = unsigned(
-        std::min<uint64_t>((P.G + 255) / 256, resident_blocks_fast(tick_list_kernel<R, false, CRC, SEM, 256>, 256)));
+        std::min<uint64_t>((P.G + 255) / 256, resident_blocks(tick_list_kernel<R, false, CRC, SEM, 256>, 256)));
     hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM, 256>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats,
                           work, work_tick, work_count, list, count, next_count);
   } else {
     const unsigned blocks = unsigned(
-        std::min<uint64_t>((P.G + 255) / 256, resident_blocks_fast(tick_list_plain_kernel<R, false, CRC, SEM>)));
+        std::min<uint64_t>((P.G + 255) / 256, resident_blocks(tick_list_plain_kernel<R, false, CRC, SEM>)));
     hipExtLaunchKernelGGL(tick_list_plain_kernel<R, false, CRC, SEM>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T,
                           stats, work, work_tick, work_count, list, count, next_count);
   }

@@ -149,8 +149,42 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
 // all-reduce carries) and zeroed for the next raft_tick call, so the atomic
 // targets never need a memset on the critical path. One 64-lane block per
 // tick; lane = slot.
-__global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hist, unsigned long long* out) {
+// With a CallCheck, one more block (the last) writes the end-of-call check
+// record: the groups the lean kernel passed to the list at the call's last
+// tick (both list counters), the groups the last general window took, and —
+// in a list-skipping call, where no list kernel consumed or zeroed them — the
+// list counters are zeroed so a later list kernel never reads stale entries.
+__device__ __forceinline__ void call_check_block(const CallCheck& c) {
+  uint64_t listed = 0, deferred = 0;
+  if (threadIdx.x < uint32_t(NSHARD)) {
+    const uint32_t k = threadIdx.x * SHARD_STRIDE;
+    listed = uint64_t(c.wcount[2 * SHARD_WORDS + k]) + uint64_t(c.wcount[3 * SHARD_WORDS + k]);
+    deferred = c.wcount[uint32_t(c.wlast) * SHARD_WORDS + k];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    listed += __shfl_xor(listed, o);
+    deferred += __shfl_xor(deferred, o);
+  }
+  __syncthreads();   // every lane has read the counters before any is zeroed
+  if (c.zero_lists && threadIdx.x < uint32_t(NSHARD)) {
+    c.wcount[2 * SHARD_WORDS + threadIdx.x * SHARD_STRIDE] = 0u;
+    c.wcount[3 * SHARD_WORDS + threadIdx.x * SHARD_STRIDE] = 0u;
+  }
+  if (threadIdx.x < NSTAT) {
+    const unsigned long long v = threadIdx.x == CHK_LISTED ? listed : threadIdx.x == CHK_DEFERRED ? deferred
+                                 : threadIdx.x == CHK_MAGIC ? 0x5241465443484Bull : 0ull;
+    c.out[threadIdx.x] = v;
+  }
+}
+
+__global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hist, unsigned long long* out,
+                                                          uint32_t nticks, CallCheck chk) {
   static_assert(STAT_SLOTS == 64, "one lane per slot");
+  if (blockIdx.x == nticks) {
+    call_check_block(chk);
+    return;
+  }
   unsigned long long* h = hist + size_t(blockIdx.x) * STAT_SLOTS * NSTAT + threadIdx.x * NSTAT;
   unsigned long long v[NSTAT];
 #pragma unroll
@@ -169,9 +203,12 @@ __global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hi
     out[size_t(blockIdx.x) * NSTAT + threadIdx.x] = x;
   }
 }
-hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s) {
-  if (!nticks) return hipSuccess;
-  hipLaunchKernelGGL(stats_reduce_kernel, dim3(nticks), dim3(64), 0, s, hist, out);
+hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s,
+                               const CallCheck* chk) {
+  const uint32_t blocks = nticks + (chk ? 1u : 0u);
+  if (!blocks) return hipSuccess;
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3(blocks), dim3(64), 0, s, hist, out, chk ? nticks : 0xFFFFFFFFu,
+                     chk ? *chk : CallCheck{});
   return hipGetLastError();
 }
 

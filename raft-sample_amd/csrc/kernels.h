@@ -63,9 +63,23 @@ hipError_t launch_init_new(int R, const DevPlanes& P, const Trace& T, hipStream_
 // Per-group state digest (same definition as oracle_state_digest) + wrapping sum.
 hipError_t launch_digest(int R, const DevPlanes& P, int raft, uint64_t* per_group, unsigned long long* total,
                          hipStream_t s);
+// End-of-call check record (one more block of the stats reduce launch):
+// out[CHK_LISTED] = groups on the two-pass list counters (both parities),
+// out[CHK_DEFERRED] = groups the last general window's worklist held,
+// out[CHK_MAGIC] = a constant proving the record was written this call.
+// zero_lists: zero both list counters afterwards (a list-skipping call).
+enum : int { CHK_LISTED = 0, CHK_DEFERRED = 1, CHK_MAGIC = 7 };
+struct CallCheck {
+  uint32_t* wcount;             // the engine's shard counters (worklist x2, list x2)
+  int wlast;                    // parity of the worklist counter the last general kernel consumed
+  int zero_lists;
+  unsigned long long* out;      // NSTAT words
+};
 // Sums the STAT_SLOTS slots of nticks consecutive per-tick records of `hist`
-// into out[nticks][NSTAT] and zeroes those slots.
-hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s);
+// into out[nticks][NSTAT] and zeroes those slots; with `chk` also writes the
+// check record (nticks may then be 0).
+hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s,
+                               const CallCheck* chk = nullptr);
 hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s);
 
 }  // namespace raftstep

@@ -106,7 +106,9 @@ struct DevPlanes {
   uint32_t K;          // ring depth (power of two): the last K entries of every log stay readable
   uint32_t KP;         // physical ring slots per replica: K, or 2K when segment switches are on
   uint32_t kmask;      // KP - 1 (physical slot mask)
-  unsigned long long* dbg;  // diagnostics (RAFTSTEP_DEBUG_FAST): fast-kernel lane class counters, else null
+  unsigned long long* dbg;  // diagnostics (raft_diag_enable): lane class counters [0,32) lean kernel,
+                            // [32,64) fast_group (list / one-pass kernels), else null
+  uint32_t dbg_pass;   // test knob (raft_debug_force_pass): the lean kernel passes this group to the list (~0u: none)
   int32_t* rec;        // [Gp][NPL][R] group records holding every per-replica row above (see rix)
   uint32_t scap;       // capacity of one shard of a sharded group list (see below)
   uint32_t diag;       // timing-only diagnostics (RAFTSTEP_DIAG_LEAN; results are wrong when set): 1 = drifted

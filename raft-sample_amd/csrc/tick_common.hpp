@@ -7,6 +7,8 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 namespace raftstep {
 
@@ -218,5 +220,30 @@ __device__ __forceinline__ void with_replica(int x, F&& f) {
   }
 
 static inline dim3 grid_for(uint64_t n) { return dim3(unsigned((n + 255) / 256)); }
+
+// Resident blocks of kernel `k` at `block` threads per block on the current
+// device (CUs x blocks per CU at its register / LDS occupancy), cached per
+// (device, kernel, block size): kernels of one signature (e.g. every R's
+// general kernel) must not share an entry, and engines on different GPUs of
+// one process may see different CU counts.
+template <typename Kern>
+static unsigned resident_blocks(Kern k, int block = 256) {
+  struct Ent { int dev; const void* fn; int block; unsigned n; };
+  static std::mutex mu;
+  static std::vector<Ent> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  const void* fn = reinterpret_cast<const void*>(k);
+  std::lock_guard<std::mutex> lock(mu);
+  for (const Ent& x : cache)
+    if (x.dev == dev && x.fn == fn && x.block == block) return x.n;
+  int cus = 0, per = 0;
+  unsigned n = 2048;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, block, 0) == hipSuccess && cus > 0 && per > 0)
+    n = unsigned(cus) * unsigned(per);
+  cache.push_back(Ent{dev, fn, block, n});
+  return n;
+}
 
 }  // namespace raftstep

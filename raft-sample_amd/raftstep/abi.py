@@ -24,6 +24,19 @@ NSTATS = len(STAT_NAMES)
 OP_CLIENT_APPEND, OP_LEADER_ROUND, OP_CANDIDATE_ROUND, OP_TIMEOUT, OP_LEADER_COMMIT = 1, 2, 3, 4, 5
 
 RAFT_EINVAL, RAFT_ENOMEM, RAFT_ERANGE, RAFT_ENODEV = -22, -12, -34, -19
+RAFT_EINTERNAL = -3000
+
+# raft_diag_read counters (include/raftstep.h enum raft_diag_counter)
+DIAG_COUNTERS = 72
+DIAG = {
+    "lean_lanes": 10, "lean_skipped": 0, "lean_ssync": 18, "lean_lxs": 19, "lean_three_seg": 20,
+    "lean_lxs_whole_row": 21, "lean_hwx": 22, "lean_passed": 23, "lean_forced": 24, "lean_switch": 5,
+    "list_lanes": 42, "list_deferred": 33, "list_isolation": 34, "list_switch": 37, "list_quiet": 48,
+    "list_isolated_leader": 49, "list_ssync": 50, "list_election": 51, "list_first_round": 52,
+    "list_return": 53, "list_return_trunc": 54, "list_stale": 55, "list_hwx": 56, "list_three_seg": 57,
+    "list_isolated_replica": 58, "list_timer_fire": 59, "list_window_start": 60,
+    "ticks": 64, "ticks_list_skipped": 65, "general_launches": 66,
+}
 
 
 class Config(C.Structure):
@@ -174,6 +187,7 @@ SIGNATURES = {
     "raft_init_steady": (C.c_int, [P, C.c_int32, C.c_int64]),
     "raft_load_state": (C.c_int, [P, P]),
     "raft_store_state": (C.c_int, [P, P]),
+    "raft_store_state_range": (C.c_int, [P, C.c_uint64, C.c_uint64, P]),
     "raft_tick": (C.c_int, [P, C.c_int64, C.c_uint32, P]),
     "raft_sync": (C.c_int, [P]),
     "raft_tick_records": (C.c_int, [P, C.c_uint32, P]),
@@ -190,6 +204,9 @@ SIGNATURES = {
     "raft_nodelog": (C.c_int, [P, C.c_uint64, C.c_char_p, C.c_size_t]),
     "raft_checkpoint_save": (C.c_int, [P, C.c_char_p]),
     "raft_checkpoint_load": (C.c_int, [P, C.c_char_p]),
+    "raft_diag_enable": (C.c_int, [P, C.c_int]),
+    "raft_diag_read": (C.c_int, [P, P, C.c_uint32]),
+    "raft_debug_force_pass": (C.c_int, [P, C.c_int64]),
 }
 
 

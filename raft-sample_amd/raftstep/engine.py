@@ -102,6 +102,16 @@ class Engine:
         _check(self.lib.raft_store_state(self.h, C.byref(v)))
         return st
 
+    def store_state_range(self, first_group, n_groups, logs=True):
+        """Canonical view of groups [first_group, first_group + n_groups) only (local indices)."""
+        st = abi.empty_state(n_groups, self.cfg.replicas, self.cfg.ring_depth)
+        if not logs:
+            for k in ("log_term", "log_value", "log_crc"):
+                st.pop(k)
+        v = abi.make_view(st)
+        _check(self.lib.raft_store_state_range(self.h, first_group, n_groups, C.byref(v)))
+        return st
+
     def load_state(self, st):
         st = abi.coerce_state(st, self.cfg.groups, self.cfg.replicas, self.cfg.ring_depth)
         v = abi.make_view(st)
@@ -204,3 +214,18 @@ class Engine:
         ms, n = C.c_double(), C.c_uint64()
         _check(self.lib.raft_profile_read(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    # -- diagnostics ---------------------------------------------------
+    def diag_enable(self, on=True):
+        """Zero and start (or stop) the tick-class counters (raft_diag_enable)."""
+        _check(self.lib.raft_diag_enable(self.h, int(bool(on))))
+
+    def diag_read(self):
+        """{class name: lanes} since the last read (abi.DIAG names; raft_diag_read), then zeroed."""
+        buf = (C.c_uint64 * abi.DIAG_COUNTERS)()
+        _check(self.lib.raft_diag_read(self.h, buf, abi.DIAG_COUNTERS))
+        return {k: int(buf[i]) for k, i in abi.DIAG.items()}
+
+    def debug_force_pass(self, group):
+        """Test knob: the lean kernel passes `group` (-1: none) to the list kernel."""
+        _check(self.lib.raft_debug_force_pass(self.h, int(group)))
