@@ -322,6 +322,8 @@ enum raft_diag_counter {
   RAFT_DIAG_LEAN_HWX = 22,            /* steady ticks of a group with a truncated log in step (HWX) */
   RAFT_DIAG_LEAN_PASSED = 23,         /* groups passed on to the list kernel */
   RAFT_DIAG_LEAN_FORCED = 24,         /* groups passed by raft_debug_force_pass */
+  RAFT_DIAG_LEAN_SXS = 25,            /* new leader replicating while the stale one is cut off (SXS) taken */
+  RAFT_DIAG_LEAN_SXS_STALE_IN_ROW = 26,/* ... with the stale leader's entry inside the common ring row */
   RAFT_DIAG_LEAN_SWITCH = 5,          /* ring segment switches */
   /* full fast-path body (list kernel / one-pass kernel): 32 + bit */
   RAFT_DIAG_LIST_LANES = 42,          /* groups looked at */
@@ -341,6 +343,8 @@ enum raft_diag_counter {
   RAFT_DIAG_LIST_ISOLATED_REPLICA = 58,/* one isolated follower / candidate */
   RAFT_DIAG_LIST_TIMER_FIRE = 59,     /* the isolated replica's election timer fired */
   RAFT_DIAG_LIST_WINDOW_START = 60,   /* a leader-isolation window decided on the fast path */
+  RAFT_DIAG_LIST_SXS_MATERIALISED = 61,/* SXS groups taken by the full body (explicit form rebuilt) */
+  RAFT_DIAG_LIST_SXS_ENTERED = 62,    /* ticks ending in the SXS compressed form */
   /* host counters since the last read */
   RAFT_DIAG_TICKS = 64,
   RAFT_DIAG_TICKS_LIST_SKIPPED = 65,  /* ticks run by the lean kernel alone (steady-state list skip) */
@@ -353,6 +357,10 @@ int raft_diag_read(raft_engine* e, uint64_t* counters, uint32_t n);
  * runs; in a list-skipping call the group's tick is lost, which the engine
  * detects (RAFT_EINTERNAL, engine poisoned until its state is replaced). */
 int raft_debug_force_pass(raft_engine* e, int64_t group);
+/* Debugging: the raw per-group words of one group (gmeta, giso, hb, the
+ * compressed record gss[4], glx[2], grot, grota, gsb, grotb, gsb2). */
+#define RAFT_DEBUG_GROUP_WORDS 14u
+int raft_debug_group_words(raft_engine* e, uint64_t group, int32_t* out, uint32_t n);
 
 #ifdef __cplusplus
 }

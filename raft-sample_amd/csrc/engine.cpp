@@ -647,20 +647,21 @@ int store_range(raft_engine* e, uint64_t g0, uint64_t n, raft_state_view* v) {
   if (raft) rec_rows(blk, PL_HWM, R, n, hw);
   if (logs) rec_rows(blk, PL_LTERM, R, n, ltm);
   std::vector<int32_t>().swap(blk);
-  // SSYNC groups: the planes are stale, the gss record is the state
+  // SSYNC groups: the planes are stale, the gss record (+ glx) is the state
   for (uint64_t g = 0; g < n; ++g) {
     const int pr = meta[g] & 0xF;
     if (!(meta[g] & M_SSYNC) || pr >= int(R)) continue;
     for (uint64_t r = 0; r < R; ++r) {
-      term[g * R + r] = gss[g].term;
+      term[g * R + r] = ss_term(gss[g], int(r), meta[g], glx[g]);
       last[g * R + r] = ss_last(gss[g], int(r), pr, meta[g], glx[g]);
-      commit[g * R + r] = int(r) == pr ? gss[g].cl : gss[g].cf;
-      if (!ltm.empty()) ltm[g * R + r] = gss[g].term;
+      commit[g * R + r] = ss_commit(gss[g], int(r), pr, meta[g], glx[g], commit[g * R + r]);
+      if (!ltm.empty()) ltm[g * R + r] = ss_term(gss[g], int(r), meta[g], glx[g]);
     }
   }
   for (uint64_t g = 0; g < n; ++g) {
     const int primary = meta[g] & 0xF;
     const bool msync = meta[g] & M_MSYNC;
+    const LxRec lxg = (meta[g] & M_SSYNC) ? glx[g] : LxRec{0, 0};
     const uint64_t gt = g0 + g - t0 * 64;   // group index inside the copied ring tiles
     if (v->fault) v->fault[g] = uint8_t((meta[g] >> 4) & 0xF);
     if (v->iso_victim) v->iso_victim[g] = giso[g];
@@ -683,15 +684,17 @@ int store_range(raft_engine* e, uint64_t g0, uint64_t n, raft_state_view* v) {
         for (uint64_t p = 0; p < R; ++p) {
           int32_t m = 0;
           if (role == ROLE_L && p != r)
-            m = (int(r) == primary) ? (msync ? last[g * R + p] : lm[g * R + p]) : xm[(r * R + p) * n + g];
+            m = (int(r) == primary) ? (msync_peer(meta[g], lxg, int(p)) ? last[g * R + p] : lm[g * R + p])
+                                    : xm[(r * R + p) * n + g];
           v->match[c * R + p] = m;
         }
       if (v->next)
         for (uint64_t p = 0; p < R; ++p) {
           int32_t nx = 0;
           if (role == ROLE_L && p != r) {
-            if (raft) nx = (int(r) == primary) ? (msync ? last[g * R + p] + 1 : ln[g * R + p]) : xn[(r * R + p) * n + g];
-            else nx = ((int(r) == primary) ? (msync ? last[g * R + p] : lm[g * R + p]) : xm[(r * R + p) * n + g]) + 1;
+            const bool mp = msync_peer(meta[g], lxg, int(p));
+            if (raft) nx = (int(r) == primary) ? (mp ? last[g * R + p] + 1 : ln[g * R + p]) : xn[(r * R + p) * n + g];
+            else nx = ((int(r) == primary) ? (mp ? last[g * R + p] : lm[g * R + p]) : xm[(r * R + p) * n + g]) + 1;
           }
           v->next[c * R + p] = nx;
         }
@@ -1298,6 +1301,32 @@ int raft_diag_read(raft_engine* e, uint64_t* counters, uint32_t n) {
   return RAFT_OK;
 }
 
+int raft_debug_group_words(raft_engine* e, uint64_t group, int32_t* out, uint32_t n) {
+  if (!e || (n && !out)) return fail(RAFT_EINVAL, "null argument");
+  if (group >= e->cfg.groups) return fail(RAFT_EINVAL, "group out of range");
+  HIPCHK(hipSetDevice(e->cfg.device));
+  uint16_t meta = 0, rot = 0, rota = 0, rotb = 0;
+  uint8_t iso = 0;
+  int32_t hb = 0, sb = 0, sb2 = 0;
+  SsRec ss{};
+  LxRec lx{};
+  HIPCHK(hipMemcpyAsync(&meta, e->P.gmeta + group, 2, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&iso, e->P.giso + group, 1, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&hb, e->P.hb + group, 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&ss, e->P.gss + group, sizeof ss, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&lx, e->P.glx + group, sizeof lx, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&rot, e->P.grot + group, 2, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&rota, e->P.grota + group, 2, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&sb, e->P.gsb + group, 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&rotb, e->P.grotb + group, 2, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&sb2, e->P.gsb2 + group, 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const int32_t w[RAFT_DEBUG_GROUP_WORDS] = {meta, iso, hb, ss.last, ss.term, ss.cl, ss.cf, lx.k, lx.dl, rot, rota, sb,
+                                             rotb, sb2};
+  for (uint32_t i = 0; i < n && i < RAFT_DEBUG_GROUP_WORDS; ++i) out[i] = w[i];
+  return RAFT_OK;
+}
+
 int raft_debug_force_pass(raft_engine* e, int64_t group) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
   if (group >= int64_t(e->cfg.groups)) return fail(RAFT_EINVAL, "group out of range");
@@ -1353,7 +1382,11 @@ int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap) {
     HIPCHK(hipMemcpyAsync(&last, e->P.last + d, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(&rs, e->P.rs + d, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    if (ssync) { term = ss.term; last = ss_last(ss, int(r), pr, meta, lx); commit = int(r) == pr ? ss.cl : ss.cf; }
+    if (ssync) {
+      term = ss_term(ss, int(r), meta, lx);
+      last = ss_last(ss, int(r), pr, meta, lx);
+      commit = ss_commit(ss, int(r), pr, meta, lx, commit);
+    }
     char line[128];
     snprintf(line, sizeof line, "[Server%u:%d:%d:%d][%s]\n", r, term, commit, last, names[rs & 3]);
     out += line;

@@ -256,7 +256,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
 #define DIAG_REASON(x)
 #endif
   if (g < P.G) {
-    const int meta = GW.meta();
+    int meta = GW.meta();
+    const int meta_st = meta;   // as stored (meta may drop the compressed-form flags below)
     const int c = meta & 0xF;
     const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
     // RAFT also takes ONECAND groups (their candidate must be isolated this tick, checked below)
@@ -277,17 +278,41 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     // CommitIndex; implies MSYNC). The rows are rebuilt in registers here and
     // either written back as the record or, when the tick breaks the form,
     // spilled as whole rows.
-    const bool ss = go && (meta & M_SSYNC);
+    bool ss = go && (meta & M_SSYNC);
     df |= skip ? 1u : 0u;
     DIAG_REASON(df |= bail ? 2048u : 0u;);   // diagnostics: deferral reason "group not steady"
     if (go) {
       if (ss) {
         const SsRec ss_rec = GW.ss();
-        const LxRec lxr = (RAFT && (meta & M_LXS)) ? GW.lx() : LxRec{0, 0};   // LXS: the leader is k ahead
+        const LxRec lxr = (RAFT && uses_glx(meta)) ? GW.lx() : LxRec{0, 0};   // LXS: the leader is k ahead
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          term[r] = ss_rec.term; last[r] = ss_last(ss_rec, r, c, meta, lxr); commit[r] = r == c ? ss_rec.cl : ss_rec.cf;
-          lt[r] = ss_rec.term;
+          term[r] = ss_term(ss_rec, r, meta, lxr); last[r] = ss_last(ss_rec, r, c, meta, lxr);
+          commit[r] = r == c ? ss_rec.cl : ss_rec.cf;
+          lt[r] = term[r];
+        }
+        if (RAFT && is_sxs(meta)) {
+          // SXS: the tick runs on the explicit ONESTALE form, so materialise it
+          // in the rows (Group::load's rule): every row but the stale leader's
+          // as the record says, its CommitIndex and the primary's MatchIndex /
+          // NextIndex for it as they stand, high-water marks max(plane, last)
+          const int xs = lxr.dl;
+          put(commit, xs, RW.at(PL_COMMIT, xs));
+          RW.store(PL_TERM, term);
+          RW.store(PL_LAST, last);
+          RW.store(PL_COMMIT, commit);
+          RW.store(PL_LTERM, lt);
+#pragma unroll
+          for (int p = 0; p < R; ++p) {
+            if (p != c && p != xs) {
+              RW.template st<WT>(PL_LMATCH, p, last[p]);
+              RW.template st<WT>(PL_LNEXT, p, last[p] + 1);
+            }
+            if (RW.at(PL_HWM, p) < last[p]) RW.template st<WT>(PL_HWM, p, last[p]);
+          }
+          meta &= ~(M_SSYNC | M_MSYNC);
+          ss = false;
+          df |= 1u << 29;   // class: an SXS group taken by the full body (materialised)
         }
       } else {
         RW.load(PL_TERM, term);
@@ -523,7 +548,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           sv[6] = 1;       // elections won
           df |= 1u << 19;  // class: the election tick of a cut-off leader's group
         }
-        if (nm != meta) GW.meta() = uint16_t(nm);
+        if (nm != meta_st) GW.meta() = uint16_t(nm);
       }
     }
     const bool gom = go && !lx;   // the main steady-state path
@@ -848,7 +873,30 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       nm = keep_ss ? (nm | M_SSYNC) : (nm & ~M_SSYNC);
       if (x_fire) nm = (nm & ~M_STEADY) | M_ONECAND;
       if (sr >= 0) nm = (nm & ~M_ONESTALE) | M_STEADY;   // one leader, every other replica a follower
-      if (nm != meta) GW.meta() = uint16_t(nm);
+      // SXS after this tick (RAFT; the rows were stored explicitly above and are
+      // now stale but for the stale leader's): every follower of the primary
+      // accepted, every log but the stale leader's ends at Ll+n with an entry
+      // of term Lt, the followers share one CommitIndex; the stale leader
+      // (term Lt-1, its last entry of that term) only appended to its own log
+      if constexpr (RAFT && !CRC) {
+        if (stale && !hwx && R >= 3 && okm == (peers & ~(1u << xi)) && Ll + n > 0 && (n > 0 || Llt == Lt) &&
+            x_term == Lt - 1 && (n > 0 || sel(lt, xi) == x_term)) {
+          const int f = (c != 0 && xi != 0) ? 0 : ((c != 1 && xi != 1) ? 1 : 2);   // any follower of the primary
+          const int cf = sel(commit, f);
+          bool sx = true;
+#pragma unroll
+          for (int p = 0; p < R; ++p)
+            if (p != c && p != xi) sx &= commit[p] == cf && last[p] == Ll + n && (n > 0 || lt[p] == Lt);
+          if (sx) {
+            GW.ss() = SsRec{Ll + n, Lt, cm, cf};
+            GW.lx() = LxRec{sel(last, xi) + n - (Ll + n), xi};
+            GW.template st_hb<WT>(T.now);   // (the stale leader's timer ignores hb: a leader's start is its own)
+            nm |= M_SSYNC | M_MSYNC;
+            df |= 1u << 30;   // class: entered SXS
+          }
+        }
+      }
+      if (nm != meta_st) GW.meta() = uint16_t(nm);
       // this tick's entries go to the leader log + every follower that accepted
       if (n) {
         bool same = true;   // every writer appends at Ll+1 (REF: a follower's log may run past its MatchIndex)
@@ -921,7 +969,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         }
       }
     }
-    if (bail) GW.meta() = uint16_t(meta | M_DEFER);
+    if (bail) GW.meta() = uint16_t(meta_st | M_DEFER);
     else if (giso_w >= 0) GW.iso() = uint8_t(giso_w);   // a leader-isolation window decided this tick
     df |= (!bail && giso_w >= 0) ? 1u << 28 : 0u;
     stored = !skip && !bail;
@@ -1065,7 +1113,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     df |= (g < P.G) ? 1024u : 0u;
     DIAG_REASON(if (bail && !(df & (2048u | 4096u | 8192u | 16384u))) df |= 32768u;);   // reason: anything later
     DIAG_REASON(if (!bail) df &= ~(2048u | 4096u | 8192u | 16384u););
-    if (bail) df &= ~0x1FF80000u;   // the class bits 19-28 count taken ticks only
+    if (bail) df &= ~0x7FF80000u;   // the class bits 19-30 count taken ticks only
 #pragma unroll 1
     for (int k = 0; k < 32; ++k) {
       const uint64_t b = __ballot((df >> k) & 1u);
@@ -1185,11 +1233,14 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     uint8_t gi0 = 0;
     int32_t hb0 = 0;
     SsRec ss0{0, 0, 0, 0};
-    LxRec lx0{0, 0};
+    // glx is staged only when the group's form uses it; otherwise a sentinel
+    // no real record equals, so that any record the tick writes (LXS / SXS
+    // entry, whatever its value) is written back
+    LxRec lx0{-2147483647 - 1, -2147483647 - 1};
     if (valid) {
       m0 = at(P.gmeta, g); r0 = at(P.grot, g); hb0 = at(P.hb, g); ss0 = P.gss[g];
       if (T.iso_p) gi0 = at(P.giso, g);
-      if (m0 & M_LXS) lx0 = P.glx[g];
+      if (uses_glx(m0)) lx0 = P.glx[g];
     }
     smeta[t] = m0; sgrot[t] = r0; sgiso[t] = gi0; shb[t] = hb0; sgss[t] = ss0; sglx[t] = lx0;
     __syncthreads();
@@ -1299,9 +1350,12 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   const int n = int(T.client_entries());
   const int ph = int(T.entries_before(T.tick) & P.kmask);   // global ring phase of this tick's first entry
   bool take = false, pass = false, lxs = false;   // lxs: an LXS tick (the cut-off leader appends alone)
+  bool sxs = false;                             // an SXS tick (the stale leader appends alone, the primary replicates)
   int committed = 0, w_term = 0, w_slot = -1;   // w_slot >= 0: drifted lane, its own segment from that slot
   uint32_t wmask = 0;                           // replicas whose ring column gets this tick's entries
   uint64_t w_vb = 0;
+  int x_slot = -1, x_r = 0;                     // SXS: the stale leader's first slot and its replica
+  uint64_t x_vb = 0;
   uint32_t df = 0;
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
@@ -1313,6 +1367,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     df |= skip ? 1u : 0u;
     if (take) {
       const SsRec s = P.gss[g];
+      const LxRec gx = (RAFT && uses_glx(meta)) ? P.glx[g] : LxRec{0, 0};
       const uint64_t key = group_key(T.seed, P.gbase + g);
       if (T.iso_p) {   // any window over this group this tick (either mode): the list kernel ...
         uint32_t act = 0, starting = 0;
@@ -1322,13 +1377,65 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
           uint32_t gi = act ? uint32_t(at(P.giso, g)) : 0u;
           lxs = T.iso_leader && !starting && leader_iso_mask(act, 0u, gi, 0u, false) == (1u << c);
           take = lxs;
+        } else if (RAFT && !CRC && is_sxs(meta)) {
+          // ... and an SXS group whose windows cut off exactly its stale leader
+          // (leader mode: no window deciding a victim this tick)
+          uint32_t gi = act ? uint32_t(at(P.giso, g)) : 0u;
+          const uint32_t cut = T.iso_leader ? (starting ? 0u : leader_iso_mask(act, 0u, gi, 0u, false)) : im;
+          sxs = cut == (1u << gx.dl);
+          take = sxs;
         } else if (T.iso_leader ? act != 0u : im != 0u) {
           take = false;
         }
-      } else if (meta & M_LXS) {
+      } else if (uses_glx(meta)) {
         take = false;
       }
-      if (RAFT && lxs) {
+      if (RAFT && !CRC && sxs) {
+        // SXS tick (fast_group's stale-leader tick in closed form): the
+        // primary appends its client entries (main.go:327-329) and replicates
+        // them to its R-2 followers, which all accept (same term, prevLogIndex
+        // = their length, log[L].term = T: main.go:121-156 with Raft's rules),
+        // take CommitIndex max(cf, cl) and reset their timers (hb); the
+        // AppendEntries to the stale leader xs is dropped (EXT), and xs — cut
+        // off, still a leader of term T-1 — appends its own client entries to
+        // its own log and every AppendEntries it sends is dropped; its commit
+        // rule cannot move (its MatchIndex row is frozen). Commit
+        // (r_leader_commit): R-1 of R logs at L+n, an entry of the current
+        // term. The followers' entries go in the whole-row stores without
+        // xs's column, or — their logs stood still while the leader was cut
+        // off, so they usually append out of the global phase — as the lane's
+        // own segment without xs's column (no segment switch: xs's entries
+        // above L live in the current segment); xs's own entries (index
+        // L+k+1+e, current segment: k >= 0) go in its column, inside the
+        // common row when xs is in the global phase (it is when it appended
+        // alone in phase, LXS), else at its own slots.
+        const int L = s.last, xs = gx.dl, k = gx.k;
+        const int rot = at(P.grot, g);
+        take = L > 0 && k >= 0 && int64_t(L) + k + n <= I32MAX && n < int(P.K) && s.cl <= L + n &&
+               !(meta & M_HWX);
+        const int wph = (L + rot) & int(P.kmask);
+        if (take && n && wph != ph) {
+          w_slot = wph;
+          df |= 512u;
+        }
+        if (take) {
+          const int nl = L + n;
+          const int cl2 = nl > s.cl ? nl : s.cl;
+          const int cf2 = s.cl > s.cf ? s.cl : s.cf;
+          P.gss[g] = SsRec{nl, s.term, cl2, cf2};   // (glx unchanged: both logs grow by n)
+          at(P.hb, g) = T.now;                       // timer.Reset(d) of every follower
+          committed = cl2 - s.cl;
+          w_term = s.term;
+          w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+          wmask = ((1u << R) - 1u) & ~(1u << xs);
+          x_slot = (L + k + rot) & int(P.kmask);
+          x_r = xs;
+          x_vb = rng_k(key, uint32_t(xs), ST_VALUE, uint64_t(T.tick));
+          df |= (w_slot < 0 ? 256u : 0u) | (1u << 25) | (x_slot == ph ? 1u << 26 : 0u);
+        } else {
+          pass = true;
+        }
+      } else if (RAFT && lxs) {
         // LXS tick (fast_group's isolated-leader tick in closed form): the
         // leader appends its client entries alone (main.go:327-329), every
         // AppendEntries it sends is dropped (EXT), nobody's timer is reset;
@@ -1336,7 +1443,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         // the list kernel's) and the leader's log is in the global ring
         // phase. Commit (r_leader_commit): the majority order statistic is the
         // followers' length L, an entry of the current term (SSYNC).
-        const LxRec x = P.glx[g];
+        const LxRec x = gx;
         const int L = s.last, Lc = L + x.k;
         const int rot = at(P.grot, g);
         take = x.dl > T.now && n < int(P.K) && int64_t(Lc) + n <= I32MAX && (n == 0 || ((Lc + rot) & int(P.kmask)) == ph);
@@ -1458,14 +1565,18 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   }
   // this tick's entries: the taken lanes at the global phase as whole ring
   // rows, all R replicas (the cooperative row stores of fast_group); a
-  // drifted lane its own R-contiguous segment
+  // drifted lane its own R-contiguous segment. SXS: the stale leader's
+  // column carries its own entry (term T-1, its value stream) — in the common
+  // row when it is in the global phase (xrow), else at its own slot (wx).
   bool wr = take && n && w_slot < 0;
   bool wd = take && n && w_slot >= 0;
+  const bool xrow = RAFT && !CRC && take && n && x_slot == ph;
+  const bool wx = RAFT && !CRC && take && n && x_slot >= 0 && !xrow;
   if (P.diag) {   // timing-only diagnostics (wrong results): drifted lanes skip / write the common row
     if (P.diag & 2u) wr |= wd;
     wd = false;
   }
-  if (__ballot(wr || wd)) {
+  if (__ballot(wr || wd || xrow || wx)) {
     const int lane = threadIdx.x & 63;
     const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g), P.KP, R);
     int32_t* const rt = P.log_term + tb;
@@ -1473,14 +1584,16 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
     uint32_t cs = 0;
     if constexpr (CRC) cs = crc_term_state(tab, w_term);
+    const bool anyx = RAFT && !CRC && __ballot(xrow) != 0ull;   // (wave-uniform)
     int k_term[R], k_src[R];
-    bool k_on[R];
+    bool k_on[R], k_x[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int src = (k * 64 + lane) / R, rr = (k * 64 + lane) - src * R;
       k_src[k] = src;
       k_term[k] = __shfl(w_term, src);
       k_on[k] = ((uint32_t(__shfl(int(wr ? wmask : 0u), src)) >> rr) & 1u) != 0u;   // (LXS: the leader's column)
+      k_x[k] = anyx && ((uint32_t(__shfl(xrow ? int(1u << x_r) : 0, src)) >> rr) & 1u) != 0u;
     }
     for (int e = 0; e < n; ++e) {
       const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
@@ -1488,32 +1601,52 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
       const uint32_t row = uint32_t((ph + e) & int(P.kmask)) * 64u * R;
       const int vlo = int(uint32_t(uint64_t(v))), vhi = int(uint32_t(uint64_t(v) >> 32));
+      int64_t xv = 0;
+      if (RAFT && !CRC && x_slot >= 0) xv = int64_t(sm64(x_vb ^ uint64_t(uint32_t(e))) >> 1);
+      const int xlo = int(uint32_t(uint64_t(xv))), xhi = int(uint32_t(uint64_t(xv) >> 32));
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         const int lo = __shfl(vlo, k_src[k]), hi = __shfl(vhi, k_src[k]);
         uint32_t sk = 0;
         if constexpr (CRC) sk = uint32_t(__shfl(int(stamp), k_src[k]));
-        if (k_on[k]) {
+        int xl = 0, xh = 0;
+        if (anyx) { xl = __shfl(xlo, k_src[k]); xh = __shfl(xhi, k_src[k]); }
+        if (k_on[k] || k_x[k]) {
           const uint32_t o = row + uint32_t(k * 64 + lane);
-          at(rt, o) = k_term[k];
-          at(rv, o) = int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
+          at(rt, o) = k_x[k] ? k_term[k] - 1 : k_term[k];
+          at(rv, o) = k_x[k] ? int64_t((uint64_t(uint32_t(xh)) << 32) | uint32_t(xl))
+                             : int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
           if constexpr (CRC) at(rc, o) = sk;
         }
       }
       if (wd) {
         const uint32_t o = ring_in_tile(g, R, uint32_t((w_slot + e) & int(P.kmask)), 0u);
-        fill_seg<R>(rt + o, w_term);
-        fill_seg<R>(rv + o, v);
-        if constexpr (CRC) fill_seg<R>(rc + o, stamp);
+        if (wmask == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
+          fill_seg<R>(rt + o, w_term);
+          fill_seg<R>(rv + o, v);
+          if constexpr (CRC) fill_seg<R>(rc + o, stamp);
+        } else {                         // SXS: every replica but the stale leader
+#pragma unroll
+          for (int p = 0; p < R; ++p) {
+            if (!((wmask >> p) & 1u)) continue;
+            at(rt, o + uint32_t(p)) = w_term;
+            at(rv, o + uint32_t(p)) = v;
+          }
+        }
+      }
+      if (wx) {   // SXS: the stale leader out of the global phase: its own entry in its column
+        const uint32_t o = ring_in_tile(g, R, uint32_t((x_slot + e) & int(P.kmask)), uint32_t(x_r));
+        at(rt, o) = w_term - 1;
+        at(rv, o) = xv;
       }
     }
   }
   if (P.dbg) {   // diagnostics (same class bits as fast_group): lanes, skipped, taken by the lean pass
     df |= (g < P.G) ? 1024u : 0u;
     df |= pass ? 1u << 23 : 0u;
-    if (!take) df &= ~0x780000u;   // the class bits 19-22 count taken ticks only
+    if (!take) df &= ~0x6780000u;   // the class bits 19-22, 25, 26 count taken ticks only
 #pragma unroll 1
-    for (int k = 0; k < 25; ++k) {
+    for (int k = 0; k < 27; ++k) {
       const uint64_t b = __ballot((df >> k) & 1u);
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
     }
@@ -1539,8 +1672,10 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   if (stats) {
     const int t = take ? 1 : 0;
     if constexpr (RAFT) {
-      // (an LXS tick: every AppendEntries of the cut-off leader dropped)
-      const int v[5] = {committed, (take && !lxs) ? R - 1 : 0, (take && lxs) ? R - 1 : 0, t, 0};
+      // (an LXS tick: every AppendEntries of the cut-off leader dropped; an SXS
+      // tick: the one to the stale leader and every one it sends)
+      const int v[5] = {committed, (take && !lxs) ? (sxs ? R - 2 : R - 1) : 0,
+                        (take && lxs) ? R - 1 : ((take && sxs) ? R : 0), t, 0};
       const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
       block_stats<5>(v, idx, stats);
     } else {

@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
     const bool msync = (meta & M_MSYNC) && primary < R;
     const bool ssync = (meta & M_SSYNC) && primary < R;   // compressed state: the gss record
     const SsRec ss = ssync ? P.gss[g] : SsRec{0, 0, 0, 0};
-    const LxRec lx = (ssync && (meta & M_LXS)) ? P.glx[g] : LxRec{0, 0};
+    const LxRec lx = (ssync && uses_glx(meta)) ? P.glx[g] : LxRec{0, 0};
     const int hb = at(P.hb, g);
     int last[R];
 #pragma unroll
@@ -103,8 +103,8 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
       // MSYNC: max(plane, LastApplied) (HWX; the plane is at most LastApplied without it)
       const int hwm = raft ? (msync ? max(at(P.hwm, rix<R>(g, r)), l) : at(P.hwm, rix<R>(g, r))) : l;
       h = dg_mix(h, uint64_t(role) | (uint64_t((x >> 2) & 15u) << 8) | (uint64_t(r) << 16));
-      const int tm = ssync ? ss.term : at(P.term, rix<R>(g, r));
-      const int cm = ssync ? (r == primary ? ss.cl : ss.cf) : at(P.commit, rix<R>(g, r));
+      const int tm = ssync ? ss_term(ss, r, meta, lx) : at(P.term, rix<R>(g, r));
+      const int cm = ssync ? ss_commit(ss, r, primary, meta, lx, at(P.commit, rix<R>(g, r))) : at(P.commit, rix<R>(g, r));
       h = dg_mix(h, lo32(tm) | (lo32(l) << 32));
       h = dg_mix(h, lo32(cm) | (lo32(dl) << 32));
       h = dg_mix(h, lo32(dur) | (lo32(hwm) << 32));
@@ -113,10 +113,11 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
         int m = 0, nx = 0;
         if (role == ROLE_L && p != r) {
           const int lp = sel(last, p);
-          if (r == primary) m = msync ? lp : at(P.lmatch, rix<R>(g, p));
+          const bool mp = msync && msync_peer(meta, lx, p);   // (SXS: the stale leader's row is explicit)
+          if (r == primary) m = mp ? lp : at(P.lmatch, rix<R>(g, p));
           else m = at(prow(P.xmatch, r * R + p, P.Gp), g);
           if (!raft) nx = m + 1;
-          else if (r == primary) nx = msync ? lp + 1 : at(P.lnext, rix<R>(g, p));
+          else if (r == primary) nx = mp ? lp + 1 : at(P.lnext, rix<R>(g, p));
           else nx = at(prow(P.xnext, r * R + p, P.Gp), g);
         }
         h = dg_mix(h, lo32(m) | (lo32(nx) << 32));

@@ -59,11 +59,37 @@ constexpr int M_HWX = 1 << 14;
 // glx[g] = {k, D} with D the earliest follower election deadline (no
 // follower timer moves while the leader is cut off).
 constexpr int M_LXS = 1 << 15;
+// SXS (RAFT; SSYNC + ONESTALE + MSYNC, never LXS): the primary (a new leader)
+// replicates to its followers while the group's one stale leader xs (the
+// previous leader, term T-1, cut off) appends alone. The gss record holds the
+// primary and its followers; glx[g] = {k, xs}: xs's log is k entries longer
+// than theirs, its term and last-entry term are T-1, and its CommitIndex, its
+// high-water mark and the primary's MatchIndex / NextIndex for it stay
+// explicit in the record planes (none of them moves while it is cut off).
 struct __attribute__((aligned(8))) LxRec { int32_t k, dl; };
 struct __attribute__((aligned(16))) SsRec { int32_t last, term, cl, cf; };
-// LastApplied of replica r of an SSYNC group (LXS: the primary is k ahead)
+__device__ __host__ __forceinline__ bool is_sxs(int meta) {
+  return (meta & (M_SSYNC | M_ONESTALE)) == (M_SSYNC | M_ONESTALE);
+}
+// the compressed form keeps something in glx (LXS or SXS)
+__device__ __host__ __forceinline__ bool uses_glx(int meta) { return (meta & M_LXS) || is_sxs(meta); }
+// LastApplied of replica r of an SSYNC group (LXS: the primary is k ahead; SXS: the stale leader)
 __device__ __host__ __forceinline__ int32_t ss_last(const SsRec& s, int r, int primary, int meta, const LxRec& x) {
-  return s.last + ((meta & M_LXS) && r == primary ? x.k : 0);
+  return s.last + ((((meta & M_LXS) && r == primary) || (is_sxs(meta) && r == x.dl)) ? x.k : 0);
+}
+// Term (= term of the last entry) of replica r of an SSYNC group
+__device__ __host__ __forceinline__ int32_t ss_term(const SsRec& s, int r, int meta, const LxRec& x) {
+  return s.term - ((is_sxs(meta) && r == x.dl) ? 1 : 0);
+}
+// CommitIndex of replica r of an SSYNC group; `plane`: the commit plane's value (SXS's stale leader)
+__device__ __host__ __forceinline__ int32_t ss_commit(const SsRec& s, int r, int primary, int meta, const LxRec& x,
+                                                      int32_t plane) {
+  return r == primary ? s.cl : ((is_sxs(meta) && r == x.dl) ? plane : s.cf);
+}
+// MSYNC: the primary's MatchIndex (NextIndex) for peer p is implicit = LastApplied (+1),
+// except for SXS's stale leader, whose row stays explicit
+__device__ __host__ __forceinline__ bool msync_peer(int meta, const LxRec& x, int p) {
+  return (meta & M_MSYNC) && !(is_sxs(meta) && p == x.dl);
 }
 constexpr int HB_NONE = -2147483647 - 1;
 constexpr int I32MAX = 2147483647;
@@ -481,27 +507,32 @@ struct Group {
     for (int r = 0; r < R; ++r) dl[r] = with_deadlines ? eff_start(at(P.tstart, rix<R>(g, r)), r) + dur[r] : 0;
     known = with_deadlines ? (1u << R) - 1u : 0u;
     // materialise the compressed state of an SSYNC group (written back by store)
+    const LxRec x = (uses_glx(meta0) && primary < R) ? P.glx[g] : LxRec{0, 0};
     if ((meta0 & M_SSYNC) && primary < R) {
       const SsRec s = P.gss[g];
-      const LxRec x = (meta0 & M_LXS) ? P.glx[g] : LxRec{0, 0};
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        term[r] = s.term; last[r] = ss_last(s, r, primary, meta0, x); commit[r] = r == primary ? s.cl : s.cf;
-        ltm[r] = s.term;
+        term[r] = ss_term(s, r, meta0, x); last[r] = ss_last(s, r, primary, meta0, x);
+        commit[r] = ss_commit(s, r, primary, meta0, x, commit[r]);
+        ltm[r] = ss_term(s, r, meta0, x);
       }
       d_term = d_last = d_commit = d_lt = (1u << R) - 1u;
     }
     // materialise the rows the fast kernel kept implicit: MatchIndex = LastApplied
     // (RAFT also NextIndex = LastApplied+1 and high-water mark = LastApplied)
     if ((meta0 & M_MSYNC) && primary < R) {
-      const uint32_t peers = ((1u << R) - 1u) & ~(1u << primary);
+      uint32_t peers = ((1u << R) - 1u) & ~(1u << primary);
+      if (is_sxs(meta0)) peers &= ~(1u << x.dl);   // (SXS: the stale leader's row is explicit)
       rows_m = 1; d_pm = peers;
       if constexpr (SEM == SEM_RAFT) { rows_n = 1; d_pn = peers; }
 #pragma unroll
       for (int p = 0; p < R; ++p) {
-        if (p != primary) {
+        if ((peers >> p) & 1u) {
           pm[p] = last[p];
           if constexpr (SEM == SEM_RAFT) pn[p] = last[p] + 1;
+        } else if (p != primary) {   // explicit row (rows_m: pm holds every row)
+          pm[p] = at(P.lmatch, rix<R>(g, p));
+          if constexpr (SEM == SEM_RAFT) pn[p] = at(P.lnext, rix<R>(g, p));
         }
         if constexpr (SEM == SEM_RAFT) {   // max(plane, LastApplied) (HWX)
           if (hw[p] < last[p]) { hw[p] = last[p]; d_hw |= 1u << p; }

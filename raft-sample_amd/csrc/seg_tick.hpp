@@ -144,22 +144,24 @@ struct Seg {
     const int ts = at(P.tstart, ri);
     pm = 0; pn = 0;
     const bool peer_of_pri = primary < R && me != primary;
-    if (peer_of_pri && !(meta0 & M_MSYNC)) {
+    const LxRec gx = (uses_glx(meta0) && primary < R) ? P.glx[g] : LxRec{0, 0};
+    const bool mrow = msync_peer(meta0, gx, me);   // this lane's MatchIndex row implicit (MSYNC)
+    if (peer_of_pri && !mrow) {
       pm = at(P.lmatch, ri);
       if constexpr (SEM == SEM_RAFT) pn = at(P.lnext, ri);
     }
     dl = (role == ROLE_L ? ts : max(ts, hbt)) + dur;   // effective timer start counts the heartbeat
     if ((meta0 & M_SSYNC) && primary < R && act) {     // compressed state (Group::load)
       const SsRec s = P.gss[g];
-      const LxRec x = (meta0 & M_LXS) ? P.glx[g] : LxRec{0, 0};
-      term = s.term; last = ss_last(s, me, primary, meta0, x); commit = me == primary ? s.cl : s.cf; ltm = s.term;
+      term = ss_term(s, me, meta0, gx); last = ss_last(s, me, primary, meta0, gx);
+      commit = ss_commit(s, me, primary, meta0, gx, commit); ltm = ss_term(s, me, meta0, gx);
       dirty |= SD_TERM | SD_LAST | SD_COMMIT | SD_LT;
     }
     if (!act) { role = ROLE_F; dl = I32MAX; last = 0; hw = 0; }
     // rows the fast kernel kept implicit (MSYNC): MatchIndex = LastApplied
     // (RAFT also NextIndex = LastApplied+1, high-water mark = LastApplied)
     if ((meta0 & M_MSYNC) && primary < R && act) {
-      if (me != primary) {
+      if (me != primary && mrow) {
         pm = last;
         dirty |= SD_PM;
         if constexpr (SEM == SEM_RAFT) { pn = last + 1; dirty |= SD_PN; }

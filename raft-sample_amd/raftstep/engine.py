@@ -226,6 +226,14 @@ class Engine:
         _check(self.lib.raft_diag_read(self.h, buf, abi.DIAG_COUNTERS))
         return {k: int(buf[i]) for k, i in abi.DIAG.items()}
 
+    def debug_group_words(self, group):
+        """Raw per-group words (gmeta, giso, hb, gss[4], glx[2], grot, grota, gsb, grotb, gsb2)."""
+        buf = (C.c_int32 * 14)()
+        _check(self.lib.raft_debug_group_words(self.h, int(group), buf, 14))
+        names = ("meta", "giso", "hb", "ss_last", "ss_term", "ss_cl", "ss_cf", "lx_k", "lx_dl", "rot", "rota", "sb",
+                 "rotb", "sb2")
+        return dict(zip(names, list(buf)))
+
     def debug_force_pass(self, group):
         """Test knob: the lean kernel passes `group` (-1: none) to the list kernel."""
         _check(self.lib.raft_debug_force_pass(self.h, int(group)))

@@ -102,7 +102,8 @@ def test_c4_as_benchmarked_full_size():
     assert t == wl["settle"] + 5 + 300
     assert total[6] == 0, "no group may fault in RAFT mode"
     # the churn really happened at full size (every class of the C4 tick)
-    for k in ("list_election", "list_first_round", "list_return", "list_stale", "lean_lxs", "list_window_start"):
+    for k in ("list_election", "list_first_round", "list_return", "list_stale", "lean_lxs", "list_window_start",
+              "lean_sxs", "list_sxs_entered"):
         assert cls[k] > 10000, (k, cls)
 
 
@@ -170,7 +171,8 @@ def test_class_coverage_c4_config_full_oracle():
     print("class counters:", cls)
     need = ["lean_ssync", "lean_lxs", "lean_lxs_whole_row", "lean_switch", "lean_three_seg", "lean_hwx",
             "list_quiet", "list_isolated_leader", "list_election", "list_first_round", "list_return",
-            "list_return_trunc", "list_stale", "list_hwx", "list_window_start", "list_switch"]
+            "list_return_trunc", "list_stale", "list_hwx", "list_window_start", "list_switch", "lean_sxs",
+            "lean_sxs_stale_in_row", "list_sxs_entered", "list_sxs_materialised"]
     low = {k: cls[k] for k in need if cls[k] < MIN_TAKEN}
     assert not low, f"classes taken fewer than {MIN_TAKEN} times: {low}\nall: {cls}"
 
