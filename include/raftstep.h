@@ -345,6 +345,7 @@ enum raft_diag_counter {
   RAFT_DIAG_LIST_WINDOW_START = 60,   /* a leader-isolation window decided on the fast path */
   RAFT_DIAG_LIST_SXS_MATERIALISED = 61,/* SXS groups taken by the full body (explicit form rebuilt) */
   RAFT_DIAG_LIST_SXS_ENTERED = 62,    /* ticks ending in the SXS compressed form */
+  RAFT_DIAG_LIST_STALE_MOVED = 63,    /* segment switch that moved a stale leader's entries (placement only) */
   /* host counters since the last read */
   RAFT_DIAG_TICKS = 64,
   RAFT_DIAG_TICKS_LIST_SKIPPED = 65,  /* ticks run by the lean kernel alone (steady-state list skip) */

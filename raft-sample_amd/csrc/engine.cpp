@@ -185,6 +185,7 @@ Trace make_trace(const raft_engine* e, int64_t tick) {
   T.iso_p = e->cfg.isolate_per_65536;
   T.iso_min = e->cfg.isolate_min_ticks;
   T.iso_span = e->cfg.isolate_max_ticks - e->cfg.isolate_min_ticks + 1;
+  udiv_magic_of(T.iso_span, &T.iso_m, &T.iso_l);
   T.iso_leader = e->cfg.isolate_leader;
   T.secs = e->cfg.tick_seconds;
   T.period = e->cfg.client_period;

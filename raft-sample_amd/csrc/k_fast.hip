@@ -245,6 +245,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   int w_term = 0, w_ph = 0;    // their term and the ring slot of the first entry
   uint64_t w_vb = 0;    // value stream base of this tick's entries
   int cp_n = 0, cp_from = 0, cp_sb = 0, cp_sb2 = 0;   // RAFT: a returning stale leader's catch-up copy (ring writes)
+  int mv_n = 0, mv_d = 0, mv_rot = 0, mv_col = 0, mv_from = 0;   // RAFT: a stale leader's entries above a segment switch (moved)
   uint32_t cp_cs = 0, cp_rot = 0, cp_rotb = 0;
   uint32_t df = 0;      // diagnostics: lane class bits (P.dbg)
   bool stored = false;  // the group's rows may have been written (returned)
@@ -726,15 +727,19 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     }
     if (gom && !bail) {
       int cm = Lc;
-      bool sync = !stale && sr < 0;   // ONESTALE: the stale leader's row is explicit; a returning one's hwm too
+      // (ONESTALE: the stale leader's row is explicit. A returning one is in
+      // step after this tick — MatchIndex = its new length — and its
+      // high-water mark, above its truncated log, goes in the plane: HWX)
+      bool sync = !stale;
       bool hwx = false;               // RAFT: MSYNC with a high-water mark above its log's length (M_HWX)
       if constexpr (RAFT) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          if (!((hwup >> r) & 1u)) continue;
+          if (!((hwup >> r) & 1u) || r == sr) continue;
           const int la = r == c ? Ll + n : last[r];   // (accepting followers' last already moved)
           if (RW.at(PL_HWM, r) > la) hwx = true;      // the plane holds it (exact: rows were explicit or HWX)
         }
+        if (sr >= 0 && sr_hw > Ll + n) hwx = true;    // the returning stale leader's truncated log
       }
       if constexpr (RAFT) {
         // every log now ends at Ll+n (all but at most one lagging isolated
@@ -779,6 +784,10 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         df |= 262144u;
         GW.ss() = SsRec{Ll + n, Lt, cm, cf};
         GW.template st_hb<WT>(T.now);                                   // timer.Reset(d) of every follower
+        if (RAFT && sr >= 0) {   // the returning stale leader stepped down: a follower (term, length: the record)
+          RW.template st<WT>(PL_RS, sr, int32_t(ROLE_F | (uint32_t(sr_dur) << 6)));   // votedFor none, new timer
+          RW.template st<WT>(PL_HWM, sr, sr_hw);   // (its timer starts now: hb)
+        }
       } else {
       if (ss) {   // leaving the compressed form: the rows as they stood, then the element stores below
         const SsRec ss_rec = GW.ss();   // (re-read: rare, keeps it out of the live registers)
@@ -921,22 +930,38 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           const int ph = int(T.entries_before(T.tick) & P.kmask);
           const uint32_t d = uint32_t(ph - w_ph) & P.kmask;
           if (d != 0u) df |= d <= P.K ? 8u : 16u;
-          // (not with a stale leader appending elsewhere in the ring this tick)
-          if (P.KP > P.K && d != 0u && d <= P.K && Ll > 0 && !stale && sr < 0) {
+          // A stale leader cut off this tick (RAFT, typically the new leader's
+          // first round: the followers' logs stood still while the old leader
+          // appended alone in the global phase) holds entries above Ll: they
+          // are moved to the new segment's slots (placement only) by the wave
+          // below, so that the primary and its followers append in the global
+          // phase from now on (whole ring rows) and the stale leader alone
+          // writes out of phase.
+          if (P.KP > P.K && d != 0u && d <= P.K && Ll > 0 && sr < 0) {
             int lo = Ll, hi = Ll;   // log lengths before this tick (== high-water marks on this path)
 #pragma unroll
             for (int p = 0; p < R; ++p) {
               const int pre = (p != c && ((okm >> p) & 1u)) ? last[p] - n : last[p];
               lo = min(lo, pre);
-              hi = max(hi, pre);
+              if (!(stale && p == xi)) hi = max(hi, pre);
             }
+            const int xtop = stale ? sel(last, xi) + n : 0;   // the stale leader's length after this tick
             const int sbo = GW.sb();
             const uint32_t rota = GW.rota();
-            const bool ok = ring_switch_ok(d, uint32_t(rot), rota, sbo, GW.sb2(), lo, P.K, P.kmask);
+            const bool ok = ring_switch_ok(d, uint32_t(rot), rota, sbo, GW.sb2(), lo, P.K, P.kmask) &&
+                            xtop - Ll <= int(P.K);
             df |= hi > Ll ? 64u : 0u;
             df |= ok ? 0u : 128u;
             if (hi <= Ll && ok) {
               df |= 32u | ((sbo <= 1 || sbo <= lo - int(P.K) + 1) ? 0u : 1u << 25);   // (+ the previous segment stays live)
+              if (stale && xtop > Ll) {   // the stale leader's entries Ll+1..xtop: slot (i-1+rot) -> (i-1+rot+d)
+                mv_n = xtop - Ll;
+                mv_from = Ll + 1;
+                mv_d = int(d);
+                mv_rot = rot;
+                mv_col = xi;
+                df |= 1u << 31;
+              }
               GW.rotb() = uint16_t(rota);   // the three segments shift
               GW.sb2() = sbo;
               GW.rota() = uint16_t(rot);
@@ -1037,6 +1062,72 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         const int64_t v = at(P.log_value + tb, o + cc);
         st<WT>(P.log_term + tb, o + ss, t);
         st<WT>(P.log_value + tb, o + ss, v);
+      }
+    }
+    // a stale leader's entries above a segment switch (see the switch): entry
+    // i goes from slot (i-1+rot) to (i-1+rot+d). The wave packs whole groups
+    // into steps of 64 entries (one entry per lane); a step's loads all
+    // complete before its stores, so overlapping source and destination slots
+    // of one group are safe. (A group with more than 64 entries goes alone,
+    // 64 per step from the top down: entry i's destination is the source of
+    // entry i+d, moved in an earlier step.) The fence makes the entries the
+    // stale leader's lane stored this tick visible to the other lanes.
+    uint64_t mpend = __ballot(mv_n > 0);
+    if (mpend) {
+      __threadfence_block();
+      while (mpend) {
+        int src = -1, i = 0, top = 0;
+        const int s0 = int(__builtin_ctzll(mpend));
+        const int c0 = __builtin_amdgcn_readlane(mv_n, s0);
+        if (c0 > 64) {   // alone, from the top down
+          mpend &= mpend - 1ull;
+          const int from = __builtin_amdgcn_readlane(mv_from, s0);
+          for (top = from + c0 - 1; top >= from; top -= 64) {
+            i = top - lane;
+            if (i >= from) src = s0;
+            const uint32_t gg = uint32_t(__builtin_amdgcn_readlane(int(g), s0));
+            const int dd = __builtin_amdgcn_readlane(mv_d, s0), rr = __builtin_amdgcn_readlane(mv_rot, s0);
+            const uint32_t col = uint32_t(__builtin_amdgcn_readlane(mv_col, s0));
+            const uint64_t tb = ring_tile(gg, P.KP, R);
+            const uint32_t o0 = ring_in_tile(gg, R, uint32_t(i - 1 + rr) & P.kmask, col);
+            const uint32_t o1 = ring_in_tile(gg, R, uint32_t(i - 1 + rr + dd) & P.kmask, col);
+            if (i >= from) {
+              const int32_t t = at(P.log_term + tb, o0);
+              const int64_t v = at(P.log_value + tb, o0);
+              uint32_t cr = 0;
+              if constexpr (CRC) cr = at(P.log_crc + tb, o0);
+              st<WT>(P.log_term + tb, o1, t);
+              st<WT>(P.log_value + tb, o1, v);
+              if constexpr (CRC) st<WT>(P.log_crc + tb, o1, cr);
+            }
+          }
+          continue;
+        }
+        int off = 0;
+        while (mpend) {   // pack groups while their entries fit the step
+          const int sl = int(__builtin_ctzll(mpend));
+          const int cnt = __builtin_amdgcn_readlane(mv_n, sl);
+          if (cnt > 64 || off + cnt > 64) break;
+          if (lane >= off && lane < off + cnt) { src = sl; i = lane - off; }
+          off += cnt;
+          mpend &= mpend - 1ull;
+        }
+        const int ss_ = src < 0 ? lane : src;
+        const int from = __shfl(mv_from, ss_), dd = __shfl(mv_d, ss_), rr = __shfl(mv_rot, ss_);
+        const uint32_t col = uint32_t(__shfl(mv_col, ss_)), gg = uint32_t(__shfl(int(g), ss_));
+        if (src >= 0) {
+          const int idx = from + i;
+          const uint64_t tb = ring_tile(gg, P.KP, R);
+          const uint32_t o0 = ring_in_tile(gg, R, uint32_t(idx - 1 + rr) & P.kmask, col);
+          const uint32_t o1 = ring_in_tile(gg, R, uint32_t(idx - 1 + rr + dd) & P.kmask, col);
+          const int32_t t = at(P.log_term + tb, o0);
+          const int64_t v = at(P.log_value + tb, o0);
+          uint32_t cr = 0;
+          if constexpr (CRC) cr = at(P.log_crc + tb, o0);
+          st<WT>(P.log_term + tb, o1, t);
+          st<WT>(P.log_value + tb, o1, v);
+          if constexpr (CRC) st<WT>(P.log_crc + tb, o1, cr);
+        }
       }
     }
   }
@@ -1390,7 +1481,41 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       } else if (uses_glx(meta)) {
         take = false;
       }
-      if (RAFT && !CRC && sxs) {
+      // The three classes below differ only in their conditions and in the
+      // record they store; the value stream of the writing leader, the record
+      // and timer stores and the ring writes are shared (one copy of each per
+      // wave, whatever mix of classes its lanes hold).
+      const int L = s.last;
+      const int rot = at(P.grot, g);
+      // (the value stream of this tick's entries: the primary's, the only
+      // appending leader but SXS's stale one, whose stream follows below)
+      const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+      int nl = L, cl2 = s.cl, cf2 = s.cf;   // the record after this tick
+      bool hbw = false;                     // every follower's timer reset (hb = now)
+      int hwx_clear = 0;                    // RAFT HWX: a truncated log in step (high-water marks in the hwm plane)
+      int sbo = 0, sw_d = 0, sw_rota = -1;  // a ring segment switch (normal class)
+      if (RAFT && lxs) {
+        // LXS tick (fast_group's isolated-leader tick in closed form): the
+        // leader appends its client entries alone (main.go:327-329), every
+        // AppendEntries it sends is dropped (EXT), nobody's timer is reset;
+        // taken while no follower's election deadline is due (an election is
+        // the list kernel's) and the leader's log is in the global ring
+        // phase. Commit (r_leader_commit): the majority order statistic is the
+        // followers' length L, an entry of the current term (SSYNC).
+        const int Lc = L + gx.k;
+        take = gx.dl > T.now && n < int(P.K) && int64_t(Lc) + n <= I32MAX && (n == 0 || ((Lc + rot) & int(P.kmask)) == ph);
+        cl2 = L > s.cl ? L : s.cl;
+        // The whole row, not only the leader's column, when every
+        // follower's slot there is dead: with KP = 2K slots, all of a
+        // follower's live entries (L-K, L] in the current segment (gsb at
+        // most L-K+1, no segment gap) and the lead k+n at most K, the slot
+        // of leader index L+k+e last held follower index L+k+e-2K <= L-K;
+        // the follower rewrites it before its log reaches it. No partial
+        // lines then; otherwise the leader's column alone.
+        const bool whole = take && P.KP >= 2u * P.K && gx.k + n <= int(P.K) && at(P.gsb, g) <= L - int(P.K) + 1;
+        wmask = whole ? (1u << R) - 1u : (1u << c);
+        df |= take ? (131072u | 256u | (1u << 19) | (whole ? 1u << 21 : 0u)) : 0u;
+      } else if (RAFT && !CRC && sxs) {
         // SXS tick (fast_group's stale-leader tick in closed form): the
         // primary appends its client entries (main.go:327-329) and replicates
         // them to its R-2 followers, which all accept (same term, prevLogIndex
@@ -1402,165 +1527,115 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         // rule cannot move (its MatchIndex row is frozen). Commit
         // (r_leader_commit): R-1 of R logs at L+n, an entry of the current
         // term. The followers' entries go in the whole-row stores without
-        // xs's column, or — their logs stood still while the leader was cut
-        // off, so they usually append out of the global phase — as the lane's
-        // own segment without xs's column (no segment switch: xs's entries
-        // above L live in the current segment); xs's own entries (index
-        // L+k+1+e, current segment: k >= 0) go in its column, inside the
-        // common row when xs is in the global phase (it is when it appended
-        // alone in phase, LXS), else at its own slots.
-        const int L = s.last, xs = gx.dl, k = gx.k;
-        const int rot = at(P.grot, g);
-        take = L > 0 && k >= 0 && int64_t(L) + k + n <= I32MAX && n < int(P.K) && s.cl <= L + n &&
-               !(meta & M_HWX);
+        // xs's column, or as the lane's own segment without it when they
+        // append out of the global phase (no segment switch here: xs's
+        // entries above L live in the current segment); xs's own entries
+        // (index L+k+1+e, current segment: k >= 0) go in its column, inside
+        // the common row when xs is in the global phase, else at its own slots.
+        const int xs = gx.dl, k = gx.k;
+        take = L > 0 && k >= 0 && int64_t(L) + k + n <= I32MAX && n < int(P.K) && s.cl <= L + n && !(meta & M_HWX);
+        nl = L + n;
+        cl2 = nl > s.cl ? nl : s.cl;
+        cf2 = s.cl > s.cf ? s.cl : s.cf;
+        hbw = true;
+        const int wph = (L + rot) & int(P.kmask);
+        if (take && n && wph != ph) w_slot = wph;
+        wmask = ((1u << R) - 1u) & ~(1u << xs);
+        x_slot = take ? (L + k + rot) & int(P.kmask) : -1;
+        x_r = xs;
+        df |= take ? ((w_slot < 0 ? 256u : 512u) | (1u << 25) | (x_slot == ph ? 1u << 26 : 0u)) : 0u;
+      } else {
+        // (the followers' CommitIndex min(LeaderCommit, last new entry) is the
+        // leader's only while that is at most L+n: a leader's CommitIndex above
+        // its log, left by a truncation, goes to the list kernel)
+        take &= L > 0 && int64_t(L) + n <= I32MAX && n < int(P.K) && s.cl <= L + n;
+        if (RAFT && take && (meta & M_HWX)) {
+          // every AppendEntries' prevLogIndex (L) and NextIndex (L+1) must stay
+          // inside the ring window of every log: max hwm < L+K (r_deliver_ae /
+          // r_leader_round's evicted rules); the flag clears once every log has
+          // grown to its mark (the marks are then LastApplied again)
+          int hw[R];
+          load_row_p<R>(&at(P.hwm, rix<R>(g, 0)), hw);
+          int mx = hw[0];
+#pragma unroll
+          for (int r = 1; r < R; ++r) mx = max(mx, hw[r]);
+          take &= mx - L < int(P.K);
+          hwx_clear = mx <= L + n ? 1 : 0;
+        }
+        // ring phase: a group whose logs stood still under churn appends out of
+        // the global phase (drifted); it switches its ring segment in place
+        // when that is safe (ring_slot; as fast_group), else writes its own
+        // R-contiguous segment at its own slot
+        sbo = P.KP > P.K ? at(P.gsb, g) : 0;   // (loaded with the rest: no dependent round trip for drifted lanes)
         const int wph = (L + rot) & int(P.kmask);
         if (take && n && wph != ph) {
-          w_slot = wph;
-          df |= 512u;
-        }
-        if (take) {
-          const int nl = L + n;
-          const int cl2 = nl > s.cl ? nl : s.cl;
-          const int cf2 = s.cl > s.cf ? s.cl : s.cf;
-          P.gss[g] = SsRec{nl, s.term, cl2, cf2};   // (glx unchanged: both logs grow by n)
-          at(P.hb, g) = T.now;                       // timer.Reset(d) of every follower
-          committed = cl2 - s.cl;
-          w_term = s.term;
-          w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
-          wmask = ((1u << R) - 1u) & ~(1u << xs);
-          x_slot = (L + k + rot) & int(P.kmask);
-          x_r = xs;
-          x_vb = rng_k(key, uint32_t(xs), ST_VALUE, uint64_t(T.tick));
-          df |= (w_slot < 0 ? 256u : 0u) | (1u << 25) | (x_slot == ph ? 1u << 26 : 0u);
-        } else {
-          pass = true;
-        }
-      } else if (RAFT && lxs) {
-        // LXS tick (fast_group's isolated-leader tick in closed form): the
-        // leader appends its client entries alone (main.go:327-329), every
-        // AppendEntries it sends is dropped (EXT), nobody's timer is reset;
-        // taken while no follower's election deadline is due (an election is
-        // the list kernel's) and the leader's log is in the global ring
-        // phase. Commit (r_leader_commit): the majority order statistic is the
-        // followers' length L, an entry of the current term (SSYNC).
-        const LxRec x = gx;
-        const int L = s.last, Lc = L + x.k;
-        const int rot = at(P.grot, g);
-        take = x.dl > T.now && n < int(P.K) && int64_t(Lc) + n <= I32MAX && (n == 0 || ((Lc + rot) & int(P.kmask)) == ph);
-        if (take) {
-          const int cl2 = L > s.cl ? L : s.cl;
-          if (cl2 != s.cl) P.gss[g] = SsRec{L, s.term, cl2, s.cf};
-          P.glx[g] = LxRec{x.k + n, x.dl};
-          committed = cl2 - s.cl;
-          w_term = s.term;
-          w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
-          // The whole row, not only the leader's column, when every
-          // follower's slot there is dead: with KP = 2K slots, all of a
-          // follower's live entries (L-K, L] in the current segment (gsb at
-          // most L-K+1, no segment gap) and the lead k+n at most K, the slot
-          // of leader index L+k+e last held follower index L+k+e-2K <= L-K;
-          // the follower rewrites it before its log reaches it. No partial
-          // lines then; otherwise the leader's column alone.
-          const bool whole = P.KP >= 2u * P.K && x.k + n <= int(P.K) && at(P.gsb, g) <= L - int(P.K) + 1;
-          wmask = whole ? (1u << R) - 1u : (1u << c);
-          df |= 131072u | 256u | (1u << 19) | (whole ? 1u << 21 : 0u);
-        } else {
-          pass = true;
-        }
-      } else {
-      const int L = s.last;
-      // (the followers' CommitIndex min(LeaderCommit, last new entry) is the
-      // leader's only while that is at most L+n: a leader's CommitIndex above
-      // its log, left by a truncation, goes to the list kernel)
-      take &= L > 0 && int64_t(L) + n <= I32MAX && n < int(P.K) && s.cl <= L + n;
-      int hwx_clear = 0;   // RAFT HWX: a truncated log in step (high-water marks in the hwm plane)
-      if (RAFT && take && (meta & M_HWX)) {
-        // every AppendEntries' prevLogIndex (L) and NextIndex (L+1) must stay
-        // inside the ring window of every log: max hwm < L+K (r_deliver_ae /
-        // r_leader_round's evicted rules); the flag clears once every log has
-        // grown to its mark (the marks are then LastApplied again)
-        int hw[R];
-        load_row_p<R>(&at(P.hwm, rix<R>(g, 0)), hw);
-        int mx = hw[0];
-#pragma unroll
-        for (int r = 1; r < R; ++r) mx = max(mx, hw[r]);
-        take &= mx - L < int(P.K);
-        hwx_clear = mx <= L + n ? 1 : 0;
-      }
-      // ring phase: a group whose logs stood still under churn appends out of
-      // the global phase (drifted); it switches its ring segment in place
-      // when that is safe (ring_slot; as fast_group), else writes its own
-      // R-contiguous segment at its own slot
-      const int rot = at(P.grot, g);
-      const int sbo = P.KP > P.K ? at(P.gsb, g) : 0;   // (loaded with the rest: no dependent round trip for drifted lanes)
-      const int wph = (L + rot) & int(P.kmask);
-      int sw_d = 0;   // segment switch by this rotation jump (placement only, stored once the lane is taken)
-      int sw_rota = -1;   // the previous segment's rotation when it stays live (a third segment)
-      if (take && n && wph != ph) {
-        const uint32_t d = uint32_t(ph - wph) & P.kmask;
-        df |= d <= P.K ? 8u : 16u;
-        bool sw = false;
-        if (P.KP > P.K && d <= P.K) {
-          sw = sbo <= 1 || sbo <= L - int(P.K) + 1;   // the previous segment holds no readable entry
-          if (!sw) {   // it does: the segments shift when the oldest is dead and both jumps fit (ring_switch_ok)
-            const uint32_t rota = at(P.grota, g);
-            sw = ring_switch_ok(d, uint32_t(rot), rota, sbo, at(P.gsb2, g), L, P.K, P.kmask);
-            sw_rota = int(rota);
-            df |= sw ? 1u << 20 : 0u;   // class: a switch while the previous segment stays live (three segments)
-          }
-        }
-        if (sw) sw_d = int(d);
-        else w_slot = wph;
-      }
-      const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
-      if constexpr (CRC) {   // EXT: every follower verifies the stamp of each entry it received
-        if (take && n) {
-          uint32_t cm = 0;   // followers whose message is corrupted this tick: the list kernel (rejection)
-#pragma unroll
-          for (int p = 0; p < R; ++p)
-            if (p != c && P.corrupt_p && (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(T.tick)) & 0xFFFF) < P.corrupt_p)
-              cm |= 1u << p;
-          uint32_t bad = 0;   // (as fast_group: each follower checks the copy it received)
-          const uint32_t cs = crc_term_state(tab, s.term);
-          for (int e = 0; e < n; ++e) {
-            const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
-            const uint32_t stamp = crc_value_final(tab, cs, v);   // leader's stamp
-#pragma unroll
-            for (int p = 0; p < R; ++p) {
-              if (p == c) continue;
-              const int64_t rv = v ^ ((((cm >> p) & 1u) && e == n - 1) ? 1 : 0);   // what p received
-              if (crc_value_final(tab, cs, rv) != stamp) bad |= 1u << p;
+          const uint32_t d = uint32_t(ph - wph) & P.kmask;
+          df |= d <= P.K ? 8u : 16u;
+          bool sw = false;
+          if (P.KP > P.K && d <= P.K) {
+            sw = sbo <= 1 || sbo <= L - int(P.K) + 1;   // the previous segment holds no readable entry
+            if (!sw) {   // it does: the segments shift when the oldest is dead and both jumps fit (ring_switch_ok)
+              const uint32_t rota = at(P.grota, g);
+              sw = ring_switch_ok(d, uint32_t(rot), rota, sbo, at(P.gsb2, g), L, P.K, P.kmask);
+              sw_rota = int(rota);
+              df |= sw ? 1u << 20 : 0u;   // class: a switch while the previous segment stays live (three segments)
             }
           }
-          take &= bad == 0u;
+          if (sw) sw_d = int(d);
+          else w_slot = wph;
         }
+        if constexpr (CRC) {   // EXT: every follower verifies the stamp of each entry it received
+          if (take && n) {
+            uint32_t cm = 0;   // followers whose message is corrupted this tick: the list kernel (rejection)
+#pragma unroll
+            for (int p = 0; p < R; ++p)
+              if (p != c && P.corrupt_p && (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(T.tick)) & 0xFFFF) < P.corrupt_p)
+                cm |= 1u << p;
+            uint32_t bad = 0;   // (as fast_group: each follower checks the copy it received)
+            const uint32_t cs = crc_term_state(tab, s.term);
+            for (int e = 0; e < n; ++e) {
+              const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+              const uint32_t stamp = crc_value_final(tab, cs, v);   // leader's stamp
+#pragma unroll
+              for (int p = 0; p < R; ++p) {
+                if (p == c) continue;
+                const int64_t rv = v ^ ((((cm >> p) & 1u) && e == n - 1) ? 1 : 0);   // what p received
+                if (crc_value_final(tab, cs, rv) != stamp) bad |= 1u << p;
+              }
+            }
+            take &= bad == 0u;
+          }
+        }
+        nl = L + n;
+        if (RAFT ? nl > s.cl : (2 * (R - 1) > R && nl > s.cl)) cl2 = nl;
+        cf2 = s.cl > s.cf ? s.cl : s.cf;
+        hbw = true;
+        wmask = (1u << R) - 1u;
+        df |= take ? (262144u | (w_slot < 0 ? 256u : 512u) | ((RAFT && (meta & M_HWX)) ? 1u << 22 : 0u) |
+                      (sw_d ? 32u : 0u))
+                   : 0u;
       }
       if (take) {
-        const int nl = L + n;
-        int cl2 = s.cl;
-        if (RAFT ? nl > s.cl : (2 * (R - 1) > R && nl > s.cl)) cl2 = nl;
-        const int cf2 = s.cl > s.cf ? s.cl : s.cf;
-        P.gss[g] = SsRec{nl, s.term, cl2, cf2};
-        at(P.hb, g) = T.now;                               // timer.Reset(d) of every follower
+        if (nl != L || cl2 != s.cl || cf2 != s.cf) P.gss[g] = SsRec{nl, s.term, cl2, cf2};
+        if (hbw) at(P.hb, g) = T.now;                   // timer.Reset(d) of every follower
+        if (RAFT && lxs) P.glx[g] = LxRec{gx.k + n, gx.dl};   // (SXS: unchanged, both logs grow by n)
         if (hwx_clear) at(P.gmeta, g) = uint16_t(meta & ~M_HWX);
-        if (RAFT && (meta & M_HWX)) df |= 1u << 22;   // class: a truncated log in step (HWX)
         if (sw_d) {   // the new segment starts at this tick's first entry
           if (sw_rota >= 0) at(P.grotb, g) = uint16_t(sw_rota);   // (else the older segments are dead)
           at(P.gsb2, g) = sbo;
           at(P.grota, g) = uint16_t(rot);
           at(P.gsb, g) = L + 1;
           at(P.grot, g) = uint16_t((rot + sw_d) & int(P.kmask));
-          df |= 32u;
         }
         committed = cl2 - s.cl;
         w_term = s.term;
         w_vb = vb;
-        wmask = (1u << R) - 1u;
-        df |= 262144u | (w_slot < 0 ? 256u : 512u);
+        if (RAFT && !CRC && sxs) x_vb = rng_k(key, uint32_t(x_r), ST_VALUE, uint64_t(T.tick));
       } else {
         pass = true;
+        w_slot = -1;
+        x_slot = -1;
       }
-      }   // !lxs
     }
   }
   // this tick's entries: the taken lanes at the global phase as whole ring
@@ -1571,10 +1646,14 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   bool wr = take && n && w_slot < 0;
   bool wd = take && n && w_slot >= 0;
   const bool xrow = RAFT && !CRC && take && n && x_slot == ph;
-  const bool wx = RAFT && !CRC && take && n && x_slot >= 0 && !xrow;
-  if (P.diag) {   // timing-only diagnostics (wrong results): drifted lanes skip / write the common row
+  bool wx = RAFT && !CRC && take && n && x_slot >= 0 && !xrow;
+  bool holes = true;   // rows keep the columns of lanes that do not write them (diag 4: no holes)
+  if (P.diag) {   // timing-only diagnostics (wrong results): drifted lanes skip / write the common row,
+                  // 4: whole rows written (no holes left by passed lanes), 8: no stale-column writes
     if (P.diag & 2u) wr |= wd;
-    wd = false;
+    if (P.diag & 3u) wd = false;
+    if (P.diag & 4u) holes = false;
+    if (P.diag & 8u) wx = false;
   }
   if (__ballot(wr || wd || xrow || wx)) {
     const int lane = threadIdx.x & 63;
@@ -1592,7 +1671,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       const int src = (k * 64 + lane) / R, rr = (k * 64 + lane) - src * R;
       k_src[k] = src;
       k_term[k] = __shfl(w_term, src);
-      k_on[k] = ((uint32_t(__shfl(int(wr ? wmask : 0u), src)) >> rr) & 1u) != 0u;   // (LXS: the leader's column)
+      k_on[k] = ((uint32_t(__shfl(int(wr ? wmask : 0u), src)) >> rr) & 1u) != 0u || !holes;   // (LXS: the leader's column)
       k_x[k] = anyx && ((uint32_t(__shfl(xrow ? int(1u << x_r) : 0, src)) >> rr) & 1u) != 0u;
     }
     for (int e = 0; e < n; ++e) {

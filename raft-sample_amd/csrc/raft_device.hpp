@@ -269,6 +269,7 @@ struct Trace {          // per-launch trace parameters (virtual clock + RNG)
   int32_t now;          // tick * tick_seconds
   int32_t f_min, f_span, c_min, c_span;
   uint32_t iso_p, iso_min, iso_span;
+  uint32_t iso_m, iso_l;  // x / iso_span = udiv_magic(x, iso_m, iso_l) (host-computed, exact for every u32 x)
   uint32_t iso_leader;  // EXT: a window isolates the lowest-id leader at its first tick
   int32_t secs;         // tick_seconds
   uint32_t period, entries;  // client event every `period` ticks, `entries` each
@@ -287,6 +288,22 @@ struct Trace {          // per-launch trace parameters (virtual clock + RNG)
     return period && t > 0 ? uint64_t((t + int64_t(period) - 1) / int64_t(period)) * entries : 0u;
   }
 };
+
+// Exact u32 division by a launch constant d >= 1 (Granlund-Montgomery
+// round-up with the add fix-up, as libdivide's branch-free u32 form): l =
+// ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1; d = 1 is l = 0. One mulhi
+// instead of the ~25-instruction runtime division.
+__host__ __device__ __forceinline__ void udiv_magic_of(uint32_t d, uint32_t* m, uint32_t* l) {
+  uint32_t ll = 0;
+  while ((uint64_t(1) << ll) < d) ++ll;
+  *l = ll;
+  *m = ll ? uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << ll) - d)) / d + 1) : 0u;
+}
+__device__ __forceinline__ uint32_t udiv_magic(uint32_t x, uint32_t m, uint32_t l) {
+  if (l == 0) return x;
+  const uint32_t t = __umulhi(m, x);
+  return (t + ((x - t) >> 1)) >> (l - 1);
+}
 
 // ------------------------------------------------------------------ RNG --
 __device__ __forceinline__ uint64_t sm64(uint64_t x) {

@@ -21,12 +21,15 @@ __device__ __forceinline__ uint32_t iso_windows(uint64_t key, const Trace& T, ui
   uint32_t mask = 0;
   *active = *starting = 0;
   const int64_t ep = T.tick >> 5;
+  // rng_k(key, 0, ST_ISOLATE, e) = sm64(inner ^ e): the inner hash is shared by both epochs
+  const uint64_t inner = sm64(key ^ (uint64_t(ST_ISOLATE) << 32));
   for (int64_t e = ep; e >= ep - 1 && e >= 0; --e) {
-    const uint64_t h = rng_k(key, 0, ST_ISOLATE, uint64_t(e));
+    const uint64_t h = sm64(inner ^ uint64_t(e));
     if ((h & 0xFFFF) >= T.iso_p) continue;
     const uint32_t victim = uint32_t((h >> 16) & 0xFF) % uint32_t(R);
     const int64_t start = e * 32 + int64_t((h >> 24) & 31);
-    const int64_t len = int64_t(T.iso_min) + int64_t(uint32_t(h >> 32) % T.iso_span);
+    const uint32_t x = uint32_t(h >> 32);   // len = iso_min + x mod iso_span
+    const int64_t len = int64_t(T.iso_min) + int64_t(x - udiv_magic(x, T.iso_m, T.iso_l) * T.iso_span);
     if (T.tick >= start && T.tick < start + len) {
       mask |= 1u << victim;
       *active |= 1u << (e & 1);

@@ -172,7 +172,7 @@ def test_class_coverage_c4_config_full_oracle():
     need = ["lean_ssync", "lean_lxs", "lean_lxs_whole_row", "lean_switch", "lean_three_seg", "lean_hwx",
             "list_quiet", "list_isolated_leader", "list_election", "list_first_round", "list_return",
             "list_return_trunc", "list_stale", "list_hwx", "list_window_start", "list_switch", "lean_sxs",
-            "lean_sxs_stale_in_row", "list_sxs_entered", "list_sxs_materialised"]
+            "lean_sxs_stale_in_row", "list_sxs_entered", "list_sxs_materialised", "list_stale_moved"]
     low = {k: cls[k] for k in need if cls[k] < MIN_TAKEN}
     assert not low, f"classes taken fewer than {MIN_TAKEN} times: {low}\nall: {cls}"
 
