@@ -1040,28 +1040,52 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     }
   }
   // a returning stale leader's catch-up (entries L0+1..Ll of the primary's
-  // log into its own, same slots): the wave copies one lane's entries at a
-  // time, one entry per lane, so each costs one round trip instead of a
-  // serial loop in the lane whose wave waits on it
+  // log into its own, same slots): the wave packs whole groups into steps of
+  // 64 entries, one entry per lane (source and destination are different
+  // columns, so a step's loads and stores need no order), so the returns of a
+  // wave cost one or a few round trips instead of one per returning lane; a
+  // group with more than 64 entries goes alone, 64 per step
   if constexpr (RAFT) {
     uint64_t pend = __ballot(cp_n > 0);
     const int lane = threadIdx.x & 63;
     while (pend) {
-      const int src = int(__builtin_ctzll(pend));
-      pend &= pend - 1ull;
-      const int cnt = __shfl(cp_n, src), from = __shfl(cp_from, src), sb_ = __shfl(cp_sb, src);
-      const int sb2_ = __shfl(cp_sb2, src);
-      const uint32_t cs = uint32_t(__shfl(int(cp_cs), src)), rr = uint32_t(__shfl(int(cp_rot), src));
-      const uint32_t rb = uint32_t(__shfl(int(cp_rotb), src));
-      const uint32_t gg = uint32_t(__shfl(int(g), src));
+      int src = -1, j = 0;
+      const int s0 = int(__builtin_ctzll(pend));
+      const int c0 = __builtin_amdgcn_readlane(cp_n, s0);
+      int span = 1;   // entries per lane in this step (> 1: one group, 64 per pass)
+      if (c0 > 64) {
+        src = s0;
+        j = lane;
+        span = (c0 + 63) / 64;
+        pend &= pend - 1ull;
+      } else {
+        int off = 0;
+        while (pend) {   // pack groups while their entries fit the step
+          const int sl = int(__builtin_ctzll(pend));
+          const int cnt = __builtin_amdgcn_readlane(cp_n, sl);
+          if (cnt > 64 || off + cnt > 64) break;
+          if (lane >= off && lane < off + cnt) { src = sl; j = lane - off; }
+          off += cnt;
+          pend &= pend - 1ull;
+        }
+      }
+      const int ss_ = src < 0 ? lane : src;
+      const int cnt = __shfl(cp_n, ss_), from = __shfl(cp_from, ss_), sb_ = __shfl(cp_sb, ss_);
+      const int sb2_ = __shfl(cp_sb2, ss_);
+      const uint32_t cs = uint32_t(__shfl(int(cp_cs), ss_)), rr = uint32_t(__shfl(int(cp_rot), ss_));
+      const uint32_t rb = uint32_t(__shfl(int(cp_rotb), ss_));
+      const uint32_t gg = uint32_t(__shfl(int(g), ss_));
       const uint64_t tb = ring_tile(gg, P.KP, R);
       const uint32_t cc = cs & 15u, ss = cs >> 4;
-      for (int j = lane; j < cnt; j += 64) {
-        const uint32_t o = ring_in_tile(gg, R, ring_slot(from + j, rr & 0xFFFFu, rr >> 16, rb, sb_, sb2_, P.kmask), 0u);
-        const int32_t t = at(P.log_term + tb, o + cc);
-        const int64_t v = at(P.log_value + tb, o + cc);
-        st<WT>(P.log_term + tb, o + ss, t);
-        st<WT>(P.log_value + tb, o + ss, v);
+      for (int k = 0; k < span; ++k) {
+        const int jj = j + 64 * k;
+        if (src >= 0 && jj < cnt) {
+          const uint32_t o = ring_in_tile(gg, R, ring_slot(from + jj, rr & 0xFFFFu, rr >> 16, rb, sb_, sb2_, P.kmask), 0u);
+          const int32_t t = at(P.log_term + tb, o + cc);
+          const int64_t v = at(P.log_value + tb, o + cc);
+          st<WT>(P.log_term + tb, o + ss, t);
+          st<WT>(P.log_value + tb, o + ss, v);
+        }
       }
     }
     // a stale leader's entries above a segment switch (see the switch): entry
