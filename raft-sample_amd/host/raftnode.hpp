@@ -86,7 +86,7 @@ class Engine {
     s.log_crc.resize(G * R * K);
     raft_state_view v{s.role.data(), s.voted.data(), s.term.data(), s.last.data(), s.commit.data(),
                       s.deadline.data(), s.timeout.data(), s.match.data(), s.fault.data(),
-                      s.log_term.data(), s.log_value.data(), s.log_crc.data(), nullptr, nullptr};
+                      s.log_term.data(), s.log_value.data(), s.log_crc.data(), nullptr, nullptr, nullptr};
     check(raft_store_state(h_, &v), "raft_store_state");
     return s;
   }
