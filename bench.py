@@ -171,7 +171,7 @@ def main():
     ap.add_argument("--ring-depth", type=int, default=None)
     ap.add_argument("--leader", type=int, default=0, help="steady-state leader replica (-1: hashed per group)")
     ap.add_argument("--cpu-groups", type=int, default=262144)
-    ap.add_argument("--cpu-ticks", type=int, default=384)
+    ap.add_argument("--cpu-ticks", type=int, default=1024)   # ~10 s of oracle work on 16 host threads
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--isolate", type=int, default=None,
                     help="diagnostics: override the workload's isolation windows per 65536 epochs (0: none)")
