@@ -102,11 +102,25 @@ struct raft_engine {
   uint32_t hist_cap = 0;
   uint32_t last_stats_n = 0;             // nticks of the last raft_tick call with statistics (0: none yet)
   unsigned long long* cstat = nullptr;   // raft_comm_allreduce_stats staging
-  uint32_t wpar = 0;            // parity of the next worklist window (its counter was zeroed by the last general kernel)
-  // worklist of groups the steady-state kernel hands to the general kernel
-  uint32_t* work = nullptr;     // deferred group ids
-  int32_t* work_tick = nullptr; // tick each one was deferred at
-  uint32_t* wcount = nullptr;   // shard counters: worklist [2 parities][SHARD_WORDS], then the two-pass list [2][SHARD_WORDS]
+  uint32_t wpar = 0;            // parity of the next worklist window (its counters were zeroed by its last window tail)
+  // worklists of groups the fast kernels hand to the general kernel, one per
+  // window parity (the general kernel of a window may run beside the next
+  // window's first tick, which appends to the other one)
+  uint32_t* work[2] = {nullptr, nullptr};     // deferred group ids
+  int32_t* work_tick[2] = {nullptr, nullptr}; // tick each one was deferred at
+  uint32_t* wcount = nullptr;   // counter block (raft_device.hpp WCOUNT_WORDS): worklists x2, two-pass list x2, tail words
+  // Overlapped general kernel: at a window's end (not a call's last tick) the
+  // general kernel runs on gen_stream beside the next tick's lean and list
+  // kernels, catching its groups up through that tick too (they keep DEFER,
+  // so the fast kernels leave them alone); the engine stream then waits for
+  // it and runs the window tail (DEFER cleared) before the tick after.
+  // RAFTSTEP_OVERLAP_GENERAL=0 runs it in line (A/B).
+  int overlap_general = 1;
+  hipStream_t gen_stream = nullptr;
+  hipEvent_t gen_ev[2] = {nullptr, nullptr};   // engine -> gen_stream, gen_stream -> engine
+  bool gen_pending = false;     // a general kernel is running on gen_stream
+  int gen_parity = 0;           // its worklist parity
+  uint32_t gen_w0 = 0, gen_w1 = 0;   // its window's stats range (indices into the call's ticks)
   int force_general = 0;        // debug: route every group through the general kernel
   int lane_general = 0;         // RAFTSTEP_GENERAL=lane: one-lane-per-group general kernel (A/B) instead of the segment one
   uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
@@ -457,9 +471,11 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.gsb2), Gp * 4);
   // sharded group lists (raft_device.hpp): NSHARD shards of scap entries
   const uint64_t scap = ((Gp / 256 + NSHARD - 1) / NSHARD) * 256;
-  A(reinterpret_cast<void**>(&e->work), NSHARD * scap * 4);
-  A(reinterpret_cast<void**>(&e->work_tick), NSHARD * scap * 4);
-  A(reinterpret_cast<void**>(&e->wcount), 4 * SHARD_WORDS * 4);   // worklist x2 parities, two-pass list x2
+  for (int q = 0; q < 2; ++q) {
+    A(reinterpret_cast<void**>(&e->work[q]), NSHARD * scap * 4);
+    A(reinterpret_cast<void**>(&e->work_tick[q]), NSHARD * scap * 4);
+  }
+  A(reinterpret_cast<void**>(&e->wcount), WCOUNT_WORDS * 4);
   A(reinterpret_cast<void**>(&e->blist), NSHARD * scap * 4);
   A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.log_value), R * K * Gp * 8);
@@ -470,7 +486,9 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->P.crc_tab = d_tab;
   if (rc == RAFT_OK) {
     hipError_t h = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
-    if (h != hipSuccess) rc = fail(RAFT_EHIP, "hipStreamCreate: %s", hipGetErrorString(h));
+    if (h == hipSuccess) h = hipStreamCreateWithFlags(&e->gen_stream, hipStreamNonBlocking);
+    for (int q = 0; q < 2 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->gen_ev[q], hipEventDisableTiming);
+    if (h != hipSuccess) rc = fail(RAFT_EHIP, "hipStreamCreate / hipEventCreate: %s", hipGetErrorString(h));
   }
   if (rc != RAFT_OK) {
     std::string keep = g_err;
@@ -494,6 +512,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
   if (const char* dl = getenv("RAFTSTEP_DIAG_LEAN")) e->P.diag = uint32_t(atoi(dl));
+  if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = atoi(og) != 0;
   e->P.dbg_pass = 0xFFFFFFFFu;
   if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
     e->diag_print = 1;
@@ -523,7 +542,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetAsync(e->P.gsb, 0, Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grotb, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gsb2, 0, Gp * 4, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, 4 * SHARD_WORDS * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, WCOUNT_WORDS * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_value, 0, R * K * Gp * 8, e->stream) : z;
   if (c.payload_crc) z = z == hipSuccess ? hipMemsetAsync(e->P.log_crc, 0, R * K * Gp * 4, e->stream) : z;
@@ -547,6 +566,10 @@ int raft_engine_destroy(raft_engine* e) {
   for (hipEvent_t x : e->ev) (void)hipEventDestroy(x);
   for (hipEvent_t x : e->comm_ev) (void)hipEventDestroy(x);
   if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
+  if (e->gen_stream) (void)hipStreamSynchronize(e->gen_stream);
+  for (hipEvent_t x : e->gen_ev)
+    if (x) (void)hipEventDestroy(x);
+  if (e->gen_stream) (void)hipStreamDestroy(e->gen_stream);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->hist) (void)hipFree(e->hist);
   if (e->tstat) (void)hipFree(e->tstat);
@@ -892,10 +915,24 @@ static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1, const Ca
   return RAFT_OK;
 }
 
+// Join of an overlapped general kernel (see raft_engine::overlap_general):
+// the engine stream waits for gen_stream, the window tail clears the
+// window's DEFER flags and zeroes its worklist, its ticks' records are reduced.
+static int join_general(raft_engine* e, bool stats) {
+  HIPCHK(hipStreamWaitEvent(e->stream, e->gen_ev[1], 0));
+  HIPCHK(launch_window_tail(e->P, e->work[e->gen_parity], e->wcount, e->gen_parity, e->stream));
+  e->gen_pending = false;
+  if (stats)
+    if (int rc = flush_window_stats(e, e->gen_w0, e->gen_w1, nullptr)) return rc;
+  return RAFT_OK;
+}
+
 static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool stats) {
   if (int rc = settle_check(e)) return rc;
   if (int rc = check_ticks(e, first_tick, nticks)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
+  if (e->gen_pending)   // (only after a failed call: every call joins its general kernels)
+    if (int rc = join_general(e, false)) return rc;
   // (the per-tick records need nticks slots; the check records exist at any capacity)
   if (int rc = ensure_hist(e, stats ? std::max<uint32_t>(nticks, 1) : 1)) return rc;
   if (!nticks) return RAFT_OK;
@@ -940,15 +977,23 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         d = next_event(e);
         if (!c || !d) return fail(RAFT_EHIP, "hipEventCreate failed");
       }
-      HIPCHK(launch_tick_two_pass(e->R, int(e->cfg.semantics), e->P, T, st, e->work, e->work_tick, cnt, e->blist,
+      HIPCHK(launch_tick_two_pass(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar & 1],
+                                  e->work_tick[e->wpar & 1], cnt, e->blist,
                                   e->wcount + (2 + (e->lpar & 1)) * SHARD_WORDS,
                                   e->wcount + (2 + ((e->lpar + 1) & 1)) * SHARD_WORDS, e->stream, a, b,
                                   c, d, skip_list));
       ++e->lpar;
     } else {
-      HIPCHK(launch_tick_fast(e->R, int(e->cfg.semantics), e->P, T, st, e->work, e->work_tick, cnt, force,
+      HIPCHK(launch_tick_fast(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar & 1],
+                              e->work_tick[e->wpar & 1], cnt, force,
                               e->write_through, e->stream, a, b));
     }
+    // the previous window's general kernel, overlapped with this tick's fast
+    // kernels: the engine stream waits for it, then its window tail clears
+    // its groups' DEFER (before the next tick's lean kernel) and its ticks'
+    // records are final
+    if (e->gen_pending)
+      if (int rc = join_general(e, stats)) return rc;
     // deferred groups catch up every slow_every ticks and at the end of the call
     if ((i + 1) % e->slow_every == 0 || i + 1 == nticks) {
       if (e->debug_work) {   // diagnostics: worklist size of each general-kernel launch (synchronising)
@@ -958,22 +1003,40 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         for (int k = 0; k < NSHARD; ++k) nw += sh[k * SHARD_STRIDE];
         fprintf(stderr, "raftstep: general kernel ticks %lld..%lld worklist %u\n", (long long)win_first, (long long)t, nw);
       }
+      const bool last = i + 1 == nticks;
+      const int par = int(e->wpar & 1);
       // (with the list skipped nothing can be deferred — only the list kernel
-      // defers — so both worklist counters stay zero and the general kernel
-      // has nothing to do)
-      if (!skip_list) {
+      // defers — so both worklists stay empty and there is nothing to catch up)
+      const bool overlap = !skip_list && two && e->overlap_general && !last && !e->debug_work;
+      if (overlap) {
+        // beside tick t+1's lean and list kernels, through tick t+1 (its groups
+        // keep DEFER, so those kernels leave them alone; tick t+1's deferrals
+        // go to the other worklist)
+        HIPCHK(hipEventRecord(e->gen_ev[0], e->stream));
+        HIPCHK(hipStreamWaitEvent(e->gen_stream, e->gen_ev[0], 0));
+        HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t + 1,
+                                stats ? e->hist : nullptr, e->work[par], e->work_tick[par], cnt, nullptr,
+                                e->lane_general, e->gen_stream));
+        HIPCHK(hipEventRecord(e->gen_ev[1], e->gen_stream));
+        e->gen_pending = true;
+        e->gen_parity = par;
+        e->gen_w0 = stats_first;
+        e->gen_w1 = i;
+        ++e->n_general;
+      } else if (!skip_list) {
         HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t,
-                                stats ? e->hist : nullptr, e->work, e->work_tick, cnt,
-                                e->wcount + ((e->wpar + 1) & 1) * SHARD_WORDS, e->lane_general, e->stream));
+                                stats ? e->hist : nullptr, e->work[par], e->work_tick[par], cnt, nullptr,
+                                e->lane_general, e->stream));
+        HIPCHK(launch_window_tail(e->P, e->work[par], e->wcount, par, e->stream));
         ++e->n_general;
       }
       ++e->wpar;
-      // per-tick records: reduced (and all-reduced) per window; with the list
-      // skipped on one GPU nothing overlaps them, so one reduce at the end of
-      // the call covers every tick. The last one carries the check record.
-      const bool last = i + 1 == nticks;
-      const CallCheck chk{e->wcount, int((e->wpar + 1) & 1), skip_list ? 1 : 0, e->tstat + size_t(nticks) * NSTAT};
-      if (stats && (!skip_list || e->comm || last))
+      // per-tick records: reduced (and all-reduced) per window — an overlapped
+      // window's once its general kernel has joined; with the list skipped on
+      // one GPU nothing overlaps them, so one reduce at the end of the call
+      // covers every tick. The last one carries the check record.
+      const CallCheck chk{e->wcount, par, skip_list ? 1 : 0, e->tstat + size_t(nticks) * NSTAT};
+      if (stats && !overlap && (!skip_list || e->comm || last))
         if (int rc = flush_window_stats(e, stats_first, i, (last && two) ? &chk : nullptr)) return rc;
       if (!skip_list || e->comm || last) stats_first = i + 1;
       win_first = t + 1;

@@ -1017,6 +1017,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     df |= (!bail && giso_w >= 0) ? 1u << 28 : 0u;
     stored = !skip && !bail;
   }
+  if (LIST && (P.diag & 128u)) {   // timing only (results wrong): the per-group code alone
+    wr = 0; cp_n = 0; mv_n = 0;
+  }
   // ---- this tick's log entries into the rings (all lanes of the wave) ----
   // Ring row of one slot = 64 lanes x R replicas, contiguous. The lanes of
   // the wave that append at the wave's common slot s0 (logs in step: the
@@ -1027,149 +1030,121 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   // entry. Every other writing lane stores its own R-contiguous segment.
   // s0: the global phase entries_before(tick) (groups rotated at their first
   // entry, init_steady) or the first writer's slot, whichever more lanes share.
-  if (LIST && n && wr != 0) {   // scattered groups: each lane writes its own R-contiguous segment
-    const uint64_t tb = ring_tile(g, P.KP, R);
-    int32_t* const rt = P.log_term + tb;
-    int64_t* const rv = P.log_value + tb;
-    uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
-    df |= 512u;
-    uint32_t cs = 0;
-    if constexpr (CRC) cs = crc_term_state(tab, w_term);
-    for (int e = 0; e < n; ++e) {
-      const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
-      uint32_t stamp = 0;
-      if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
-      {
-            const uint32_t o = ring_in_tile(g, R, uint32_t((w_ph + e) & int(P.kmask)), 0u);
-            if (!WT && wr == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
-              fill_seg<R>(rt + o, w_term);
-              fill_seg<R>(rv + o, v);
-              if constexpr (CRC) fill_seg<R>(rc + o, stamp);
-            } else {
-#pragma unroll
-              for (int p = 0; p < R; ++p) {
-                if (!((wr >> p) & 1u)) continue;
-                rst<WT>(rt, o + p, w_term);
-                rst<WT>(rv, o + p, v);
-                if constexpr (CRC) rst<WT>(rc, o + p, stamp);
-              }
-            }
-      }
-    }
-  }
-  // a returning stale leader's catch-up (entries L0+1..Ll of the primary's
-  // log into its own, same slots): the wave packs whole groups into steps of
-  // 64 entries, one entry per lane (source and destination are different
-  // columns, so a step's loads and stores need no order), so the returns of a
-  // wave cost one or a few round trips instead of one per returning lane; a
-  // group with more than 64 entries goes alone, 64 per step
+  // Entry copies (RAFT): a returning stale leader's catch-up (entries
+  // L0+1..Ll of the primary's column into its own, same slots) and a stale
+  // leader's entries above a segment switch (entry i of its column from slot
+  // (i-1+rot) to (i-1+rot+d), from the top down). The wave gathers every
+  // entry of all its lanes' jobs with loads issued together (CPS entries per
+  // lane and pass, in registers), then writes this tick's own entries, then
+  // scatters the gathered ones: one load round trip per pass for the whole
+  // wave, instead of a store->load chain per 64-entry step (vmcnt counts
+  // stores too). Within a pass every load completes before any store, so a
+  // move's overlapping source and destination slots are safe; across passes
+  // a move goes from the top down (entry i's destination is the source of
+  // entry i+d, read in the same or an earlier pass). Copy and move never
+  // meet in one group (a switch needs sr < 0).
+  constexpr int CPS = 4;   // entries per lane and pass
+  int jn = 0, jpre = 0, jtot = 0;   // this lane's job size, exclusive wave prefix, wave total
   if constexpr (RAFT) {
-    uint64_t pend = __ballot(cp_n > 0);
-    const int lane = threadIdx.x & 63;
-    while (pend) {
-      int src = -1, j = 0;
-      const int s0 = int(__builtin_ctzll(pend));
-      const int c0 = __builtin_amdgcn_readlane(cp_n, s0);
-      int span = 1;   // entries per lane in this step (> 1: one group, 64 per pass)
-      if (c0 > 64) {
-        src = s0;
-        j = lane;
-        span = (c0 + 63) / 64;
-        pend &= pend - 1ull;
-      } else {
-        int off = 0;
-        while (pend) {   // pack groups while their entries fit the step
-          const int sl = int(__builtin_ctzll(pend));
-          const int cnt = __builtin_amdgcn_readlane(cp_n, sl);
-          if (cnt > 64 || off + cnt > 64) break;
-          if (lane >= off && lane < off + cnt) { src = sl; j = lane - off; }
-          off += cnt;
-          pend &= pend - 1ull;
-        }
-      }
-      const int ss_ = src < 0 ? lane : src;
-      const int cnt = __shfl(cp_n, ss_), from = __shfl(cp_from, ss_), sb_ = __shfl(cp_sb, ss_);
-      const int sb2_ = __shfl(cp_sb2, ss_);
-      const uint32_t cs = uint32_t(__shfl(int(cp_cs), ss_)), rr = uint32_t(__shfl(int(cp_rot), ss_));
-      const uint32_t rb = uint32_t(__shfl(int(cp_rotb), ss_));
-      const uint32_t gg = uint32_t(__shfl(int(g), ss_));
-      const uint64_t tb = ring_tile(gg, P.KP, R);
-      const uint32_t cc = cs & 15u, ss = cs >> 4;
-      for (int k = 0; k < span; ++k) {
-        const int jj = j + 64 * k;
-        if (src >= 0 && jj < cnt) {
-          const uint32_t o = ring_in_tile(gg, R, ring_slot(from + jj, rr & 0xFFFFu, rr >> 16, rb, sb_, sb2_, P.kmask), 0u);
-          const int32_t t = at(P.log_term + tb, o + cc);
-          const int64_t v = at(P.log_value + tb, o + cc);
-          rst<WT>(P.log_term + tb, o + ss, t);
-          rst<WT>(P.log_value + tb, o + ss, v);
+    jn = cp_n > 0 ? cp_n : mv_n;
+    jpre = jn;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {   // inclusive scan
+      const int y = __shfl_up(jpre, o);
+      if (int(threadIdx.x & 63) >= o) jpre += y;
+    }
+    jtot = __shfl(jpre, 63);
+    jpre -= jn;
+    if (jtot && __ballot(mv_n > 0)) __threadfence_block();   // the stale leader's entries stored this tick (moved)
+  }
+  const int passes = RAFT ? (jtot + 64 * CPS - 1) / (64 * CPS) : 0;   // (wave-uniform)
+  for (int pass_i = 0; pass_i < (passes > 0 ? passes : 1); ++pass_i) {
+    int32_t ct[CPS];
+    int64_t cv[CPS];
+    uint32_t cc[CPS];
+    uint32_t cdst[CPS];      // destination element offset inside the ring (64-bit tile base below)
+    uint64_t ctb[CPS];
+    bool con[CPS];
+    if constexpr (RAFT) {
+      const int lane = threadIdx.x & 63;
+#pragma unroll
+      for (int k = 0; k < CPS; ++k) {
+        const int e = pass_i * 64 * CPS + k * 64 + lane;
+        con[k] = e < jtot;
+        ct[k] = 0; cv[k] = 0; cc[k] = 0; cdst[k] = 0; ctb[k] = 0;
+        // owner: the last lane whose prefix is <= e (its job holds entry e)
+        int o = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+          if (__shfl(jpre, o + step) <= e) o += step;
+        const int j = e - __shfl(jpre, o);
+        // (every shuffle unconditional: a shuffle reading a lane that is off
+        // in a divergent branch returns 0)
+        const int kcp = __shfl(cp_n, o);
+        const int cpf = __shfl(cp_from, o), mvf = __shfl(mv_from, o);
+        const int cnt = __shfl(jn, o);
+        const uint32_t gg = uint32_t(__shfl(int(g), o));
+        const uint32_t cpr = uint32_t(__shfl(int(cp_rot), o)), mvr = uint32_t(__shfl(mv_rot, o));
+        const int from = kcp > 0 ? cpf : mvf;
+        const uint32_t rr = kcp > 0 ? cpr : mvr;
+        const uint32_t rb = uint32_t(__shfl(int(cp_rotb), o));
+        const int sb_ = __shfl(cp_sb, o), sb2_ = __shfl(cp_sb2, o), dd = __shfl(mv_d, o);
+        const uint32_t cs = uint32_t(__shfl(int(cp_cs), o)), mcol = uint32_t(__shfl(mv_col, o));
+        if (con[k]) {
+          const uint64_t tb = ring_tile(gg, P.KP, R);
+          uint32_t osrc, odst;
+          if (kcp > 0) {   // catch-up: same slot, the primary's column into the stale leader's
+            const uint32_t o0 = ring_in_tile(gg, R, ring_slot(from + j, rr & 0xFFFFu, rr >> 16, rb, sb_, sb2_, P.kmask), 0u);
+            osrc = o0 + (cs & 15u);
+            odst = o0 + (cs >> 4);
+          } else {         // move: from the top down, same column
+            const int idx = from + cnt - 1 - j;
+            osrc = ring_in_tile(gg, R, uint32_t(idx - 1 + int(rr)) & P.kmask, mcol);
+            odst = ring_in_tile(gg, R, uint32_t(idx - 1 + int(rr) + dd) & P.kmask, mcol);
+          }
+          ct[k] = at(P.log_term + tb, osrc);
+          cv[k] = at(P.log_value + tb, osrc);
+          if constexpr (CRC) cc[k] = at(P.log_crc + tb, osrc);
+          cdst[k] = odst;
+          ctb[k] = tb;
         }
       }
     }
-    // a stale leader's entries above a segment switch (see the switch): entry
-    // i goes from slot (i-1+rot) to (i-1+rot+d). The wave packs whole groups
-    // into steps of 64 entries (one entry per lane); a step's loads all
-    // complete before its stores, so overlapping source and destination slots
-    // of one group are safe. (A group with more than 64 entries goes alone,
-    // 64 per step from the top down: entry i's destination is the source of
-    // entry i+d, moved in an earlier step.) The fence makes the entries the
-    // stale leader's lane stored this tick visible to the other lanes.
-    uint64_t mpend = __ballot(mv_n > 0);
-    if (mpend) {
-      __threadfence_block();
-      while (mpend) {
-        int src = -1, i = 0, top = 0;
-        const int s0 = int(__builtin_ctzll(mpend));
-        const int c0 = __builtin_amdgcn_readlane(mv_n, s0);
-        if (c0 > 64) {   // alone, from the top down
-          mpend &= mpend - 1ull;
-          const int from = __builtin_amdgcn_readlane(mv_from, s0);
-          for (top = from + c0 - 1; top >= from; top -= 64) {
-            i = top - lane;
-            if (i >= from) src = s0;
-            const uint32_t gg = uint32_t(__builtin_amdgcn_readlane(int(g), s0));
-            const int dd = __builtin_amdgcn_readlane(mv_d, s0), rr = __builtin_amdgcn_readlane(mv_rot, s0);
-            const uint32_t col = uint32_t(__builtin_amdgcn_readlane(mv_col, s0));
-            const uint64_t tb = ring_tile(gg, P.KP, R);
-            const uint32_t o0 = ring_in_tile(gg, R, uint32_t(i - 1 + rr) & P.kmask, col);
-            const uint32_t o1 = ring_in_tile(gg, R, uint32_t(i - 1 + rr + dd) & P.kmask, col);
-            if (i >= from) {
-              const int32_t t = at(P.log_term + tb, o0);
-              const int64_t v = at(P.log_value + tb, o0);
-              uint32_t cr = 0;
-              if constexpr (CRC) cr = at(P.log_crc + tb, o0);
-              rst<WT>(P.log_term + tb, o1, t);
-              rst<WT>(P.log_value + tb, o1, v);
-              if constexpr (CRC) rst<WT>(P.log_crc + tb, o1, cr);
-            }
+    if (LIST && pass_i == 0 && n && wr != 0) {   // this tick's entries: scattered groups, each lane its own R-contiguous segment
+      const uint64_t tb = ring_tile(g, P.KP, R);
+      int32_t* const rt = P.log_term + tb;
+      int64_t* const rv = P.log_value + tb;
+      uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
+      df |= 512u;
+      uint32_t cs = 0;
+      if constexpr (CRC) cs = crc_term_state(tab, w_term);
+      for (int e = 0; e < n; ++e) {
+        const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
+        uint32_t stamp = 0;
+        if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+        const uint32_t o = ring_in_tile(g, R, uint32_t((w_ph + e) & int(P.kmask)), 0u);
+        if (!WT && wr == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
+          fill_seg<R>(rt + o, w_term);
+          fill_seg<R>(rv + o, v);
+          if constexpr (CRC) fill_seg<R>(rc + o, stamp);
+        } else {
+#pragma unroll
+          for (int p = 0; p < R; ++p) {
+            if (!((wr >> p) & 1u)) continue;
+            rst<WT>(rt, o + p, w_term);
+            rst<WT>(rv, o + p, v);
+            if constexpr (CRC) rst<WT>(rc, o + p, stamp);
           }
-          continue;
         }
-        int off = 0;
-        while (mpend) {   // pack groups while their entries fit the step
-          const int sl = int(__builtin_ctzll(mpend));
-          const int cnt = __builtin_amdgcn_readlane(mv_n, sl);
-          if (cnt > 64 || off + cnt > 64) break;
-          if (lane >= off && lane < off + cnt) { src = sl; i = lane - off; }
-          off += cnt;
-          mpend &= mpend - 1ull;
-        }
-        const int ss_ = src < 0 ? lane : src;
-        const int from = __shfl(mv_from, ss_), dd = __shfl(mv_d, ss_), rr = __shfl(mv_rot, ss_);
-        const uint32_t col = uint32_t(__shfl(mv_col, ss_)), gg = uint32_t(__shfl(int(g), ss_));
-        if (src >= 0) {
-          const int idx = from + i;
-          const uint64_t tb = ring_tile(gg, P.KP, R);
-          const uint32_t o0 = ring_in_tile(gg, R, uint32_t(idx - 1 + rr) & P.kmask, col);
-          const uint32_t o1 = ring_in_tile(gg, R, uint32_t(idx - 1 + rr + dd) & P.kmask, col);
-          const int32_t t = at(P.log_term + tb, o0);
-          const int64_t v = at(P.log_value + tb, o0);
-          uint32_t cr = 0;
-          if constexpr (CRC) cr = at(P.log_crc + tb, o0);
-          rst<WT>(P.log_term + tb, o1, t);
-          rst<WT>(P.log_value + tb, o1, v);
-          if constexpr (CRC) rst<WT>(P.log_crc + tb, o1, cr);
-        }
+      }
+    }
+    if constexpr (RAFT) {
+#pragma unroll
+      for (int k = 0; k < CPS; ++k) {
+        if (!con[k]) continue;
+        rst<WT>(P.log_term + ctb[k], cdst[k], ct[k]);
+        rst<WT>(P.log_value + ctb[k], cdst[k], cv[k]);
+        if constexpr (CRC) rst<WT>(P.log_crc + ctb[k], cdst[k], cc[k]);
       }
     }
   }
@@ -1394,7 +1369,11 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     const uint32_t gs = valid ? g : 0u;   // (invalid lanes never touch their words)
     const WordAcc<true> gw{&smeta[t], &sgrot[t], &P.grota[gs], &sgiso[t], &shb[t], &P.gsb[gs], &sgss[t], &P.grotb[gs],
                            &P.gsb2[gs], &sglx[t], g};
-    const bool wrote = fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab, rw, gw);
+    // (P.diag, timing only, results wrong: 32 = staging alone, 64 = staging and write-back, no tick)
+    if (P.diag & 32u) { __syncthreads(); continue; }
+    const bool wrote = (P.diag & 64u) ? valid
+                                      : fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g,
+                                                                          tab, rw, gw);
     {   // dirty rows -> the 16-B pieces of the record they touch
       const uint32_t rows = (valid && wrote) ? sdm[t] : 0u;
       uint32_t pm = 0;

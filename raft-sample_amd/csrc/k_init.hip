@@ -160,13 +160,13 @@ __device__ __forceinline__ void call_check_block(const CallCheck& c) {
   if (threadIdx.x < uint32_t(NSHARD)) {
     const uint32_t k = threadIdx.x * SHARD_STRIDE;
     listed = uint64_t(c.wcount[2 * SHARD_WORDS + k]) + uint64_t(c.wcount[3 * SHARD_WORDS + k]);
-    deferred = c.wcount[uint32_t(c.wlast) * SHARD_WORDS + k];
+
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    listed += __shfl_xor(listed, o);
-    deferred += __shfl_xor(deferred, o);
-  }
+  for (int o = 32; o > 0; o >>= 1) listed += __shfl_xor(listed, o);
+  // what the last window tail took (its counters are zeroed by then); a
+  // list-skipping call defers nothing and runs no tail
+  deferred = c.zero_lists ? 0u : c.wcount[WC_TAKEN + c.wlast];
   __syncthreads();   // every lane has read the counters before any is zeroed
   if (c.zero_lists && threadIdx.x < uint32_t(NSHARD)) {
     c.wcount[2 * SHARD_WORDS + threadIdx.x * SHARD_STRIDE] = 0u;
@@ -177,6 +177,42 @@ __device__ __forceinline__ void call_check_block(const CallCheck& c) {
                                  : threadIdx.x == CHK_MAGIC ? 0x5241465443484Bull : 0ull;
     c.out[threadIdx.x] = v;
   }
+}
+
+// Window tail: after the general kernel has caught the window's deferred
+// groups up, their DEFER flags are cleared here (the general kernel keeps
+// them, so that it can run beside the next tick's fast kernels, which leave
+// DEFER groups alone), the total is kept for the check record, and the last
+// block to finish zeroes the window's worklist counters for the window after
+// next (its parity's next use).
+__global__ __launch_bounds__(256) void window_tail_kernel(uint16_t* gmeta, const uint32_t* work, uint32_t scap,
+                                                          uint32_t* wcount, int parity) {
+  __shared__ uint32_t pre[NSHARD + 1];
+  __shared__ bool last;
+  uint32_t* cnt = wcount + parity * SHARD_WORDS;
+  const uint32_t n = shard_prefix(cnt, pre);
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    const uint32_t g = work[shard_locate(pre, scap, i)];
+    const uint16_t m = at(gmeta, g);
+    if (m & M_DEFER) at(gmeta, g) = uint16_t(m & ~M_DEFER);
+  }
+  __syncthreads();   // every thread of the block has read the counters
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(&wcount[WC_DONE], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last) {
+    if (threadIdx.x < uint32_t(NSHARD)) cnt[threadIdx.x * SHARD_STRIDE] = 0u;
+    if (threadIdx.x == 0) {
+      wcount[WC_TAKEN + parity] = n;
+      wcount[WC_DONE] = 0u;
+    }
+  }
+}
+hipError_t launch_window_tail(const DevPlanes& P, const uint32_t* work, uint32_t* wcount, int parity, hipStream_t s) {
+  hipLaunchKernelGGL(window_tail_kernel, dim3(64), dim3(256), 0, s, P.gmeta, work, P.scap, wcount, parity);
+  return hipGetLastError();
 }
 
 __global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hist, unsigned long long* out,

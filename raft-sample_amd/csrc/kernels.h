@@ -70,14 +70,17 @@ hipError_t launch_digest(int R, const DevPlanes& P, int raft, uint64_t* per_grou
 // zero_lists: zero both list counters afterwards (a list-skipping call).
 enum : int { CHK_LISTED = 0, CHK_DEFERRED = 1, CHK_MAGIC = 7 };
 struct CallCheck {
-  uint32_t* wcount;             // the engine's shard counters (worklist x2, list x2)
-  int wlast;                    // parity of the worklist counter the last general kernel consumed
+  uint32_t* wcount;             // the engine's counter block (raft_device.hpp WCOUNT_WORDS)
+  int wlast;                    // parity of the worklist the last window tail took
   int zero_lists;
   unsigned long long* out;      // NSTAT words
 };
 // Sums the STAT_SLOTS slots of nticks consecutive per-tick records of `hist`
 // into out[nticks][NSTAT] and zeroes those slots; with `chk` also writes the
 // check record (nticks may then be 0).
+// Clears DEFER of the groups on worklist `parity` (work), records their
+// number and zeroes that worklist's counters (k_init.hip window_tail_kernel).
+hipError_t launch_window_tail(const DevPlanes& P, const uint32_t* work, uint32_t* wcount, int parity, hipStream_t s);
 hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s,
                                const CallCheck* chk = nullptr);
 hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s);

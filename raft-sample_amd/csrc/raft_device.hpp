@@ -139,6 +139,7 @@ struct DevPlanes {
   uint32_t scap;       // capacity of one shard of a sharded group list (see below)
   uint32_t diag;       // timing-only diagnostics (RAFTSTEP_DIAG_LEAN; results are wrong when set): 1 = drifted
                        // lanes of the lean kernel skip their ring writes, 2 = they write the wave's common row
+                       // (list kernel: 32 = staging alone, 64 = no tick, 128 = no ring writes / copies)
 };
 
 // Sharded group lists (the general kernel's worklist, the two-pass tick's
@@ -154,6 +155,13 @@ struct DevPlanes {
 constexpr int NSHARD = 64;
 constexpr int SHARD_STRIDE = 16;   // u32 words between two shard counters
 constexpr int SHARD_WORDS = NSHARD * SHARD_STRIDE;
+// engine counter block (u32 words): worklist counters [2 parities][SHARD_WORDS],
+// two-pass list counters [2][SHARD_WORDS], then the window tail's words:
+// the total each parity's last tail took (WC_TAKEN + parity) and its
+// blocks-done counter (WC_DONE)
+constexpr int WC_TAKEN = 4 * SHARD_WORDS;
+constexpr int WC_DONE = WC_TAKEN + 8;
+constexpr int WCOUNT_WORDS = WC_TAKEN + SHARD_STRIDE;
 __device__ __forceinline__ uint32_t shard_home(uint32_t g) { return (g >> 8) & uint32_t(NSHARD - 1); }
 // pre[0..NSHARD] (LDS) = exclusive prefix of the shard counts; returns the total.
 // Block-wide: every thread calls it.
@@ -624,7 +632,7 @@ struct Group {
     const int sx = one ? int(__builtin_ctz(others)) >> 1 : 0;
     const bool onestale = SEM == SEM_RAFT && one && (others & 0xAAAAu) != 0u && sel(term, sx) < sel(term, pri & 7);
     const int m = pri | (fault << 4) | (steady ? M_STEADY : 0) | (onecand ? M_ONECAND : 0) |
-                  (onestale ? M_ONESTALE : 0);
+                  (onestale ? M_ONESTALE : 0) | (meta0 & M_DEFER);   // (DEFER: cleared by the window tail)
     if (m != meta0) at(P.gmeta, g) = uint16_t(m);
   }
 

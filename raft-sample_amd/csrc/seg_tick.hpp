@@ -223,8 +223,10 @@ struct Seg {
     const bool onecand = one && (others & cands) != 0u;
     const int sx = one ? first_of(others) : 0;
     const bool onestale = SEM == SEM_RAFT && one && (others & leaders) != 0u && bc(term, sx) < bc(term, pri & 7);
+    // (DEFER stays until the window tail: the general kernel may run beside the
+    // next tick's fast kernels, which must keep leaving this group alone)
     const int m = pri | (fault << 4) | (steady ? M_STEADY : 0) | (onecand ? M_ONECAND : 0) |
-                  (onestale ? M_ONESTALE : 0);
+                  (onestale ? M_ONESTALE : 0) | (meta0 & M_DEFER);
     if (me == 0) {
       if (rd) {   // (grota never changes here)
         at(P.grot, g) = uint16_t(rt);
