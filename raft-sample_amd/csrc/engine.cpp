@@ -104,17 +104,18 @@ struct raft_engine {
   unsigned long long* cstat = nullptr;   // raft_comm_allreduce_stats staging
   uint32_t wpar = 0;            // parity of the next worklist window (its counters were zeroed by its last window tail)
   // worklists of groups the fast kernels hand to the general kernel, one per
-  // window parity (the general kernel of a window may run beside the next
-  // window's first tick, which appends to the other one)
-  uint32_t* work[2] = {nullptr, nullptr};     // deferred group ids
-  int32_t* work_tick[2] = {nullptr, nullptr}; // tick each one was deferred at
+  // window index mod NWORK (the general kernel of a window may run beside the
+  // next window's first tick, whose list kernel may already defer into the
+  // window after)
+  uint32_t* work[NWORK] = {};   // deferred group ids (window index mod NWORK)
+  int32_t* work_tick[NWORK] = {}; // tick each one was deferred at
   uint32_t* wcount = nullptr;   // counter block (raft_device.hpp WCOUNT_WORDS): worklists x2, two-pass list x2, tail words
   // Overlapped general kernel: at a window's end (not a call's last tick) the
   // general kernel runs on gen_stream beside the next tick's lean and list
   // kernels, catching its groups up through that tick too (they keep DEFER,
   // so the fast kernels leave them alone); the engine stream then waits for
   // it and runs the window tail (DEFER cleared) before the tick after.
-  // RAFTSTEP_OVERLAP_GENERAL=0 runs it in line (A/B).
+  // RAFTSTEP_OVERLAP_GENERAL=0 runs it in line (A/B; not with the pipeline).
   int overlap_general = 1;
   hipStream_t gen_stream = nullptr;
   hipEvent_t gen_ev[2] = {nullptr, nullptr};   // engine -> gen_stream, gen_stream -> engine
@@ -129,8 +130,18 @@ struct raft_engine {
   // two-pass tick (RAFTSTEP_TWO_PASS, default on): the lean kernel takes the
   // compressed steady groups, the list kernel every other live group
   int two_pass = 1;
-  uint32_t* blist = nullptr;    // [Gp] groups the lean kernel passed on
-  uint32_t lpar = 0;            // parity of the two-pass list's shard counters
+  uint32_t* blist[3] = {nullptr, nullptr, nullptr};   // groups the lean kernel passed on, one list per tick mod 3
+  uint32_t lpar = 0;            // tick counter of the two-pass lists (list lpar % 3 is the next tick's)
+  // Pipelined tick (RAFTSTEP_PIPELINE, default on; two-pass, list not
+  // skipped): the list kernel of tick t runs on list_stream and carries its
+  // groups through tick t+1 too, so the lean kernel of t+1 (which leaves those
+  // groups alone, P.glst marks) runs beside it; the lean kernel of t+2 waits
+  // for it. Lists and their counters rotate over three sets: lean(t+1) fills
+  // one while list(t) reads another and zeroes the third.
+  int pipeline = 0;
+  hipStream_t list_stream = nullptr;
+  hipEvent_t ev_lean[2] = {nullptr, nullptr};   // engine stream -> list_stream (list(t) after lean(t))
+  hipEvent_t ev_list[4] = {nullptr, nullptr, nullptr, nullptr};   // list_stream -> engine stream (list(t) done)
   // Steady-state list skip. After init_steady (every log empty, entries
   // appended from there only) and no host mutation since, once a call ends
   // with nothing deferred in its last window and an empty list at its last
@@ -471,12 +482,13 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.gsb2), Gp * 4);
   // sharded group lists (raft_device.hpp): NSHARD shards of scap entries
   const uint64_t scap = ((Gp / 256 + NSHARD - 1) / NSHARD) * 256;
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < NWORK; ++q) {
     A(reinterpret_cast<void**>(&e->work[q]), NSHARD * scap * 4);
     A(reinterpret_cast<void**>(&e->work_tick[q]), NSHARD * scap * 4);
   }
   A(reinterpret_cast<void**>(&e->wcount), WCOUNT_WORDS * 4);
-  A(reinterpret_cast<void**>(&e->blist), NSHARD * scap * 4);
+  for (int q = 0; q < 3; ++q) A(reinterpret_cast<void**>(&e->blist[q]), NSHARD * scap * 4);
+  A(reinterpret_cast<void**>(&e->P.glst), Gp);
   A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.log_value), R * K * Gp * 8);
   if (c.payload_crc) A(reinterpret_cast<void**>(&e->P.log_crc), R * K * Gp * 4);
@@ -487,7 +499,10 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (rc == RAFT_OK) {
     hipError_t h = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (h == hipSuccess) h = hipStreamCreateWithFlags(&e->gen_stream, hipStreamNonBlocking);
+    if (h == hipSuccess) h = hipStreamCreateWithFlags(&e->list_stream, hipStreamNonBlocking);
     for (int q = 0; q < 2 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->gen_ev[q], hipEventDisableTiming);
+    for (int q = 0; q < 2 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->ev_lean[q], hipEventDisableTiming);
+    for (int q = 0; q < 4 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->ev_list[q], hipEventDisableTiming);
     if (h != hipSuccess) rc = fail(RAFT_EHIP, "hipStreamCreate / hipEventCreate: %s", hipGetErrorString(h));
   }
   if (rc != RAFT_OK) {
@@ -513,6 +528,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
   if (const char* dl = getenv("RAFTSTEP_DIAG_LEAN")) e->P.diag = uint32_t(atoi(dl));
   if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = atoi(og) != 0;
+  if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = atoi(pp) != 0;
   e->P.dbg_pass = 0xFFFFFFFFu;
   if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
     e->diag_print = 1;
@@ -535,6 +551,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(e->P.gmeta), uint16_t(NO_PRIMARY), Gp,
                                            e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.giso, 0, Gp, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.glst, 0, Gp, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gss, 0, Gp * sizeof(SsRec), e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.glx, 0, Gp * sizeof(LxRec), e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grot, 0, Gp * 2, e->stream) : z;
@@ -567,9 +584,15 @@ int raft_engine_destroy(raft_engine* e) {
   for (hipEvent_t x : e->comm_ev) (void)hipEventDestroy(x);
   if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
   if (e->gen_stream) (void)hipStreamSynchronize(e->gen_stream);
+  if (e->list_stream) (void)hipStreamSynchronize(e->list_stream);
   for (hipEvent_t x : e->gen_ev)
     if (x) (void)hipEventDestroy(x);
+  for (hipEvent_t x : e->ev_lean)
+    if (x) (void)hipEventDestroy(x);
+  for (hipEvent_t x : e->ev_list)
+    if (x) (void)hipEventDestroy(x);
   if (e->gen_stream) (void)hipStreamDestroy(e->gen_stream);
+  if (e->list_stream) (void)hipStreamDestroy(e->list_stream);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->hist) (void)hipFree(e->hist);
   if (e->tstat) (void)hipFree(e->tstat);
@@ -915,6 +938,9 @@ static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1, const Ca
   return RAFT_OK;
 }
 
+// Counters of two-pass list q (of 3).
+static uint32_t* lcount(raft_engine* e, uint32_t q) { return e->wcount + (NWORK + q) * SHARD_WORDS; }
+
 // Join of an overlapped general kernel (see raft_engine::overlap_general):
 // the engine stream waits for gen_stream, the window tail clears the
 // window's DEFER flags and zeroes its worklist, its ticks' records are reduced.
@@ -947,6 +973,10 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   e->n_ticks += nticks;
   if (skip_list) e->n_skip_ticks += nticks;
   const bool two = e->two_pass && !e->force_general && !e->write_through;
+  const bool pipe = two && !skip_list && e->pipeline && !e->debug_work;
+  // every call that runs list kernels starts with the lists' counters zeroed
+  // (a pipelined call's last list kernel leaves the carried list's count)
+  if (two && !skip_list) HIPCHK(hipMemsetAsync(lcount(e, 0), 0, size_t(NLISTS) * SHARD_WORDS * 4, e->stream));
   uint32_t stats_first = 0;   // first tick (index in this call) whose records are not reduced yet
   hipEvent_t ra = nullptr, rb = nullptr;
   if (e->prof == 2) {
@@ -961,7 +991,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     unsigned long long* st = stats ? e->hist + size_t(i) * STAT_SLOTS * NSTAT : nullptr;
     // worklist counter of this window; zeroed by the previous general kernel
     // (or at engine creation), so no per-call memset
-    uint32_t* cnt = e->wcount + (e->wpar & 1) * SHARD_WORDS;
+    uint32_t* cnt = e->wcount + (e->wpar % NWORK) * SHARD_WORDS;
     hipEvent_t a = nullptr, b = nullptr;
     if (e->prof == 1) {
       a = next_event(e);
@@ -969,7 +999,39 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
     }
     const int force = e->force_general;
-    if (two) {
+    if (pipe) {
+      // lean(t) appends to list L; list(t) reads it, zeroes list L+2 (last
+      // read by list(t-1), next filled by lean(t+2), which waits for list(t))
+      const uint32_t L = e->lpar % 3;
+      const bool carry = i + 1 < nticks;   // list(t) runs its groups through t+1 too
+      const int lflags = (i > 0 ? 1 : 0) | (carry ? 2 : 0);
+      hipEvent_t c = nullptr, d = nullptr;
+      if (e->prof == 3) {
+        c = next_event(e);
+        d = next_event(e);
+        if (!c || !d) return fail(RAFT_EHIP, "hipEventCreate failed");
+      }
+      if (i >= 2) HIPCHK(hipStreamWaitEvent(e->stream, e->ev_list[(i - 2) & 3], 0));   // carried its groups through t-1
+      HIPCHK(launch_tick_lean(e->R, int(e->cfg.semantics), e->P, T, st, e->blist[L], lcount(e, L), lflags, e->stream,
+                              a, b));
+      HIPCHK(hipEventRecord(e->ev_lean[i & 1], e->stream));
+      HIPCHK(hipStreamWaitEvent(e->list_stream, e->ev_lean[i & 1], 0));
+      ListNext nx{};
+      if (carry) {   // tick t+1: its stats record, the worklist of its window
+        const int np = int((e->wpar + ((i + 1) % e->slow_every == 0 ? 1u : 0u)) % NWORK);
+        nx = ListNext{stats ? st + size_t(STAT_SLOTS) * NSTAT : nullptr, e->work[np], e->work_tick[np],
+                      e->wcount + np * SHARD_WORDS};
+      }
+      // (the call's last list kernel zeroes nothing: list L+2 then still
+      // counts the groups list(t-1) carried into this tick, which the
+      // end-of-call check counts as listed at the last tick; every pipelined
+      // call starts with the three lists' counters zeroed)
+      HIPCHK(launch_tick_list(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar % NWORK], e->work_tick[e->wpar % NWORK],
+                              cnt, e->blist[L], lcount(e, L), carry ? lcount(e, (L + 2) % 3) : nullptr,
+                              carry ? &nx : nullptr, e->list_stream, c, d));
+      HIPCHK(hipEventRecord(e->ev_list[i & 3], e->list_stream));
+      ++e->lpar;
+    } else if (two) {
       // lean pass appends to list counter lpar, the list pass zeroes the other one
       hipEvent_t c = nullptr, d = nullptr;
       if (e->prof == 3 && !skip_list) {
@@ -977,15 +1039,14 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         d = next_event(e);
         if (!c || !d) return fail(RAFT_EHIP, "hipEventCreate failed");
       }
-      HIPCHK(launch_tick_two_pass(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar & 1],
-                                  e->work_tick[e->wpar & 1], cnt, e->blist,
-                                  e->wcount + (2 + (e->lpar & 1)) * SHARD_WORDS,
-                                  e->wcount + (2 + ((e->lpar + 1) & 1)) * SHARD_WORDS, e->stream, a, b,
-                                  c, d, skip_list));
+      const uint32_t L = e->lpar % 3;
+      HIPCHK(launch_tick_two_pass(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar % NWORK],
+                                  e->work_tick[e->wpar % NWORK], cnt, e->blist[L], lcount(e, L), lcount(e, (L + 2) % 3),
+                                  e->stream, a, b, c, d, skip_list));
       ++e->lpar;
     } else {
-      HIPCHK(launch_tick_fast(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar & 1],
-                              e->work_tick[e->wpar & 1], cnt, force,
+      HIPCHK(launch_tick_fast(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar % NWORK],
+                              e->work_tick[e->wpar % NWORK], cnt, force,
                               e->write_through, e->stream, a, b));
     }
     // the previous window's general kernel, overlapped with this tick's fast
@@ -1004,15 +1065,22 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         fprintf(stderr, "raftstep: general kernel ticks %lld..%lld worklist %u\n", (long long)win_first, (long long)t, nw);
       }
       const bool last = i + 1 == nticks;
-      const int par = int(e->wpar & 1);
+      const int par = int(e->wpar % NWORK);
+      // pipelined: the window's deferrals are complete once list(t) is done
+      // (its second step, tick t+1, defers to the next window's worklist)
+      hipStream_t after = pipe ? e->list_stream : e->stream;
       // (with the list skipped nothing can be deferred — only the list kernel
       // defers — so both worklists stay empty and there is nothing to catch up)
-      const bool overlap = !skip_list && two && e->overlap_general && !last && !e->debug_work;
+      // (pipelined, a window's general kernel must run through tick t+1 and
+      // its tail come after the lean kernel of t+1, which leaves the groups
+      // list(t) passed on alone even when list(t) deferred them at tick t:
+      // so the pipeline always takes this form)
+      const bool overlap = !skip_list && two && (e->overlap_general || pipe) && !last && !e->debug_work;
       if (overlap) {
         // beside tick t+1's lean and list kernels, through tick t+1 (its groups
         // keep DEFER, so those kernels leave them alone; tick t+1's deferrals
         // go to the other worklist)
-        HIPCHK(hipEventRecord(e->gen_ev[0], e->stream));
+        HIPCHK(hipEventRecord(e->gen_ev[0], after));
         HIPCHK(hipStreamWaitEvent(e->gen_stream, e->gen_ev[0], 0));
         HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t + 1,
                                 stats ? e->hist : nullptr, e->work[par], e->work_tick[par], cnt, nullptr,
@@ -1024,6 +1092,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         e->gen_w1 = i;
         ++e->n_general;
       } else if (!skip_list) {
+        if (pipe) HIPCHK(hipStreamWaitEvent(e->stream, e->ev_list[i & 3], 0));
         HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t,
                                 stats ? e->hist : nullptr, e->work[par], e->work_tick[par], cnt, nullptr,
                                 e->lane_general, e->stream));
@@ -1054,7 +1123,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (!stats && skip_list) {
     // no readback in this call: the check record goes to tstat[cap + 1] and
     // its pinned copy is verified by the next call (settle_check)
-    const CallCheck chk{e->wcount, int((e->wpar + 1) & 1), 1, e->tstat + size_t(e->hist_cap + 1) * NSTAT};
+    const CallCheck chk{e->wcount, int((e->wpar + NWORK - 1) % NWORK), 1, e->tstat + size_t(e->hist_cap + 1) * NSTAT};
     HIPCHK(launch_stats_reduce(nullptr, nullptr, 0, e->stream, &chk));
     const size_t off = size_t(e->hist_cap + 1) * NSTAT;
     HIPCHK(hipMemcpyAsync(e->hrb + off, e->tstat + off, NSTAT * 8, hipMemcpyDeviceToHost, e->stream));

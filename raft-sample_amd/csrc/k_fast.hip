@@ -38,6 +38,15 @@ template <typename T>
 __device__ __forceinline__ void ring_st(T* base, uint32_t idx, T v) {
   __builtin_nontemporal_store(v, &base[idx]);
 }
+// Ring loads of the list / one-pass kernels: the entries may have been
+// written earlier in the same kernel (a carried group's first step, another
+// lane's copy) with non-temporal stores, which do not refresh the CU's L1,
+// so the loads bypass L1 (agent-scope relaxed: global_load ... sc1, served
+// by the XCD's L2, which holds those stores).
+template <typename T>
+__device__ __forceinline__ T ring_ld(const T* base, uint32_t idx) {
+  return __hip_atomic_load(&base[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <bool WT, typename T>
 __device__ __forceinline__ void rst(T* base, uint32_t idx, T v) {
   if constexpr (WT) st<true>(base, idx, v);
@@ -708,8 +717,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       const uint32_t o1 = ring_in_tile(g, R, ring_slot(L0 + 1, rot, rota, rotb, sbo, sb2, P.kmask), 0u);
       const int32_t* const rt = P.log_term + tb;
       const int nx0 = at(prow(P.xnext, sr * R + p0, P.Gp), g);
-      const int tc0 = at(rt, o0 + uint32_t(c)), ts0 = at(rt, o0 + uint32_t(sr));
-      const int tc1 = at(rt, o1 + uint32_t(c)), ts1 = at(rt, o1 + uint32_t(sr));
+      const int tc0 = ring_ld(rt, o0 + uint32_t(c)), ts0 = ring_ld(rt, o0 + uint32_t(sr));
+      const int tc1 = ring_ld(rt, o1 + uint32_t(c)), ts1 = ring_ld(rt, o1 + uint32_t(sr));
       // sr's own round (sr < c) reaches p0 before it learns the higher term:
       // r_leader_round's NextIndex / prevLogTerm checks on sr's row must not fault
       if (sr < c) bail |= nx0 < 1 || nx0 > ls + n + 1 || (nx0 >= 2 ? nx0 - 1 : 1) <= sr_hw - Kd;
@@ -1102,9 +1111,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             osrc = ring_in_tile(gg, R, uint32_t(idx - 1 + int(rr)) & P.kmask, mcol);
             odst = ring_in_tile(gg, R, uint32_t(idx - 1 + int(rr) + dd) & P.kmask, mcol);
           }
-          ct[k] = at(P.log_term + tb, osrc);
-          cv[k] = at(P.log_value + tb, osrc);
-          if constexpr (CRC) cc[k] = at(P.log_crc + tb, osrc);
+          ct[k] = ring_ld(P.log_term + tb, osrc);
+          cv[k] = ring_ld(P.log_value + tb, osrc);
+          if constexpr (CRC) cc[k] = ring_ld(P.log_crc + tb, osrc);
           cdst[k] = odst;
           ctb[k] = tb;
         }
@@ -1310,7 +1319,7 @@ template <int R, bool WT, bool CRC, int SEM, int LB>
 __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, unsigned long long* stats,
                                                         uint32_t* work, int32_t* work_tick, uint32_t* work_count,
                                                         const uint32_t* list, const uint32_t* count,
-                                                        uint32_t* next_count) {
+                                                        uint32_t* next_count, int steps, ListNext nx) {
   constexpr uint32_t RW = recw<R>();   // words per group record (16-B multiple)
   constexpr uint32_t RQ = RW / 4;      // 16-B pieces per record
   __shared__ uint32_t tab[CRC ? 2048 : 1];
@@ -1371,9 +1380,14 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
                            &P.gsb2[gs], &sglx[t], g};
     // (P.diag, timing only, results wrong: 32 = staging alone, 64 = staging and write-back, no tick)
     if (P.diag & 32u) { __syncthreads(); continue; }
-    const bool wrote = (P.diag & 64u) ? valid
-                                      : fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g,
-                                                                          tab, rw, gw);
+    bool wrote = (P.diag & 64u) ? valid
+                                : fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab,
+                                                                    rw, gw);
+    if (steps > 1) {   // the following tick too, on the staged state (pipelined tick)
+      __threadfence_block();   // this step's ring stores, seen by the next step's gathers
+      wrote |= fast_group<R, WT, CRC, SEM, true>(P, T.at_tick(T.tick + 1), nx.stats, nx.work, nx.work_tick,
+                                                 nx.work_count, 0, g, tab, rw, gw);
+    }
     {   // dirty rows -> the 16-B pieces of the record they touch
       const uint32_t rows = (valid && wrote) ? sdm[t] : 0u;
       uint32_t pm = 0;
@@ -1414,7 +1428,7 @@ template <int R, bool WT, bool CRC, int SEM>
 __global__ __launch_bounds__(256) void tick_list_plain_kernel(DevPlanes P, Trace T, unsigned long long* stats,
                                                               uint32_t* work, int32_t* work_tick, uint32_t* work_count,
                                                               const uint32_t* list, const uint32_t* count,
-                                                              uint32_t* next_count) {
+                                                              uint32_t* next_count, int steps, ListNext nx) {
   __shared__ uint32_t tab[CRC ? 2048 : 1];
   __shared__ uint32_t pre[NSHARD + 1];
   shard_zero(next_count);
@@ -1426,6 +1440,11 @@ __global__ __launch_bounds__(256) void tick_list_plain_kernel(DevPlanes P, Trace
     const uint32_t g = i < n ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
     fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab, rows_global<R>(P, g),
                                       words_global(P, g));
+    if (steps > 1) {
+      __threadfence_block();
+      fast_group<R, WT, CRC, SEM, true>(P, T.at_tick(T.tick + 1), nx.stats, nx.work, nx.work_tick, nx.work_count, 0, g,
+                                        tab, rows_global<R>(P, g), words_global(P, g));
+    }
     __syncthreads();   // the body's block reductions reuse their LDS words next round
   }
 }
@@ -1454,7 +1473,7 @@ __global__ __launch_bounds__(256) void tick_list_plain_kernel(DevPlanes P, Trace
 // (a drifted group: its own R-contiguous segment, or a ring segment switch).
 template <int R, bool CRC, int SEM>
 __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, unsigned long long* stats, uint32_t* list,
-                                                        uint32_t* count) {
+                                                        uint32_t* count, int lflags) {
   constexpr bool RAFT = SEM == SEM_RAFT;
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
   __shared__ uint32_t tab[CRC ? 2048 : 1];
@@ -1478,8 +1497,12 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   if (T.iso_p) im = iso_windows<R>(key, T, &act, &starting);
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
+    // pipelined tick: a group the last list kernel carries through this tick
+    // too is left alone (its state is being written beside this kernel)
+    const bool held = (lflags & 1) && at(P.glst, g) != 0;
+    if (held) at(P.glst, g) = uint8_t(0);
     const int c = meta & 0xF;
-    const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
+    const bool skip = held || (meta & M_DEFER) || ((meta >> 4) & 0xF);   // carried / pending catch-up / frozen group
     take = !skip && (meta & M_SSYNC) && c < R && g != P.dbg_pass;   // (test knob: pass one group on)
     pass = !skip && !take;
     df |= (!skip && g == P.dbg_pass) ? 1u << 24 : 0u;
@@ -1775,6 +1798,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     uint32_t off = k * P.scap + wbase + uint32_t(__popcll(bm & ((1ull << lane) - 1ull)));
     for (int w = 0; w < wave; ++w) off += wn[w];
     list[off] = g;
+    if (lflags & 2) at(P.glst, g) = uint8_t(1);   // the list kernel carries it through the next tick too
   }
   if (stats) {
     const int t = take ? 1 : 0;
@@ -1822,17 +1846,22 @@ hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, 
 }
 
 template <int R, bool CRC, int SEM>
-static void launch_two_pass_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
-                              int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
-                              uint32_t* next_count, hipStream_t s, hipEvent_t a, hipEvent_t b, hipEvent_t c,
-                              hipEvent_t d, bool skip_list) {
+static void launch_lean_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
+                          uint32_t* count, int lflags, hipStream_t s, hipEvent_t a, hipEvent_t b) {
+  hipExtLaunchKernelGGL(tick_lean_kernel<R, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, list,
+                        count, lflags);
+}
+
+template <int R, bool CRC, int SEM>
+static void launch_list_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                          int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
+                          uint32_t* next_count, const ListNext* next, hipStream_t s, hipEvent_t c, hipEvent_t d) {
   static const bool stage = [] {
     const char* v = getenv("RAFTSTEP_LIST_STAGE");
     return !v || atoi(v) != 0;
   }();
-  hipExtLaunchKernelGGL(tick_lean_kernel<R, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, list,
-                        count);
-  if (skip_list) return;   // the engine proved the list empty (engine.cpp, steady-state list skip)
+  const int steps = next ? 2 : 1;
+  const ListNext nx = next ? *next : ListNext{nullptr, nullptr, nullptr, nullptr};
   // list blocks of four waves (default); RAFTSTEP_LIST_BLOCK=64 for one-wave
   // blocks (no block barrier waits on another wave): the same list kernel
   // time on C4, but the following lean kernel measured 15% slower (A/B in
@@ -1845,18 +1874,28 @@ static void launch_two_pass_t(const DevPlanes& P, const Trace& T, unsigned long 
     const unsigned blocks = unsigned(
         std::min<uint64_t>((P.G + 63) / 64, resident_blocks(tick_list_kernel<R, false, CRC, SEM, 64>, 64)));
     hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM, 64>, dim3(blocks), dim3(64), 0, s, c, d, 0, P, T, stats,
-                          work, work_tick, work_count, list, count, next_count);
+                          work, work_tick, work_count, list, count, next_count, steps, nx);
   } else if (stage) {
     const unsigned blocks = unsigned(
         std::min<uint64_t>((P.G + 255) / 256, resident_blocks(tick_list_kernel<R, false, CRC, SEM, 256>, 256)));
     hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM, 256>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats,
-                          work, work_tick, work_count, list, count, next_count);
+                          work, work_tick, work_count, list, count, next_count, steps, nx);
   } else {
     const unsigned blocks = unsigned(
         std::min<uint64_t>((P.G + 255) / 256, resident_blocks(tick_list_plain_kernel<R, false, CRC, SEM>)));
     hipExtLaunchKernelGGL(tick_list_plain_kernel<R, false, CRC, SEM>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T,
-                          stats, work, work_tick, work_count, list, count, next_count);
+                          stats, work, work_tick, work_count, list, count, next_count, steps, nx);
   }
+}
+
+template <int R, bool CRC, int SEM>
+static void launch_two_pass_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                              int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
+                              uint32_t* next_count, hipStream_t s, hipEvent_t a, hipEvent_t b, hipEvent_t c,
+                              hipEvent_t d, bool skip_list) {
+  launch_lean_t<R, CRC, SEM>(P, T, stats, list, count, 0, s, a, b);
+  if (skip_list) return;   // the engine proved the list empty (engine.cpp, steady-state list skip)
+  launch_list_t<R, CRC, SEM>(P, T, stats, work, work_tick, work_count, list, count, next_count, nullptr, s, c, d);
 }
 hipError_t launch_tick_two_pass(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats,
                                 uint32_t* work, int32_t* work_tick, uint32_t* work_count, uint32_t* list,
@@ -1867,14 +1906,44 @@ hipError_t launch_tick_two_pass(int R, int sem, const DevPlanes& P, const Trace&
   if (sem == SEM_RAFT) {                                                                                           \
     RAFT_DISPATCH_R(R, (launch_two_pass_t<RR, CRC_, SEM_RAFT>(P, T, stats, work, work_tick, work_count, list, count, \
                                                               next_count, s, lean_start, lean_stop, list_start,      \
-                                                              list_stop, skip_list)))                                           \
+                                                              list_stop, skip_list)))                                \
   } else {                                                                                                         \
     RAFT_DISPATCH_R(R, (launch_two_pass_t<RR, CRC_, SEM_REF>(P, T, stats, work, work_tick, work_count, list, count,  \
                                                              next_count, s, lean_start, lean_stop, list_start,       \
-                                                             list_stop, skip_list)))                                            \
+                                                             list_stop, skip_list)))                                 \
   }
   if (crc) { RAFT_TWO(true); } else { RAFT_TWO(false); }
 #undef RAFT_TWO
+  return hipGetLastError();
+}
+hipError_t launch_tick_lean(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
+                            uint32_t* count, int lflags, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
+  const bool crc = P.crc_on != 0;
+#define RAFT_LEAN(CRC_)                                                                                          \
+  if (sem == SEM_RAFT) {                                                                                          \
+    RAFT_DISPATCH_R(R, (launch_lean_t<RR, CRC_, SEM_RAFT>(P, T, stats, list, count, lflags, s, ev_start, ev_stop))) \
+  } else {                                                                                                        \
+    RAFT_DISPATCH_R(R, (launch_lean_t<RR, CRC_, SEM_REF>(P, T, stats, list, count, lflags, s, ev_start, ev_stop)))  \
+  }
+  if (crc) { RAFT_LEAN(true); } else { RAFT_LEAN(false); }
+#undef RAFT_LEAN
+  return hipGetLastError();
+}
+hipError_t launch_tick_list(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                            int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
+                            uint32_t* next_count, const ListNext* next, hipStream_t s, hipEvent_t ev_start,
+                            hipEvent_t ev_stop) {
+  const bool crc = P.crc_on != 0;
+#define RAFT_LIST(CRC_)                                                                                          \
+  if (sem == SEM_RAFT) {                                                                                          \
+    RAFT_DISPATCH_R(R, (launch_list_t<RR, CRC_, SEM_RAFT>(P, T, stats, work, work_tick, work_count, list, count,   \
+                                                          next_count, next, s, ev_start, ev_stop)))                \
+  } else {                                                                                                        \
+    RAFT_DISPATCH_R(R, (launch_list_t<RR, CRC_, SEM_REF>(P, T, stats, work, work_tick, work_count, list, count,    \
+                                                         next_count, next, s, ev_start, ev_stop)))                 \
+  }
+  if (crc) { RAFT_LIST(true); } else { RAFT_LIST(false); }
+#undef RAFT_LIST
   return hipGetLastError();
 }
 

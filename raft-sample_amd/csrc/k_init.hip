@@ -152,15 +152,14 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
 // tick; lane = slot.
 // With a CallCheck, one more block (the last) writes the end-of-call check
 // record: the groups the lean kernel passed to the list at the call's last
-// tick (both list counters), the groups the last general window took, and —
+// tick (every list's counters), the groups the last general window took, and —
 // in a list-skipping call, where no list kernel consumed or zeroed them — the
 // list counters are zeroed so a later list kernel never reads stale entries.
 __device__ __forceinline__ void call_check_block(const CallCheck& c) {
   uint64_t listed = 0, deferred = 0;
   if (threadIdx.x < uint32_t(NSHARD)) {
     const uint32_t k = threadIdx.x * SHARD_STRIDE;
-    listed = uint64_t(c.wcount[2 * SHARD_WORDS + k]) + uint64_t(c.wcount[3 * SHARD_WORDS + k]);
-
+    for (int q = 0; q < NLISTS; ++q) listed += uint64_t(c.wcount[(NWORK + q) * SHARD_WORDS + k]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) listed += __shfl_xor(listed, o);
@@ -168,10 +167,8 @@ __device__ __forceinline__ void call_check_block(const CallCheck& c) {
   // list-skipping call defers nothing and runs no tail
   deferred = c.zero_lists ? 0u : c.wcount[WC_TAKEN + c.wlast];
   __syncthreads();   // every lane has read the counters before any is zeroed
-  if (c.zero_lists && threadIdx.x < uint32_t(NSHARD)) {
-    c.wcount[2 * SHARD_WORDS + threadIdx.x * SHARD_STRIDE] = 0u;
-    c.wcount[3 * SHARD_WORDS + threadIdx.x * SHARD_STRIDE] = 0u;
-  }
+  if (c.zero_lists && threadIdx.x < uint32_t(NSHARD))
+    for (int q = 0; q < NLISTS; ++q) c.wcount[(NWORK + q) * SHARD_WORDS + threadIdx.x * SHARD_STRIDE] = 0u;
   if (threadIdx.x < NSTAT) {
     const unsigned long long v = threadIdx.x == CHK_LISTED ? listed : threadIdx.x == CHK_DEFERRED ? deferred
                                  : threadIdx.x == CHK_MAGIC ? 0x5241465443484Bull : 0ull;

@@ -51,6 +51,24 @@ hipError_t launch_tick_two_pass(int R, int sem, const DevPlanes& P, const Trace&
                                 uint32_t* work, int32_t* work_tick, uint32_t* work_count, uint32_t* list,
                                 uint32_t* count, uint32_t* next_count, hipStream_t s, hipEvent_t lean_start,
                                 hipEvent_t lean_stop, hipEvent_t list_start, hipEvent_t list_stop, bool skip_list);
+// The two passes launched separately (the pipelined tick, engine.cpp):
+// lflags bit 0 = leave the groups marked in P.glst alone (and clear the
+// marks), bit 1 = mark the groups passed on. With `next` the list kernel
+// runs its groups through the following tick too (a second fast_group step
+// on the staged state; its stats and deferrals go to next's record and
+// worklist), so that the next lean kernel can run beside it.
+struct ListNext {
+  unsigned long long* stats;    // the following tick's stats slots
+  uint32_t* work;               // the worklist of the following tick's window
+  int32_t* work_tick;
+  uint32_t* work_count;
+};
+hipError_t launch_tick_lean(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
+                            uint32_t* count, int lflags, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop);
+hipError_t launch_tick_list(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
+                            int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
+                            uint32_t* next_count, const ListNext* next, hipStream_t s, hipEvent_t ev_start,
+                            hipEvent_t ev_stop);
 // General kernel: catches every worklisted group up to last_tick; zeroes
 // `next_count`. lane_per_group: the one-lane-per-group form (tick_slow_kernel)
 // instead of the replica-parallel one (tick_seg_kernel).

@@ -137,6 +137,8 @@ struct DevPlanes {
   uint32_t dbg_pass;   // test knob (raft_debug_force_pass): the lean kernel passes this group to the list (~0u: none)
   int32_t* rec;        // [Gp][NPL][R] group records holding every per-replica row above (see rix)
   uint32_t scap;       // capacity of one shard of a sharded group list (see below)
+  uint8_t* glst;       // [Gp] two-step list marks: 1 = passed by the last lean kernel to a list kernel that
+                       // also runs this tick for it (the lean kernel leaves the group alone and clears the mark)
   uint32_t diag;       // timing-only diagnostics (RAFTSTEP_DIAG_LEAN; results are wrong when set): 1 = drifted
                        // lanes of the lean kernel skip their ring writes, 2 = they write the wave's common row
                        // (list kernel: 32 = staging alone, 64 = no tick, 128 = no ring writes / copies)
@@ -155,11 +157,13 @@ struct DevPlanes {
 constexpr int NSHARD = 64;
 constexpr int SHARD_STRIDE = 16;   // u32 words between two shard counters
 constexpr int SHARD_WORDS = NSHARD * SHARD_STRIDE;
-// engine counter block (u32 words): worklist counters [2 parities][SHARD_WORDS],
-// two-pass list counters [2][SHARD_WORDS], then the window tail's words:
-// the total each parity's last tail took (WC_TAKEN + parity) and its
+// engine counter block (u32 words): worklist counters [NWORK windows][SHARD_WORDS],
+// two-pass list counters [NLISTS ticks][SHARD_WORDS], then the window tail's
+// words: the total each worklist's last tail took (WC_TAKEN + index) and its
 // blocks-done counter (WC_DONE)
-constexpr int WC_TAKEN = 4 * SHARD_WORDS;
+constexpr int NWORK = 3;
+constexpr int NLISTS = 3;
+constexpr int WC_TAKEN = (NWORK + NLISTS) * SHARD_WORDS;
 constexpr int WC_DONE = WC_TAKEN + 8;
 constexpr int WCOUNT_WORDS = WC_TAKEN + SHARD_STRIDE;
 __device__ __forceinline__ uint32_t shard_home(uint32_t g) { return (g >> 8) & uint32_t(NSHARD - 1); }
@@ -188,8 +192,8 @@ __device__ __forceinline__ uint32_t shard_locate(const uint32_t* pre, uint32_t s
     if (pre[k + step] <= i) k += step;
   return k * scap + (i - pre[k]);
 }
-__device__ __forceinline__ void shard_zero(uint32_t* cnt) {   // block 0, threads 0..NSHARD-1
-  if (blockIdx.x == 0 && threadIdx.x < uint32_t(NSHARD)) cnt[threadIdx.x * SHARD_STRIDE] = 0;
+__device__ __forceinline__ void shard_zero(uint32_t* cnt) {   // block 0, threads 0..NSHARD-1 (cnt null: nothing)
+  if (cnt && blockIdx.x == 0 && threadIdx.x < uint32_t(NSHARD)) cnt[threadIdx.x * SHARD_STRIDE] = 0;
 }
 
 // Ring phase segments. A group whose logs stop growing for L ticks (no

@@ -36,7 +36,9 @@ def test_forced_pass_is_exact_while_the_list_kernel_runs():
         assert list(e.tick(t, k)) == list(o.tick(t, k))
     H.assert_same_state(e.store_state(), o.store_state(), "forced pass, list kernel running")
     c = e.diag_read()
-    assert c["lean_forced"] == 15 and c["ticks_list_skipped"] == 0, c
+    # every tick the lean kernel either passes group 17 on or (pipelined tick)
+    # leaves it to the list kernel that carries it through that tick
+    assert c["lean_forced"] + c["lean_skipped"] == 15 and c["ticks_list_skipped"] == 0, c
 
 
 def test_skip_violation_fails_in_the_call_with_statistics():
