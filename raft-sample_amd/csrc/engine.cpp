@@ -138,7 +138,7 @@ struct raft_engine {
   // groups alone, P.glst marks) runs beside it; the lean kernel of t+2 waits
   // for it. Lists and their counters rotate over three sets: lean(t+1) fills
   // one while list(t) reads another and zeroes the third.
-  int pipeline = 0;
+  int pipeline = 1;
   hipStream_t list_stream = nullptr;
   hipEvent_t ev_lean[2] = {nullptr, nullptr};   // engine stream -> list_stream (list(t) after lean(t))
   hipEvent_t ev_list[4] = {nullptr, nullptr, nullptr, nullptr};   // list_stream -> engine stream (list(t) done)

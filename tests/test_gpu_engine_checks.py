@@ -37,8 +37,12 @@ def test_forced_pass_is_exact_while_the_list_kernel_runs():
     H.assert_same_state(e.store_state(), o.store_state(), "forced pass, list kernel running")
     c = e.diag_read()
     # every tick the lean kernel either passes group 17 on or (pipelined tick)
-    # leaves it to the list kernel that carries it through that tick
-    assert c["lean_forced"] + c["lean_skipped"] == 15 and c["ticks_list_skipped"] == 0, c
+    # leaves it to the list kernel that carries it through that tick (so at
+    # least every other tick, and every tick without the pipeline); the
+    # skipped lanes also hold every group of the first tick after
+    # init_steady, which the list kernel compresses and carries
+    assert c["lean_forced"] >= 8 and c["lean_forced"] + c["lean_skipped"] >= 15, c
+    assert c["ticks_list_skipped"] == 0, c
 
 
 def test_skip_violation_fails_in_the_call_with_statistics():
