@@ -48,7 +48,16 @@ def algorithmic_bytes(R, E, crc=False):
     return 25 + 37 * (R - 1) + 12 * E * R + (4 * E * R if crc else 0)
 
 
-def lean_bytes(R, E, crc=False, segmented=False):
+def fused_ticks(wl):
+    """Ticks per launch of the steady-state tick (engine.cpp raft_engine::fuse):
+    RAFTSTEP_FUSE (default 4) while the steady-state list skip holds — the
+    steady workloads without payload CRC — else 1."""
+    if wl.get("init") == "new" or wl["crc"] or os.environ.get("RAFTSTEP_TWO_PASS", "1") == "0":
+        return 1
+    return max(1, int(os.environ.get("RAFTSTEP_FUSE", "4")))
+
+
+def lean_bytes(R, E, crc=False, segmented=False, fuse=1):
     """Algorithmic bytes per group-step of tick_lean_kernel (the dominant
     kernel of the two-pass tick, k_fast.hip) in this engine's layout: a group
     in the compressed steady state (SSYNC) holds term / LastApplied / the
@@ -58,8 +67,10 @@ def lean_bytes(R, E, crc=False, segmented=False):
     segment boundary 4 B when the ring has 2K physical slots) and writes the
     record 16 B + hb 4 B + this tick's entries on all R replicas, 12 E R B
     (+4 E R with a CRC32C stamp). C2: 100 B; C4 shape (R=7, 2K slots): 128 B;
-    C5: 5160 B."""
-    return 20 + (4 if segmented else 0) + 20 + 12 * E * R + (4 * E * R if crc else 0)
+    C5: 5160 B. With `fuse` ticks per launch (tick_fused_kernel) the
+    record / meta / rotation / heartbeat bytes are moved once per launch:
+    40 / fuse + 12 E R (C2 at 4 ticks per launch: 70 B)."""
+    return (20 + (4 if segmented else 0) + 20) / fuse + 12 * E * R + (4 * E * R if crc else 0)
 
 
 # SURVEY.md §8(d) workloads runnable by this bench (per GPU)
@@ -308,7 +319,8 @@ def main():
     # the dominant kernel's algorithmic bytes in its own layout: the lean
     # kernel (compressed steady state) in the two-pass tick, else the
     # one-pass fast kernel with SURVEY §8(d)'s per-replica SoA accounting
-    B = lean_bytes(R, E, crc, segmented="iso" in wl and wl["iso"][0] > 0) if two_pass else B_survey
+    fuse = fused_ticks(wl)
+    B = lean_bytes(R, E, crc, segmented="iso" in wl and wl["iso"][0] > 0, fuse=fuse) if two_pass else B_survey
     avg_kernel_s = kernel_ms / 1e3 / max(kernel_launches, 1)    # steady-state kernel, kernel-exact
     avg_region_s = region_ms / 1e3 / max(region_launches, 1)    # all launches of a tick + gaps
     # C4REF: the lean kernel's algorithmic bytes are those of the live groups it
@@ -316,17 +328,23 @@ def main():
     units = G if live_value is None else live_value * elapsed / world / args.steps
     achieved = B * units / avg_kernel_s / 1e9
     workload = f"{wl_key}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}, K={K}"
-    traffic, traffic_src = load_pmc(workload, "tick_lean_kernel" if two_pass else "tick_fast_kernel")
+    kname = ("tick_fused_kernel" if fuse > 1 else "tick_lean_kernel") if two_pass else "tick_fast_kernel"
+    traffic, traffic_src = load_pmc(workload, kname)
+    if traffic and fuse > 1:   # (the passes count bytes per launch; the roofline is per tick)
+        traffic /= fuse
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "frac_measured": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
             "traffic_source": traffic_src,
             "bytes_per_group_step": B,
-            "bytes_accounting": ("tick_lean_kernel, compressed steady state (bench.py lean_bytes), every group "
-                                 "counted as taken by the lean pass" if two_pass else
+            "bytes_accounting": (("tick_fused_kernel, %d steady ticks per launch (bench.py lean_bytes)" % fuse
+                                  if fuse > 1 else
+                                  "tick_lean_kernel, compressed steady state (bench.py lean_bytes), every group "
+                                  "counted as taken by the lean pass") if two_pass else
                                  "SURVEY.md §8(d) B(R,E), per-replica SoA"),
+            "ticks_per_launch": fuse,
             "units_per_launch": units,
-            "kernel": "tick_lean_kernel" if two_pass else "tick_fast_kernel",
+            "kernel": ("tick_fused_kernel" if fuse > 1 else "tick_lean_kernel") if two_pass else "tick_fast_kernel",
             "avg_kernel_us": avg_kernel_s * 1e6, "kernel_launches": kernel_launches,
             "list_kernel_us": (list_ms * 1e3 / max(list_launches, 1)) if two_pass else None,
             "avg_region_us_per_tick": avg_region_s * 1e6,

@@ -139,6 +139,11 @@ struct raft_engine {
   // for it. Lists and their counters rotate over three sets: lean(t+1) fills
   // one while list(t) reads another and zeroes the third.
   int pipeline = 1;
+  // Fused steady ticks (RAFTSTEP_FUSE, default 4): while the steady-state list
+  // skip holds (and without payload CRC, whose per-follower verification the
+  // lean kernel does tick by tick), that many ticks run in one launch of
+  // tick_fused_kernel (k_fast.hip)
+  uint32_t fuse = 4;
   hipStream_t list_stream = nullptr;
   hipEvent_t ev_lean[2] = {nullptr, nullptr};   // engine stream -> list_stream (list(t) after lean(t))
   hipEvent_t ev_list[4] = {nullptr, nullptr, nullptr, nullptr};   // list_stream -> engine stream (list(t) done)
@@ -176,6 +181,7 @@ struct raft_engine {
   // 2 one event pair around each raft_tick call's launches (no per-launch cost)
   int prof = 0;
   std::vector<hipEvent_t> ev;
+  std::vector<uint32_t> ev_ticks;   // mode 1: ticks each event pair covers (fused steady ticks: several)
   size_t ev_used = 0;
   double prof_ms = 0.0;
   uint64_t prof_n = 0;
@@ -529,6 +535,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* dl = getenv("RAFTSTEP_DIAG_LEAN")) e->P.diag = uint32_t(atoi(dl));
   if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = atoi(og) != 0;
   if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = atoi(pp) != 0;
+  if (const char* fu = getenv("RAFTSTEP_FUSE")) e->fuse = uint32_t(std::max(1, atoi(fu)));
   e->P.dbg_pass = 0xFFFFFFFFu;
   if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
     e->diag_print = 1;
@@ -974,6 +981,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (skip_list) e->n_skip_ticks += nticks;
   const bool two = e->two_pass && !e->force_general && !e->write_through;
   const bool pipe = two && !skip_list && e->pipeline && !e->debug_work;
+  const uint32_t fuse = (two && skip_list && !e->cfg.payload_crc && e->prof != 3) ? e->fuse : 1u;
   // every call that runs list kernels starts with the lists' counters zeroed
   // (a pipelined call's last list kernel leaves the carried list's count)
   if (two && !skip_list) HIPCHK(hipMemsetAsync(lcount(e, 0), 0, size_t(NLISTS) * SHARD_WORDS * 4, e->stream));
@@ -993,13 +1001,22 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     // (or at engine creation), so no per-call memset
     uint32_t* cnt = e->wcount + (e->wpar % NWORK) * SHARD_WORDS;
     hipEvent_t a = nullptr, b = nullptr;
-    if (e->prof == 1) {
+    const bool fused = fuse > 1;
+    if (e->prof == 1 && (!fused || i % fuse == 0)) {
       a = next_event(e);
       b = next_event(e);
       if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
+      e->ev_ticks.push_back(fused ? std::min<uint32_t>(fuse, nticks - i) : 1u);
     }
     const int force = e->force_general;
-    if (pipe) {
+    if (fused) {
+      // fused steady ticks: one launch per `fuse` ticks (its first), stats of
+      // each tick in its own record; the list counters rotate per tick as usual
+      if (i % fuse == 0)
+        HIPCHK(launch_tick_fused(e->R, int(e->cfg.semantics), e->P, T, int(std::min<uint32_t>(fuse, nticks - i)), st,
+                                 e->blist[e->lpar % 3], lcount(e, e->lpar % 3), e->stream, a, b));
+      ++e->lpar;
+    } else if (pipe) {
       // lean(t) appends to list L; list(t) reads it, zeroes list L+2 (last
       // read by list(t-1), next filled by lean(t+2), which waits for list(t))
       const uint32_t L = e->lpar % 3;
@@ -1379,6 +1396,7 @@ int raft_profile_enable(raft_engine* e, int mode) {
   }
   e->prof = mode;
   e->ev_used = 0;
+  e->ev_ticks.clear();
   e->prof_ms = 0.0;
   e->prof_n = 0;
   return RAFT_OK;
@@ -1392,9 +1410,11 @@ int raft_profile_read(raft_engine* e, double* total_ms, uint64_t* launches) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, e->ev[i], e->ev[i + 1]));
     e->prof_ms += ms;
-    if (e->prof != 2) e->prof_n += 1;   // mode 2 counts launches as it records
+    if (e->prof != 2) e->prof_n += (e->prof == 1 && i / 2 < e->ev_ticks.size()) ? e->ev_ticks[i / 2] : 1u;   // mode 1: ticks
+    // (mode 2 counts ticks as it records)
   }
   e->ev_used = 0;
+  e->ev_ticks.clear();
   if (total_ms) *total_ms = e->prof_ms;
   if (launches) *launches = e->prof_n;
   return RAFT_OK;

@@ -1817,6 +1817,155 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   }
 }
 
+// Fused steady ticks (the steady-state list skip, engine.cpp): every live
+// group is proven compressed and takeable and no isolation or corruption is
+// configured, so the lean kernel's normal class is the whole tick of every
+// group, and `nt` consecutive ticks run in one launch: the record, ring
+// rotation and meta are read once, each tick's closed form (client append,
+// AppendEntries to every follower, responses, commit rule, heartbeat — see
+// tick_lean_kernel) is applied in registers and its entries are written as
+// whole ring rows, the tick's statistics go to its own record, and the
+// record and heartbeat are stored once after the last tick. Per group and
+// tick this moves the ring bytes (12·E·R) plus 1/nt of the record / meta /
+// rotation / heartbeat bytes. A group that stops being takeable at tick j
+// (which the skip's proof excludes) is stored as of tick j-1 and passed to
+// the list, which the end-of-call check turns into RAFT_EINTERNAL.
+template <int R, bool CRC, int SEM>
+__global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, int nt, unsigned long long* stats,
+                                                         uint32_t* list, uint32_t* count) {
+  constexpr bool RAFT = SEM == SEM_RAFT;
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  __shared__ uint32_t tab[CRC ? 2048 : 1];
+  stage_crc_tab<CRC>(P, tab);
+  const uint64_t key = group_key(T.seed, P.gbase + g);
+  bool live = false, pass = false;
+  int c = 0, rot = 0, L = 0, term = 0, cl = 0, cf = 0, done = 0;
+  SsRec s0{0, 0, 0, 0};
+  if (g < P.G) {
+    const int meta = at(P.gmeta, g);
+    c = meta & 0xF;
+    const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);
+    live = !skip && (meta & M_SSYNC) && c < R && !uses_glx(meta) && !(RAFT && (meta & M_HWX)) &&
+           g != P.dbg_pass;
+    pass = !skip && !live;
+    if (live) {
+      s0 = P.gss[g];
+      rot = at(P.grot, g);
+      L = s0.last; term = s0.term; cl = s0.cl; cf = s0.cf;
+    }
+  }
+  const int lane = threadIdx.x & 63;
+  const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g), P.KP, R);
+  int32_t* const rt = P.log_term + tb;
+  int64_t* const rv = P.log_value + tb;
+  uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
+  int k_src[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) k_src[k] = (k * 64 + lane) / R;
+  for (int j = 0; j < nt; ++j) {   // (wave-uniform)
+    const Trace Tj = T.at_tick(T.tick + j);
+    const int n = int(Tj.client_entries());
+    const int ph = int(Tj.entries_before(Tj.tick) & P.kmask);
+    // the lean kernel's normal class, in phase (init_steady puts every group there)
+    bool take = live && L > 0 && int64_t(L) + n <= I32MAX && n < int(P.K) && cl <= L + n &&
+                (n == 0 || ((L + rot) & int(P.kmask)) == ph);
+    if (live && !take) { pass = true; live = false; }
+    int committed = 0;
+    if (take) {
+      const int nl = L + n;
+      const int cl2 = (RAFT ? nl > cl : (2 * (R - 1) > R && nl > cl)) ? nl : cl;
+      cf = cl > cf ? cl : cf;
+      committed = cl2 - cl;
+      L = nl;
+      cl = cl2;
+      done = j + 1;
+    }
+    if (n && __ballot(take)) {   // this tick's entries as whole ring rows (holes for the other lanes)
+      const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(Tj.tick));
+      uint32_t cs = 0;
+      if constexpr (CRC) cs = crc_term_state(tab, term);
+      int k_term[R];
+      bool k_on[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        k_term[k] = __shfl(term, k_src[k]);
+        k_on[k] = __shfl(take ? 1 : 0, k_src[k]) != 0;
+      }
+      for (int e = 0; e < n; ++e) {
+        const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+        uint32_t stamp = 0;
+        if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+        const uint32_t row = uint32_t((ph + e) & int(P.kmask)) * 64u * R;
+        const int vlo = int(uint32_t(uint64_t(v))), vhi = int(uint32_t(uint64_t(v) >> 32));
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const int lo = __shfl(vlo, k_src[k]), hi = __shfl(vhi, k_src[k]);
+          uint32_t sk = 0;
+          if constexpr (CRC) sk = uint32_t(__shfl(int(stamp), k_src[k]));
+          if (k_on[k]) {
+            const uint32_t o = row + uint32_t(k * 64 + lane);
+            ring_st(rt, o, k_term[k]);
+            ring_st(rv, o, int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo)));
+            if constexpr (CRC) ring_st(rc, o, sk);
+          }
+        }
+      }
+    }
+    if (stats) {   // tick j's record
+      unsigned long long* st = stats + size_t(j) * STAT_SLOTS * NSTAT;
+      const int t1 = take ? 1 : 0;
+      if constexpr (RAFT) {
+        const int v[5] = {committed, t1 * (R - 1), 0, t1, 0};
+        const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
+        block_stats<5>(v, idx, st);
+      } else {
+        const int v[4] = {committed, t1 * (R - 1), 0, t1};
+        const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
+        block_stats<4>(v, idx, st);
+      }
+      __syncthreads();   // (block_stats' LDS words are reused by the next tick)
+    }
+  }
+  if (done) {   // the record and every follower's timer as of the last tick taken
+    if (L != s0.last || cl != s0.cl || cf != s0.cf) P.gss[g] = SsRec{L, term, cl, cf};
+    at(P.hb, g) = T.at_tick(T.tick + done - 1).now;
+  }
+  if (P.dbg) {   // diagnostics (lean kernel counters): lanes x ticks, compressed ticks taken, passed on
+    const uint64_t b0 = __ballot(g < P.G), b1 = __ballot(pass);
+    const long long tk = wave_sum(done);
+    if (lane == 0) {
+      atomicAdd(&P.dbg[10], (unsigned long long)(__popcll(b0) * uint64_t(nt)));
+      if (tk) atomicAdd(&P.dbg[18], (unsigned long long)tk);
+      if (b1) atomicAdd(&P.dbg[23], (unsigned long long)__popcll(b1));
+    }
+  }
+  // passed on (the skip's proof violated): one atomic per passing lane
+  if (pass) {
+    const uint32_t k = blockIdx.x & uint32_t(NSHARD - 1);
+    list[k * P.scap + atomicAdd(&count[k * SHARD_STRIDE], 1u)] = g;
+  }
+}
+
+template <int R, bool CRC, int SEM>
+static void launch_fused_t(const DevPlanes& P, const Trace& T, int nt, unsigned long long* stats, uint32_t* list,
+                           uint32_t* count, hipStream_t s, hipEvent_t a, hipEvent_t b) {
+  hipExtLaunchKernelGGL(tick_fused_kernel<R, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, nt, stats,
+                        list, count);
+}
+hipError_t launch_tick_fused(int R, int sem, const DevPlanes& P, const Trace& T, int nticks, unsigned long long* stats,
+                             uint32_t* list, uint32_t* count, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
+  const bool crc = P.crc_on != 0;
+#define RAFT_FUSED(CRC_)                                                                                        \
+  if (sem == SEM_RAFT) {                                                                                         \
+    RAFT_DISPATCH_R(R, (launch_fused_t<RR, CRC_, SEM_RAFT>(P, T, nticks, stats, list, count, s, ev_start, ev_stop))) \
+  } else {                                                                                                       \
+    RAFT_DISPATCH_R(R, (launch_fused_t<RR, CRC_, SEM_REF>(P, T, nticks, stats, list, count, s, ev_start, ev_stop)))  \
+  }
+  if (crc) { RAFT_FUSED(true); } else { RAFT_FUSED(false); }
+#undef RAFT_FUSED
+  return hipGetLastError();
+}
+
 template <int R, bool WT, bool CRC, int SEM>
 static void launch_fast_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                           int32_t* work_tick, uint32_t* work_count, int force_slow, hipStream_t s, hipEvent_t a,

@@ -63,6 +63,10 @@ struct ListNext {
   int32_t* work_tick;
   uint32_t* work_count;
 };
+// Fused steady ticks (steady-state list skip): nticks ticks of every
+// compressed steady group in one launch; stats of tick j at stats + j slots.
+hipError_t launch_tick_fused(int R, int sem, const DevPlanes& P, const Trace& T, int nticks, unsigned long long* stats,
+                             uint32_t* list, uint32_t* count, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop);
 hipError_t launch_tick_lean(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
                             uint32_t* count, int lflags, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop);
 hipError_t launch_tick_list(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,

@@ -22,24 +22,26 @@ def bench_line(f):
     return json.loads(open(os.path.join(src, f)).read().strip().splitlines()[-1])
 
 
-passes = {   # workload tag -> (bench line, pmc pass prefix, kernels)
-    "C2": ("bench_c2.json", "pmc_c2", ["tick_lean_kernel"]),
-    "C2_4M": ("bench_c2_4m.json", "pmc_c2_4m", ["tick_lean_kernel"]),
-    "C3": ("bench_c3.json", "pmc_c3", ["tick_lean_kernel"]),
+passes = {   # workload tag -> (bench line, pmc pass prefix, kernels); the first is the line's roofline kernel
+    "C2": ("bench_c2.json", "pmc_c2", ["tick_fused_kernel"]),
+    "C2_4M": ("bench_c2_4m.json", "pmc_c2_4m", ["tick_fused_kernel"]),
+    "C3": ("bench_c3.json", "pmc_c3", ["tick_fused_kernel"]),
     "C4": ("bench_c4.json", "pmc_c4", ["tick_lean_kernel", "tick_list_kernel", "tick_seg_kernel"]),
     "C5": ("bench_c5.json", "pmc_c5", ["tick_lean_kernel"]),
 }
 for tag, (bf, pre, kernels) in passes.items():
     line = bench_line(bf)
     for k in kernels:
-        out = os.path.join(ROOT, "profiles", f"pmc_{tag}.json" if k == "tick_lean_kernel" else f"pmc_{tag}_{k[5:]}.json")
+        main = k == kernels[0]
+        out = os.path.join(ROOT, "profiles", f"pmc_{tag}.json" if main else f"pmc_{tag}_{k[5:]}.json")
         cmd = [sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"),
                "--calib-fetch", os.path.join(src, "pmc_calib_fetch"), "--calib-write", os.path.join(src, "pmc_calib_write"),
                "--fetch", os.path.join(src, pre + "_fetch"), "--write", os.path.join(src, pre + "_write"),
                "--kernel", k, "--workload", line["config"]["workload"], "--commit", commit, "--out", out]
-        if k == "tick_lean_kernel":
+        if main:   # (bytes per tick x ticks per launch: the passes count per launch)
             r = line["roofline"]
-            cmd += ["--algorithmic-bytes", str(r["bytes_per_group_step"] * r["units_per_launch"])]
+            cmd += ["--algorithmic-bytes",
+                    str(r["bytes_per_group_step"] * r["units_per_launch"] * r.get("ticks_per_launch", 1))]
         subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL)
         d = json.load(open(out))
         print(f"{tag:6s} {k:18s} {d['hbm_bytes_per_launch'] / 1e6:9.1f} MB/launch", d.get("traffic_over_algorithmic", ""))
