@@ -72,3 +72,26 @@ def test_group_base_shards_are_invariant():
     parts = [lo.store_state(), hi.store_state()]
     joined = {k: np.concatenate([p[k] for p in parts]) for k in f}
     harness.assert_same_state(joined, f, "sharded")
+
+
+def test_fused_steady_ticks_with_communicator():
+    """The steady-state list skip with fused ticks (4 per launch) under a
+    single-rank communicator: per-window stats all-reduced on the side stream
+    equal the oracle's per-tick stats, calls of lengths that split the fused
+    launches and the 8-tick windows differently."""
+    from raftstep import Engine
+    import oracle
+    import harness
+    kw = dict(replicas=5, groups=5000, ring_depth=32, client_period=1, seed=0x5EED0003)
+    e, o = Engine(**kw), oracle.Oracle(**kw)
+    e.comm_init(1, 0, Engine.comm_unique_id())
+    e.init_steady(0, 0)
+    o.init_steady(0, 0)
+    t = 1
+    for k in (6, 10, 7, 21, 1, 16):   # the first proves the list empty; the rest skip it and fuse
+        assert list(e.tick(t, k)) == list(o.tick(t, k)), f"ticks [{t}, {t + k})"
+        recs = e.tick_records(k)
+        t += k
+        assert recs[:, 0].tolist() == [5000] * k   # every tick commits one entry per group
+    harness.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")
+    assert e.comm_info()[2] > 0
