@@ -50,11 +50,11 @@ def algorithmic_bytes(R, E, crc=False):
 
 def fused_ticks(wl):
     """Ticks per launch of the steady-state tick (engine.cpp raft_engine::fuse):
-    RAFTSTEP_FUSE (default 4) while the steady-state list skip holds — the
+    RAFTSTEP_FUSE (default 16) while the steady-state list skip holds — the
     steady workloads without payload CRC — else 1."""
     if wl.get("init") == "new" or wl["crc"] or os.environ.get("RAFTSTEP_TWO_PASS", "1") == "0":
         return 1
-    return max(1, int(os.environ.get("RAFTSTEP_FUSE", "4")))
+    return max(1, int(os.environ.get("RAFTSTEP_FUSE", "16")))
 
 
 def lean_bytes(R, E, crc=False, segmented=False, fuse=1):

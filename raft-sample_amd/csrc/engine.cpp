@@ -139,11 +139,11 @@ struct raft_engine {
   // for it. Lists and their counters rotate over three sets: lean(t+1) fills
   // one while list(t) reads another and zeroes the third.
   int pipeline = 1;
-  // Fused steady ticks (RAFTSTEP_FUSE, default 4): while the steady-state list
+  // Fused steady ticks (RAFTSTEP_FUSE, default 16): while the steady-state list
   // skip holds (and without payload CRC, whose per-follower verification the
   // lean kernel does tick by tick), that many ticks run in one launch of
   // tick_fused_kernel (k_fast.hip)
-  uint32_t fuse = 4;
+  uint32_t fuse = 16;
   hipStream_t list_stream = nullptr;
   hipEvent_t ev_lean[2] = {nullptr, nullptr};   // engine stream -> list_stream (list(t) after lean(t))
   hipEvent_t ev_list[4] = {nullptr, nullptr, nullptr, nullptr};   // list_stream -> engine stream (list(t) done)
