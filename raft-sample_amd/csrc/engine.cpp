@@ -127,6 +127,7 @@ struct raft_engine {
   uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
   int write_through = 0;        // fast kernel stores with sc1 (write-through) instead of write-back
   int debug_work = 0;           // RAFTSTEP_DEBUG_WORK: print each general-kernel worklist size
+  int debug_pipe = 0;           // RAFTSTEP_DEBUG_PIPE: print each call's pipeline choice
   // two-pass tick (RAFTSTEP_TWO_PASS, default on): the lean kernel takes the
   // compressed steady groups, the list kernel every other live group
   int two_pass = 1;
@@ -138,7 +139,12 @@ struct raft_engine {
   // groups alone, P.glst marks) runs beside it; the lean kernel of t+2 waits
   // for it. Lists and their counters rotate over three sets: lean(t+1) fills
   // one while list(t) reads another and zeroes the third.
+  // RAFTSTEP_PIPELINE=2 (auto) pipelines a call only while the previous
+  // call's last tick listed at most pipe_max_list groups per 65536: a large
+  // list's two-step list kernel outlasts the lean kernel it runs beside (C4R).
   int pipeline = 1;
+  uint32_t pipe_max_list = 1024;   // RAFTSTEP_PIPELINE_MAX_LIST, groups per 65536
+  uint64_t last_list = 0;          // the previous call's check record, CHK_LAST_LIST
   // Fused steady ticks (RAFTSTEP_FUSE, default 16): while the steady-state list
   // skip holds (and without payload CRC, whose per-follower verification the
   // lean kernel does tick by tick), that many ticks run in one launch of
@@ -531,10 +537,12 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* se = getenv("RAFTSTEP_SLOW_EVERY")) e->slow_every = std::max(1, atoi(se));
   if (const char* wt = getenv("RAFTSTEP_WRITE_THROUGH")) e->write_through = atoi(wt) != 0;
   if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
+  if (const char* dp = getenv("RAFTSTEP_DEBUG_PIPE")) e->debug_pipe = atoi(dp) != 0;
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
   if (const char* dl = getenv("RAFTSTEP_DIAG_LEAN")) e->P.diag = uint32_t(atoi(dl));
   if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = atoi(og) != 0;
-  if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = atoi(pp) != 0;
+  if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = std::min(2, std::max(0, atoi(pp)));
+  if (const char* pm = getenv("RAFTSTEP_PIPELINE_MAX_LIST")) e->pipe_max_list = uint32_t(std::max(0, atoi(pm)));
   if (const char* fu = getenv("RAFTSTEP_FUSE")) e->fuse = uint32_t(std::max(1, atoi(fu)));
   e->P.dbg_pass = 0xFFFFFFFFu;
   if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
@@ -980,7 +988,12 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   e->n_ticks += nticks;
   if (skip_list) e->n_skip_ticks += nticks;
   const bool two = e->two_pass && !e->force_general && !e->write_through;
-  const bool pipe = two && !skip_list && e->pipeline && !e->debug_work;
+  const bool pipe = two && !skip_list && !e->debug_work &&
+                    (e->pipeline == 1 ||
+                     (e->pipeline == 2 && e->last_list * 65536ull <= uint64_t(e->pipe_max_list) * e->cfg.groups));
+  if (e->debug_pipe)
+    fprintf(stderr, "raftstep: ticks %lld..%lld pipeline %d (last call's last list %llu)\n", (long long)first_tick,
+            (long long)(first_tick + nticks - 1), int(pipe), (unsigned long long)e->last_list);
   const uint32_t fuse = (two && skip_list && !e->cfg.payload_crc && e->prof != 3) ? e->fuse : 1u;
   // every call that runs list kernels starts with the lists' counters zeroed
   // (a pipelined call's last list kernel leaves the carried list's count)
@@ -1121,7 +1134,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       // window's once its general kernel has joined; with the list skipped on
       // one GPU nothing overlaps them, so one reduce at the end of the call
       // covers every tick. The last one carries the check record.
-      const CallCheck chk{e->wcount, par, skip_list ? 1 : 0, e->tstat + size_t(nticks) * NSTAT};
+      const CallCheck chk{e->wcount, par, skip_list ? 1 : 0, e->tstat + size_t(nticks) * NSTAT, int((e->lpar + 2) % 3)};
       if (stats && !overlap && (!skip_list || e->comm || last))
         if (int rc = flush_window_stats(e, stats_first, i, (last && two) ? &chk : nullptr)) return rc;
       if (!skip_list || e->comm || last) stats_first = i + 1;
@@ -1140,7 +1153,8 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (!stats && skip_list) {
     // no readback in this call: the check record goes to tstat[cap + 1] and
     // its pinned copy is verified by the next call (settle_check)
-    const CallCheck chk{e->wcount, int((e->wpar + NWORK - 1) % NWORK), 1, e->tstat + size_t(e->hist_cap + 1) * NSTAT};
+    const CallCheck chk{e->wcount, int((e->wpar + NWORK - 1) % NWORK), 1, e->tstat + size_t(e->hist_cap + 1) * NSTAT,
+                        int((e->lpar + 2) % 3)};
     HIPCHK(launch_stats_reduce(nullptr, nullptr, 0, e->stream, &chk));
     const size_t off = size_t(e->hist_cap + 1) * NSTAT;
     HIPCHK(hipMemcpyAsync(e->hrb + off, e->tstat + off, NSTAT * 8, hipMemcpyDeviceToHost, e->stream));
@@ -1197,6 +1211,7 @@ int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_sta
       // steady-state list skip: proven for the next call when nothing was
       // listed at the last tick and the last general window took nothing
       if (e->steady_origin) e->steady_ok = c[CHK_LISTED] == 0 && c[CHK_DEFERRED] == 0;
+      e->last_list = c[CHK_LAST_LIST];
     }
   }
   return RAFT_OK;

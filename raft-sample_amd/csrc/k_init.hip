@@ -156,13 +156,20 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
 // in a list-skipping call, where no list kernel consumed or zeroed them — the
 // list counters are zeroed so a later list kernel never reads stale entries.
 __device__ __forceinline__ void call_check_block(const CallCheck& c) {
-  uint64_t listed = 0, deferred = 0;
+  uint64_t listed = 0, deferred = 0, last = 0;
   if (threadIdx.x < uint32_t(NSHARD)) {
     const uint32_t k = threadIdx.x * SHARD_STRIDE;
-    for (int q = 0; q < NLISTS; ++q) listed += uint64_t(c.wcount[(NWORK + q) * SHARD_WORDS + k]);
+    for (int q = 0; q < NLISTS; ++q) {
+      const uint64_t n = c.wcount[(NWORK + q) * SHARD_WORDS + k];
+      listed += n;
+      if (q == c.llast) last = n;
+    }
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) listed += __shfl_xor(listed, o);
+  for (int o = 32; o > 0; o >>= 1) {
+    listed += __shfl_xor(listed, o);
+    last += __shfl_xor(last, o);
+  }
   // what the last window tail took (its counters are zeroed by then); a
   // list-skipping call defers nothing and runs no tail
   deferred = c.zero_lists ? 0u : c.wcount[WC_TAKEN + c.wlast];
@@ -171,6 +178,7 @@ __device__ __forceinline__ void call_check_block(const CallCheck& c) {
     for (int q = 0; q < NLISTS; ++q) c.wcount[(NWORK + q) * SHARD_WORDS + threadIdx.x * SHARD_STRIDE] = 0u;
   if (threadIdx.x < NSTAT) {
     const unsigned long long v = threadIdx.x == CHK_LISTED ? listed : threadIdx.x == CHK_DEFERRED ? deferred
+                                 : threadIdx.x == CHK_LAST_LIST ? last
                                  : threadIdx.x == CHK_MAGIC ? 0x5241465443484Bull : 0ull;
     c.out[threadIdx.x] = v;
   }

@@ -88,14 +88,17 @@ hipError_t launch_digest(int R, const DevPlanes& P, int raft, uint64_t* per_grou
 // End-of-call check record (one more block of the stats reduce launch):
 // out[CHK_LISTED] = groups on the two-pass list counters (both parities),
 // out[CHK_DEFERRED] = groups the last general window's worklist held,
+// out[CHK_LAST_LIST] = groups on list llast alone (what the lean kernel passed
+// on at the call's last tick; the engine's pipeline choice, RAFTSTEP_PIPELINE=2),
 // out[CHK_MAGIC] = a constant proving the record was written this call.
 // zero_lists: zero both list counters afterwards (a list-skipping call).
-enum : int { CHK_LISTED = 0, CHK_DEFERRED = 1, CHK_MAGIC = 7 };
+enum : int { CHK_LISTED = 0, CHK_DEFERRED = 1, CHK_LAST_LIST = 2, CHK_MAGIC = 7 };
 struct CallCheck {
   uint32_t* wcount;             // the engine's counter block (raft_device.hpp WCOUNT_WORDS)
   int wlast;                    // parity of the worklist the last window tail took
   int zero_lists;
   unsigned long long* out;      // NSTAT words
+  int llast;                    // list set of the call's last tick
 };
 // Sums the STAT_SLOTS slots of nticks consecutive per-tick records of `hist`
 // into out[nticks][NSTAT] and zeroes those slots; with `chk` also writes the
