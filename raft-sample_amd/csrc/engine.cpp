@@ -139,9 +139,9 @@ struct raft_engine {
   // groups alone, P.glst marks) runs beside it; the lean kernel of t+2 waits
   // for it. Lists and their counters rotate over three sets: lean(t+1) fills
   // one while list(t) reads another and zeroes the third.
-  // RAFTSTEP_PIPELINE=2 (auto) pipelines a call only while the previous
-  // call's last tick listed at most pipe_max_list groups per 65536: a large
-  // list's two-step list kernel outlasts the lean kernel it runs beside (C4R).
+  // RAFTSTEP_PIPELINE=2 (A/B) pipelines a call only while the previous
+  // call's last tick listed at most pipe_max_list groups per 65536 (measured:
+  // no gain — the pipelined tick is faster on C4R's large lists too).
   int pipeline = 1;
   uint32_t pipe_max_list = 1024;   // RAFTSTEP_PIPELINE_MAX_LIST, groups per 65536
   uint64_t last_list = 0;          // the previous call's check record, CHK_LAST_LIST
