@@ -142,10 +142,10 @@ def engine_kwargs(wl, R, G, base, K, E, crc):
     return kw
 
 
-def load_pmc(workload, kernel):
+def load_pmc(workload, kernel, ticks=1):
     """HBM traffic per launch of the dominant kernel from the committed
-    rocprofv3 --pmc summary of exactly this workload and kernel
-    (profiles/pmc_*.json, made by tools/pmc_summary.py from FETCH_SIZE /
+    rocprofv3 --pmc summary of exactly this workload, kernel and ticks per
+    launch (profiles/pmc_*.json, made by tools/pmc_summary.py from FETCH_SIZE /
     WRITE_SIZE passes), and where it came from; (None, None) if no pass
     covers it."""
     import glob
@@ -154,7 +154,8 @@ def load_pmc(workload, kernel):
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if d.get("workload") == workload and d.get("kernel") == kernel and d.get("hbm_bytes_per_launch"):
+        if d.get("workload") == workload and d.get("kernel") == kernel and d.get("hbm_bytes_per_launch") and \
+                d.get("ticks_per_launch", 1) == ticks:
             src = f"{os.path.relpath(p, ROOT)} (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of this workload, " \
                   f"calibrated by tools/pmc_calib; not measured in this run" + \
                   (f"; build {d['commit']}" if d.get("commit") else "") + ")"
@@ -329,7 +330,7 @@ def main():
     achieved = B * units / avg_kernel_s / 1e9
     workload = f"{wl_key}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}, K={K}"
     kname = ("tick_fused_kernel" if fuse > 1 else "tick_lean_kernel") if two_pass else "tick_fast_kernel"
-    traffic, traffic_src = load_pmc(workload, kname)
+    traffic, traffic_src = load_pmc(workload, kname, fuse)
     if traffic and fuse > 1:   # (the passes count bytes per launch; the roofline is per tick)
         traffic /= fuse
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

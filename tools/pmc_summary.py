@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--workload", required=True)
     ap.add_argument("--algorithmic-bytes", type=float, default=None)
     ap.add_argument("--commit", default=None, help="git commit of the build the passes ran on")
+    ap.add_argument("--ticks-per-launch", type=int, default=1,
+                    help="ticks one launch of the kernel ran (tick_fused_kernel); bench.py matches on it")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -75,6 +77,7 @@ def main():
     }
     if a.algorithmic_bytes:
         out["traffic_over_algorithmic"] = (rd + wr) / a.algorithmic_bytes
+    out["ticks_per_launch"] = a.ticks_per_launch
     if a.commit:
         out["commit"] = a.commit
     json.dump(out, open(a.out, "w"), indent=1)

@@ -30,6 +30,9 @@ passes = {   # workload tag -> (bench line, pmc pass prefix, kernels); the first
     "C5": ("bench_c5.json", "pmc_c5", ["tick_lean_kernel"]),
 }
 for tag, (bf, pre, kernels) in passes.items():
+    if not os.path.exists(os.path.join(src, pre + "_write")):
+        print(f"{tag}: no PMC passes in {src}, kept as is")
+        continue
     line = bench_line(bf)
     for k in kernels:
         main = k == kernels[0]
@@ -37,7 +40,8 @@ for tag, (bf, pre, kernels) in passes.items():
         cmd = [sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"),
                "--calib-fetch", os.path.join(src, "pmc_calib_fetch"), "--calib-write", os.path.join(src, "pmc_calib_write"),
                "--fetch", os.path.join(src, pre + "_fetch"), "--write", os.path.join(src, pre + "_write"),
-               "--kernel", k, "--workload", line["config"]["workload"], "--commit", commit, "--out", out]
+               "--kernel", k, "--workload", line["config"]["workload"], "--commit", commit, "--out", out,
+               "--ticks-per-launch", str(line["roofline"].get("ticks_per_launch", 1) if main else 1)]
         if main:   # (bytes per tick x ticks per launch: the passes count per launch)
             r = line["roofline"]
             cmd += ["--algorithmic-bytes",
