@@ -145,7 +145,7 @@ def engine_kwargs(wl, R, G, base, K, E, crc):
 def load_pmc(workload, kernel, ticks=1):
     """HBM traffic per launch of the dominant kernel from the committed
     rocprofv3 --pmc summary of exactly this workload, kernel and ticks per
-    launch (profiles/pmc_*.json, made by tools/pmc_summary.py from FETCH_SIZE /
+    launch (mean over the pass's launches; profiles/pmc_*.json, made by tools/pmc_summary.py from FETCH_SIZE /
     WRITE_SIZE passes), and where it came from; (None, None) if no pass
     covers it."""
     import glob
@@ -155,7 +155,7 @@ def load_pmc(workload, kernel, ticks=1):
         except (OSError, ValueError):
             continue
         if d.get("workload") == workload and d.get("kernel") == kernel and d.get("hbm_bytes_per_launch") and \
-                d.get("ticks_per_launch", 1) == ticks:
+                abs(d.get("ticks_per_launch", 1) - ticks) < 1e-6:
             src = f"{os.path.relpath(p, ROOT)} (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of this workload, " \
                   f"calibrated by tools/pmc_calib; not measured in this run" + \
                   (f"; build {d['commit']}" if d.get("commit") else "") + ")"
@@ -321,7 +321,10 @@ def main():
     # kernel (compressed steady state) in the two-pass tick, else the
     # one-pass fast kernel with SURVEY §8(d)'s per-replica SoA accounting
     fuse = fused_ticks(wl)
-    B = lean_bytes(R, E, crc, segmented="iso" in wl and wl["iso"][0] > 0, fuse=fuse) if two_pass else B_survey
+    # a call of K ticks runs ceil(K / fuse) fused launches (K = 20: 16 + 4);
+    # the bytes moved once per launch are priced at the mean ticks per launch
+    tpl = args.steps / -(-args.steps // fuse) if fuse > 1 else 1
+    B = lean_bytes(R, E, crc, segmented="iso" in wl and wl["iso"][0] > 0, fuse=tpl) if two_pass else B_survey
     avg_kernel_s = kernel_ms / 1e3 / max(kernel_launches, 1)    # steady-state kernel, kernel-exact
     avg_region_s = region_ms / 1e3 / max(region_launches, 1)    # all launches of a tick + gaps
     # C4REF: the lean kernel's algorithmic bytes are those of the live groups it
@@ -330,20 +333,22 @@ def main():
     achieved = B * units / avg_kernel_s / 1e9
     workload = f"{wl_key}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}, K={K}"
     kname = ("tick_fused_kernel" if fuse > 1 else "tick_lean_kernel") if two_pass else "tick_fast_kernel"
-    traffic, traffic_src = load_pmc(workload, kname, fuse)
-    if traffic and fuse > 1:   # (the passes count bytes per launch; the roofline is per tick)
-        traffic /= fuse
+    traffic, traffic_src = load_pmc(workload, kname, tpl)
+    if traffic and fuse > 1:   # (the passes count bytes per launch, mean over launches; the roofline is per tick)
+        traffic /= tpl
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "frac_measured": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
             "traffic_source": traffic_src,
             "bytes_per_group_step": B,
-            "bytes_accounting": (("tick_fused_kernel, %d steady ticks per launch (bench.py lean_bytes)" % fuse
+            "bytes_accounting": (("tick_fused_kernel, up to %d steady ticks per launch, %.4g on average over this "
+                                  "call's launches (bench.py lean_bytes)" % (fuse, tpl)
                                   if fuse > 1 else
                                   "tick_lean_kernel, compressed steady state (bench.py lean_bytes), every group "
                                   "counted as taken by the lean pass") if two_pass else
                                  "SURVEY.md §8(d) B(R,E), per-replica SoA"),
-            "ticks_per_launch": fuse,
+            "ticks_per_launch": tpl,
+            "max_ticks_per_launch": fuse,
             "units_per_launch": units,
             "kernel": ("tick_fused_kernel" if fuse > 1 else "tick_lean_kernel") if two_pass else "tick_fast_kernel",
             "avg_kernel_us": avg_kernel_s * 1e6, "kernel_launches": kernel_launches,

@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--workload", required=True)
     ap.add_argument("--algorithmic-bytes", type=float, default=None)
     ap.add_argument("--commit", default=None, help="git commit of the build the passes ran on")
-    ap.add_argument("--ticks-per-launch", type=int, default=1,
+    ap.add_argument("--ticks-per-launch", type=float, default=1,
                     help="ticks one launch of the kernel ran (tick_fused_kernel); bench.py matches on it")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()

@@ -18,6 +18,13 @@ dst = os.path.join(ROOT, "profiles", "r03", name)
 os.makedirs(dst, exist_ok=True)
 
 
+def tpl(line):
+    """Mean ticks per launch of the line's calls (bench.py: --steps over ceil(steps / depth) launches)."""
+    r = line["roofline"]
+    t = r.get("max_ticks_per_launch", r.get("ticks_per_launch", 1))
+    return line["steps"] / -(-line["steps"] // t) if t > 1 else 1
+
+
 def bench_line(f):
     return json.loads(open(os.path.join(src, f)).read().strip().splitlines()[-1])
 
@@ -41,11 +48,15 @@ for tag, (bf, pre, kernels) in passes.items():
                "--calib-fetch", os.path.join(src, "pmc_calib_fetch"), "--calib-write", os.path.join(src, "pmc_calib_write"),
                "--fetch", os.path.join(src, pre + "_fetch"), "--write", os.path.join(src, pre + "_write"),
                "--kernel", k, "--workload", line["config"]["workload"], "--commit", commit, "--out", out,
-               "--ticks-per-launch", str(line["roofline"].get("ticks_per_launch", 1) if main else 1)]
-        if main:   # (bytes per tick x ticks per launch: the passes count per launch)
+               "--ticks-per-launch", str(tpl(line) if main else 1)]
+        if main:   # (bytes per tick x mean ticks per launch: the passes count per launch)
             r = line["roofline"]
-            cmd += ["--algorithmic-bytes",
-                    str(r["bytes_per_group_step"] * r["units_per_launch"] * r.get("ticks_per_launch", 1))]
+            t = r.get("ticks_per_launch", 1)
+            B = r["bytes_per_group_step"]
+            if "max_ticks_per_launch" not in r and t > 1:   # (older lines: priced at the full depth, 40 B per launch)
+                n = -(-line["steps"] // t)
+                B, t = B - 40 / t + 40 * n / line["steps"], line["steps"] / n
+            cmd += ["--algorithmic-bytes", str(B * r["units_per_launch"] * t)]
         subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL)
         d = json.load(open(out))
         print(f"{tag:6s} {k:18s} {d['hbm_bytes_per_launch'] / 1e6:9.1f} MB/launch", d.get("traffic_over_algorithmic", ""))
