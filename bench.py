@@ -3,8 +3,10 @@
 One step = one tick of every group: client append of E
 entries to the leader (main.go:327-329), one leader replication round to all
 R-1 peers through their AppendEntries handlers (main.go:334-379, 121-156),
-the commit rule (main.go:381-391) and the election timers — one fused kernel
-launch per tick, state read from and written back to HBM every tick.
+the commit rule (main.go:381-391) and the election timers. The headline
+(`value`, `ms_per_step`, `roofline`) is measured in §8(d)'s form: ONE TICK PER
+KERNEL LAUNCH (raft_config.ticks_per_launch = 1), every group's state read
+from and written back to HBM every tick.
 
 Workload at N=1: SURVEY config C2 — 2^20 independent 5-replica groups,
 steady-state AppendEntries + commitIndex, one client entry per tick, seeded
@@ -13,12 +15,21 @@ synthetic trace. For N>1 the default is SURVEY config C3: each rank owns
 data-path collective); the per-tick statistics are reduced on the device and
 summed across GPUs with RCCL on a side stream inside the engine.
 
+Also in the same line (N=1, default workload):
+  * `fused`: the same workload with up to 16 steady ticks per launch of
+    tick_fused_kernel (ticks_per_launch = 16; state kept in registers between
+    the ticks of a launch — NOT the §8(d) form, so never in `value` or
+    `roofline`), with its own kernel fraction;
+  * `extra_workloads`: SURVEY configs C4 (2^22 x 7 replicas, leader-isolation
+    churn, RAFT semantics) and C5 (E=64 with CRC32C), each timed with the same
+    protocol, with its own roofline and statistics check.
+
 Protocol: W untimed warm-up ticks, then the timed region of
 exactly K ticks (barrier + synchronize on both sides, max over ranks) is
 repeated --repeats times (default 5) and the median is reported. The
-roofline's `achieved` uses the steady-state kernel's own average duration,
-measured by HIP events attached to each of its dispatches (profile mode 1)
-in a separate, untimed pass of K ticks.
+roofline's `achieved` uses the dominant kernel's own average duration,
+measured by HIP events attached to each of its dispatches on the engine
+stream (profile mode 1) in a separate, untimed pass of K ticks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2|C3|C4|C4R|C4REF|C5]
 """
@@ -35,26 +46,43 @@ sys.path.insert(0, os.path.join(ROOT, "raft-sample_amd"))
 
 R_DEFAULT = 5
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FUSED_TICKS = 16        # ticks_per_launch of the `fused` block
+
+# Environment knobs the engine reads (engine.cpp raft_engine_create). The
+# bench records every RAFTSTEP_* variable it sees in config.engine_env and
+# refuses to run with a results-altering one.
+ENV_KNOBS = {
+    "RAFTSTEP_DIAG_LEAN": "results-altering (timing diagnostics; the engine refuses it without debug_flags)",
+    "RAFTSTEP_TWO_PASS": "exact: 0 = one-pass fast kernel (tests/test_gpu_parity.py)",
+    "RAFTSTEP_FORCE_GENERAL": "exact: every group through the general kernel (tests/test_gpu_parity.py)",
+    "RAFTSTEP_GENERAL": "exact: lane = one-lane-per-group general kernel (tests/test_gpu_tick_kat.py)",
+    "RAFTSTEP_SLOW_EVERY": "exact: general-kernel window (tests/test_gpu_pipeline.py, test_gpu_dist.py)",
+    "RAFTSTEP_PIPELINE": "exact: 0 = two passes in line (tests/test_gpu_pipeline.py)",
+    "RAFTSTEP_OVERLAP_GENERAL": "exact: 0 = general kernel in line (tests/test_gpu_pipeline.py)",
+    "RAFTSTEP_DEBUG_WORK": "exact: prints worklist sizes, synchronises (in-line form)",
+    "RAFTSTEP_DEBUG_PIPE": "exact: prints the pipeline choice",
+    "RAFTSTEP_DEBUG_FAST": "exact: prints class counters after every call (synchronising)",
+    "RAFTSTEP_LIB": "path of the library under test",
+    "RAFTSTEP_BENCH_SAME_DEVICE": "test hook: N ranks on one GPU, gloo, no engine communicator",
+}
+RESULTS_ALTERING = ("RAFTSTEP_DIAG_LEAN",)
+
+
+def engine_env():
+    """Every RAFTSTEP_* variable of this process, with what it does."""
+    return {k: {"value": v, "effect": ENV_KNOBS.get(k, "unknown to this bench (not read by the engine)")}
+            for k, v in sorted(os.environ.items()) if k.startswith("RAFTSTEP_")}
 
 
 def algorithmic_bytes(R, E, crc=False):
     """minimal SoA bytes per group-step, REF steady state:
-    B(R,E) = 25 + 37(R-1) + 12 E R (233 B at R=5, E=1), + 4 E R with a
-    CRC32C stamp per entry (C5: 5293 B). This is the per-replica SoA
+    B(R,E) = 25 + 37(R-1) + 12 E R (233 B at R=5, E=1; 331 B at R=7), + 4 E R
+    with a CRC32C stamp per entry (C5: 5293 B). This is the per-replica SoA
     accounting (every replica's term/last/commit/deadline and every peer's
     MatchIndex read and written each tick); the compressed steady state
     needs less (lean_bytes), so the SURVEY figure is reported as an
-    equivalent rate, never against the HBM peak."""
+    equivalent rate for the lean kernel and prices the list kernel's group-steps."""
     return 25 + 37 * (R - 1) + 12 * E * R + (4 * E * R if crc else 0)
-
-
-def fused_ticks(wl):
-    """Ticks per launch of the steady-state tick (engine.cpp raft_engine::fuse):
-    RAFTSTEP_FUSE (default 16) while the steady-state list skip holds — the
-    steady workloads without payload CRC — else 1."""
-    if wl.get("init") == "new" or wl["crc"] or os.environ.get("RAFTSTEP_TWO_PASS", "1") == "0":
-        return 1
-    return max(1, int(os.environ.get("RAFTSTEP_FUSE", "16")))
 
 
 def lean_bytes(R, E, crc=False, segmented=False, fuse=1):
@@ -67,9 +95,9 @@ def lean_bytes(R, E, crc=False, segmented=False, fuse=1):
     segment boundary 4 B when the ring has 2K physical slots) and writes the
     record 16 B + hb 4 B + this tick's entries on all R replicas, 12 E R B
     (+4 E R with a CRC32C stamp). C2: 100 B; C4 shape (R=7, 2K slots): 128 B;
-    C5: 5160 B. With `fuse` ticks per launch (tick_fused_kernel) the
-    record / meta / rotation / heartbeat bytes are moved once per launch:
-    40 / fuse + 12 E R (C2 at 4 ticks per launch: 70 B)."""
+    C5: 5160 B. With `fuse` ticks per launch (tick_fused_kernel, the `fused`
+    block only) the record / meta / rotation / heartbeat bytes are moved once
+    per launch: 40 / fuse + 12 E R."""
     return (20 + (4 if segmented else 0) + 20) / fuse + 12 * E * R + (4 * E * R if crc else 0)
 
 
@@ -101,26 +129,26 @@ WORKLOADS = {
                   iso=(8192, 8, 32, 1), seed=0x5EED0004, allow_faults=True,
                   desc="NewNode start, leader-isolation churn, REF semantics (prefix; groups freeze on their first fault)"),
 }
+EXTRA_DEFAULT = ("C4", "C5")
 
 
-def cpu_baseline(args, wl, R, E, K, crc):
+def cpu_baseline(wl, R, E, K, crc, groups, ticks):
     """The oracle (C restatement of main.go's handlers, oracle/) timed on the
     host cores on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-    G, T = args.cpu_groups, args.cpu_ticks
+    G, T = groups, ticks
     if E > 1:   # keep the sample's CPU time and memory bounded for big batches
         G, T = max(1024, 4 * G // E), max(16, T // 4)
-    o = oracle.Oracle(**engine_kwargs(wl, R, G, 0, K, E, crc))
     if wl.get("init") == "new":
         G, T = G // 2, T // 2
-        o.close()
         o = oracle.Oracle(**engine_kwargs(wl, R, G, 0, K, E, crc))
         o.init_new_nodes(0)
         o.tick(0, wl["settle"], threads=threads)
         t_first, start = wl["settle"], "after a NewNode start and %d settle ticks" % wl["settle"]
     else:
+        o = oracle.Oracle(**engine_kwargs(wl, R, G, 0, K, E, crc))
         o.init_steady(0, 0)
         t_first, start = 1, "steady state from init_steady"
     t0 = time.perf_counter()
@@ -143,11 +171,11 @@ def engine_kwargs(wl, R, G, base, K, E, crc):
 
 
 def load_pmc(workload, kernel, ticks=1):
-    """HBM traffic per launch of the dominant kernel from the committed
-    rocprofv3 --pmc summary of exactly this workload, kernel and ticks per
-    launch (mean over the pass's launches; profiles/pmc_*.json, made by tools/pmc_summary.py from FETCH_SIZE /
-    WRITE_SIZE passes), and where it came from; (None, None) if no pass
-    covers it."""
+    """HBM traffic per launch of a kernel from the committed rocprofv3 --pmc
+    summary of exactly this workload, kernel and ticks per launch (mean over
+    the pass's launches; profiles/pmc_*.json, made by tools/pmc_summary.py
+    from FETCH_SIZE / WRITE_SIZE passes), and where it came from; (None,
+    None) if no pass covers it."""
     import glob
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         try:
@@ -159,14 +187,227 @@ def load_pmc(workload, kernel, ticks=1):
             src = f"{os.path.relpath(p, ROOT)} (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of this workload, " \
                   f"calibrated by tools/pmc_calib; not measured in this run" + \
                   (f"; build {d['commit']}" if d.get("commit") else "") + ")"
-            return d["hbm_bytes_per_launch"], src
+            return d, src
     return None, None
+
+
+def live_group_steps(groups, frozen, faults_per_tick):
+    """Group-steps of the groups not frozen by a fault (REF prefix, C4REF):
+    `groups` groups, `frozen` of them frozen before the first tick, and
+    faults_per_tick[t] groups freezing during tick t (a group that faults
+    during a tick did that tick's work). All three must count the same scope:
+    with the engine's RCCL communicator the per-tick records are already
+    summed over every rank, so `groups` is then the whole job's (ADVICE r3:
+    subtracting whole-job fault counts from one rank's groups, then summing
+    over ranks, subtracted them once per rank)."""
+    f = np.asarray(faults_per_tick, np.int64)
+    before = frozen + np.concatenate([[0], np.cumsum(f)[:-1]])
+    return int(groups * len(f) - before.sum())
 
 
 def median(xs):
     xs = sorted(xs)
     n = len(xs)
     return xs[n // 2] if n % 2 else 0.5 * (xs[n // 2 - 1] + xs[n // 2])
+
+
+class Ctx:
+    """Process / rank context of one bench run."""
+
+    def __init__(self, world, rank, local, dist, same_dev):
+        self.world, self.rank, self.local, self.dist, self.same_dev = world, rank, local, dist, same_dev
+
+    @property
+    def comm(self):   # the engine carries an RCCL communicator over every rank
+        return self.dist is not None and not self.same_dev
+
+    def barrier(self):
+        import torch
+        torch.cuda.synchronize()
+        if self.dist is not None:
+            self.dist.barrier()
+        torch.cuda.synchronize()
+
+
+def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0, cpu=None):
+    """One line: `repeats` timed regions of exactly `steps` ticks of workload
+    `wl` on this rank's shard (G groups) with `tpl` ticks per launch, then the
+    untimed profile passes for the dominant kernel's duration. Returns the
+    line's fields (value over all ranks)."""
+    from raftstep import Engine, STAT_NAMES
+    from raftstep import dist as rdist
+    world, dist = ctx.world, ctx.dist
+    crc = wl["crc"]
+    churn = wl.get("init") == "new"
+    base = ctx.rank * G
+    eng = Engine(device=ctx.local, ticks_per_launch=tpl, **engine_kwargs(wl, R, G, base, K, E, crc))
+    if ctx.comm:
+        eng.comm_init(world, ctx.rank, rdist.exchange_comm_id(dist, ctx.rank, Engine.comm_unique_id))
+    fi = STAT_NAMES.index("faults")
+    untimed = np.zeros(len(STAT_NAMES), np.int64)   # stats of the settle and warm-up ticks
+    if churn:   # NewNode start; the first elections happen in untimed settle ticks
+        eng.init_new_nodes(0)
+        untimed += eng.tick(0, wl["settle"], stats=True)
+        tick = wl["settle"]
+    else:
+        eng.init_steady(leader, 0)
+        tick = 1
+    if warmup:
+        untimed += eng.tick(tick, warmup, stats=True)
+        tick += warmup
+
+    # timed regions: exactly `steps` ticks each (+ the per-tick stats, reduced
+    # on the device and, at N>1, all-reduced by RCCL on the engine's side stream)
+    times, stats = [], np.zeros(len(STAT_NAMES), np.int64)
+    # C4REF (REF prefix): a group frozen by a fault does no work, so the value
+    # counts only the live group-steps. With the engine communicator every
+    # record is already the sum over all ranks, so the live count is computed
+    # once over the whole job; without one each rank counts its own shard.
+    scope = G * world if ctx.comm else G
+    frozen = int(untimed[fi])
+    live_steps = []
+    for _ in range(max(1, repeats)):
+        ctx.barrier()
+        t0 = time.perf_counter()
+        s = eng.tick(tick, steps, stats=True)
+        ctx.barrier()
+        el = time.perf_counter() - t0
+        if wl.get("allow_faults"):   # (outside the timed region) per-tick fault counts
+            f = eng.tick_records(steps)[:, fi]
+            live_steps.append(live_group_steps(scope, frozen, f))
+            frozen += int(f.sum())
+        if dist is not None:
+            el = rdist.max_over_ranks(dist, el, device=None if ctx.same_dev else "cuda")
+            if ctx.same_dev:   # no engine communicator: sum the stats through torch.distributed
+                s = np.array(rdist.sum_over_ranks(dist, s), np.int64)
+        times.append(el)
+        stats += s
+        tick += steps
+    # untimed passes: the steady-state kernel's own duration (events attached
+    # to each of its dispatches), then the list kernel's and its group-steps
+    two_pass = os.environ.get("RAFTSTEP_TWO_PASS", "1") != "0"
+    eng.profile(1)
+    eng.tick(tick, steps, stats=False)
+    tick += steps
+    kernel_ms, kernel_ticks = eng.profile_read()
+    list_ms = list_launches = list_steps = 0
+    if two_pass and churn:   # the second pass (list kernel over the groups the lean kernel passed on)
+        eng.profile(3)
+        eng.tick(tick, steps, stats=False)
+        tick += steps
+        list_ms, list_launches = eng.profile_read()
+        eng.profile(0)
+        eng.diag_enable(True)   # (separately: the class counters cost time) listed group-steps per launch
+        eng.tick(tick, steps, stats=False)
+        tick += steps
+        list_steps = eng.diag_read()["list_lanes"]
+        eng.diag_enable(False)
+    eng.profile(0)
+    nranks, _, allreduces = eng.comm_info()
+    eng.close()
+
+    reps = len(times)
+    elapsed = median(times)
+    total_steps = G * world * steps
+    value = total_steps / elapsed
+    live_value = None
+    if wl.get("allow_faults"):
+        mid = sorted(range(reps), key=lambda i: times[i])[reps // 2]
+        live = live_steps[mid]
+        if dist is not None and not ctx.comm:
+            live = int(sum(rdist.sum_over_ranks(dist, [live])))
+        live_value = live / times[mid]
+        value = live_value
+    # correctness guard on the timed runs: the steady state commits exactly one
+    # entry per group per tick and never faults; under churn nothing faults
+    # and most groups have a leader (REF prefix: faults are the point)
+    faults = int(stats[fi])
+    if churn:
+        ok = bool(wl.get("allow_faults") or
+                  (faults == 0 and stats[STAT_NAMES.index("leader_groups")] > 0.5 * G * world * steps * reps))
+    else:
+        ok = bool(stats[STAT_NAMES.index("committed")] == G * world * steps * E * reps and faults == 0)
+
+    # roofline of the dominant kernel, in its own layout's algorithmic bytes:
+    # the lean kernel (one tick per launch) or the fused kernel (tpl > 1,
+    # priced at the call's mean ticks per launch: K = 20 at 16 is 16 + 4)
+    fused = tpl > 1 and not churn and not crc and two_pass
+    mean_tpl = steps / -(-steps // tpl) if fused else 1
+    B = lean_bytes(R, E, crc, segmented="iso" in wl and wl["iso"][0] > 0, fuse=mean_tpl) if two_pass else \
+        algorithmic_bytes(R, E, crc)
+    kname = ("tick_fused_kernel" if fused else "tick_lean_kernel") if two_pass else "tick_fast_kernel"
+    avg_kernel_s = kernel_ms / 1e3 / max(kernel_ticks, 1)   # per tick
+    # C4REF: the lean kernel's algorithmic bytes are those of the live groups it
+    # takes (a frozen group is read as 2 B of gmeta and skipped)
+    units = G if live_value is None else live_value * elapsed / world / steps
+    achieved = B * units / avg_kernel_s / 1e9
+    workload = f"{wl_key}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}, K={K}"
+    pmc, pmc_src = load_pmc(workload, kname, mean_tpl)
+    traffic = pmc["hbm_bytes_per_launch"] / mean_tpl if pmc else None   # per tick
+    B_survey = algorithmic_bytes(R, E, crc)
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "frac_measured": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
+            "traffic_source": pmc_src,
+            "kernel": kname,
+            "ticks_per_launch": mean_tpl,
+            "max_ticks_per_launch": tpl if fused else 1,
+            "bytes_per_group_step": B,
+            "bytes_accounting": (
+                ("tick_fused_kernel, up to %d steady ticks per launch, %.4g on average over this call's launches "
+                 "(bench.py lean_bytes; NOT SURVEY §8(d)'s one-tick-per-launch form)" % (tpl, mean_tpl))
+                if fused else
+                ("tick_lean_kernel, one tick per launch, compressed steady state (bench.py lean_bytes), every "
+                 "group counted as taken by the lean pass") if two_pass else
+                "SURVEY.md §8(d) B(R,E), per-replica SoA"),
+            "units_per_launch": units * (mean_tpl if fused else 1),
+            "avg_kernel_us": avg_kernel_s * 1e6 * (mean_tpl if fused else 1),
+            "avg_kernel_us_per_tick": avg_kernel_s * 1e6,
+            "kernel_launches": kernel_ticks if not fused else -(-kernel_ticks // tpl),
+            # SURVEY §8(d)'s per-replica SoA figure at the measured tick rate:
+            # the bandwidth an uncompressed SoA engine would need for this
+            # throughput (above the HBM peak = beyond any per-replica layout)
+            "survey_bytes_per_group_step": B_survey,
+            "survey_equivalent_GBs": B_survey * value / world / 1e9}
+    line = {
+        "value": value, "ms_per_step": elapsed * 1e3 / steps, "steps": steps, "warmup": warmup,
+        "workload": workload, "groups_per_gpu": G, "groups_total": G * world, "replicas": R,
+        "entries_per_tick": E, "ring_depth": K, "payload_crc32c": bool(crc), "seed": hex(wl["seed"]),
+        "semantics": "RAFT (EXT, Raft paper)" if wl.get("semantics") else "REF (main.go)",
+        "ticks_per_launch": tpl,
+        "timing": {"repeats": reps, "median_s": elapsed, "repeat_ms_per_step": [t * 1e3 / steps for t in times]},
+        "roofline": roof,
+        "stats": dict(zip(STAT_NAMES, [int(x) for x in stats])),
+        "stats_check": ok,
+        "rccl": {"nranks": nranks, "stat_allreduces": allreduces},
+    }
+    if two_pass and churn:
+        # the list kernel: the full fast-path body over the groups the lean
+        # kernel passed on (elections, first rounds, returns, isolated
+        # leaders), two steps per launch in the pipelined tick, priced with
+        # SURVEY §8(d)'s per-replica bytes per group-step it advances
+        lus = list_ms * 1e3 / max(list_launches, 1)
+        per_launch = list_steps / max(list_launches, 1)
+        lpmc, lsrc = load_pmc(workload, "tick_list_kernel", 1)
+        line["list_kernel"] = {
+            "avg_us": lus, "launches": list_launches, "group_steps_per_launch": per_launch,
+            "bytes_per_group_step": B_survey,
+            "achieved": B_survey * per_launch / max(lus, 1e-9) / 1e3, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": B_survey * per_launch / max(lus, 1e-9) / 1e3 / HBM_PEAK_GBS,
+            "traffic_per_group_step": (lpmc["hbm_bytes_per_launch"] / per_launch) if (lpmc and per_launch) else None,
+            "traffic_source": lsrc}
+    if wl.get("allow_faults"):   # REF prefix: groups frozen by a main.go panic / deadlock so far
+        uf = int(untimed[fi])   # (with the engine communicator already the sum over ranks)
+        if dist is not None and not ctx.comm:
+            uf = int(sum(rdist.sum_over_ranks(dist, [uf])))
+        line["faults_prefix"] = {"groups": G * world, "faulted_before_timed": uf, "faulted_in_timed": faults,
+                                 "frozen_fraction": (uf + faults) / (G * world),
+                                 "value_counts": "live (not frozen) group-steps only",
+                                 "live_group_steps_median_repeat": int(round(live_value * elapsed)),
+                                 "all_group_steps_per_s": total_steps / elapsed}
+    if cpu and ctx.rank == 0 and world == 1:
+        line["cpu_baseline"] = cpu_baseline(wl, R, E, K, crc, *cpu)
+    return line
 
 
 def main():
@@ -185,9 +426,21 @@ def main():
     ap.add_argument("--cpu-groups", type=int, default=262144)
     ap.add_argument("--cpu-ticks", type=int, default=1024)   # ~10 s of oracle work on 16 host threads
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fused", action="store_true", help="skip the `fused` block")
+    ap.add_argument("--extra", default=None,
+                    help="comma-separated extra workloads timed after the headline at N=1 (default C4,C5 with the "
+                         "default workload; 'none' to skip)")
+    ap.add_argument("--extra-budget", type=float, default=120.0,
+                    help="seconds: no further extra workload starts once the run has taken this long")
     ap.add_argument("--isolate", type=int, default=None,
                     help="diagnostics: override the workload's isolation windows per 65536 epochs (0: none)")
     args = ap.parse_args()
+    t_start = time.perf_counter()
+
+    env = engine_env()
+    bad = [k for k in env if k in RESULTS_ALTERING]
+    if bad:
+        raise SystemExit(f"bench: {bad} alter results; refusing to time with them")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -210,8 +463,7 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    from raftstep import Engine, STAT_NAMES
+    ctx = Ctx(world, rank, local, dist, same_dev)
 
     wl = WORKLOADS[wl_key]
     if args.isolate is not None and "iso" in wl:
@@ -220,193 +472,96 @@ def main():
     G = args.groups_per_gpu or wl["groups"]
     E = args.entries or wl["entries"]
     K = args.ring_depth or wl["ring_depth"]
-    crc = wl["crc"]
-    churn = wl.get("init") == "new"
-    base = rank * G
-    eng = Engine(device=local, **engine_kwargs(wl, R, G, base, K, E, crc))
-    if dist is not None and not same_dev:
-        from raftstep import dist as rdist
-        eng.comm_init(world, rank, rdist.exchange_comm_id(dist, rank, Engine.comm_unique_id))
-    untimed = np.zeros(len(STAT_NAMES), np.int64)   # stats of the settle and warm-up ticks
-    if churn:   # NewNode start; the first elections happen in untimed settle ticks
-        eng.init_new_nodes(0)
-        untimed += eng.tick(0, wl["settle"], stats=True)
-        tick = wl["settle"]
-    else:
-        eng.init_steady(args.leader, 0)
-        tick = 1
-    if args.warmup:
-        untimed += eng.tick(tick, args.warmup, stats=True)
-        tick += args.warmup
+    cpu = None if args.no_cpu_baseline else (args.cpu_groups, args.cpu_ticks)
+    head = measure(ctx, wl_key, wl, G, R, E, K, args.steps, args.warmup, args.repeats, tpl=1, leader=args.leader,
+                   cpu=cpu)
+    ok = head["stats_check"]
 
-    def barrier():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
+    multi = None
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, {"rank": rank, "group_base": rank * G, "groups": G,
+                                       "rccl_nranks": head["rccl"]["nranks"],
+                                       "stat_allreduces": head["rccl"]["stat_allreduces"]})
+        multi = {"rccl_nranks": head["rccl"]["nranks"] if not same_dev else None,
+                 "engine_communicator": not same_dev, "per_rank": ranks}
+        if not same_dev:
+            # the engine communicator must span every rank, and every window's
+            # stats must have gone through it (ncclAllReduce on the side stream)
+            if any(r["rccl_nranks"] != world for r in ranks):
+                raise SystemExit(f"bench: RCCL communicator ranks {[r['rccl_nranks'] for r in ranks]}, "
+                                 f"WORLD_SIZE is {world}")
+            ok = ok and all(r["stat_allreduces"] > 0 for r in ranks)
 
-    # timed regions: exactly K fused ticks each (+ the per-tick stats, reduced
-    # on the device and, at N>1, all-reduced by RCCL on the engine's side stream)
-    times, stats = [], np.zeros(len(STAT_NAMES), np.int64)
-    # groups frozen by a fault before each tick (REF prefix: a frozen group does
-    # no work, so C4REF's value counts only the live group-steps)
-    frozen = int(untimed[STAT_NAMES.index("faults")])
-    live_steps = []
-    eng.profile(2)   # one HIP event pair on the engine stream around each timed call
-    for _ in range(max(1, args.repeats)):
-        barrier()
-        t0 = time.perf_counter()
-        s = eng.tick(tick, args.steps, stats=True)
-        barrier()
-        el = time.perf_counter() - t0
-        if wl.get("allow_faults"):   # (outside the timed region) per-tick fault counts of this rank
-            f = eng.tick_records(args.steps)[:, STAT_NAMES.index("faults")]
-            before = frozen + np.concatenate([[0], np.cumsum(f)[:-1]])
-            live_steps.append(int(G * args.steps - before.sum()))
-            frozen += int(f.sum())
-        if dist is not None:
-            from raftstep import dist as rdist
-            el = rdist.max_over_ranks(dist, el, device=None if same_dev else "cuda")
-            if same_dev:   # no engine communicator: sum the stats through torch.distributed
-                s = np.array(rdist.sum_over_ranks(dist, s), np.int64)
-        times.append(el)
-        stats += s
-        tick += args.steps
-    region_ms, region_launches = eng.profile_read()
-    # untimed pass: the steady-state kernel's own duration, events attached to each dispatch
-    eng.profile(1)
-    eng.tick(tick, args.steps, stats=False)
-    kernel_ms, kernel_launches = eng.profile_read()
-    two_pass = os.environ.get("RAFTSTEP_TWO_PASS", "1") != "0"
-    list_ms = list_launches = 0
-    if two_pass:   # the second pass (list kernel over the groups the lean kernel passed on)
-        eng.profile(3)
-        eng.tick(tick + args.steps, args.steps, stats=False)
-        list_ms, list_launches = eng.profile_read()
-    eng.profile(0)
-    nranks, _, allreduces = eng.comm_info()
+    steady_default = args.workload is None and world == 1 and not any(
+        x is not None for x in (args.groups_per_gpu, args.replicas, args.entries, args.ring_depth))
+    fused = None
+    if world == 1 and not args.no_fused and wl.get("init") != "new" and not wl["crc"]:
+        fl = measure(ctx, wl_key, wl, G, R, E, K, args.steps, args.warmup, args.repeats, tpl=FUSED_TICKS,
+                     leader=args.leader)
+        ok = ok and fl["stats_check"]
+        fused = {"note": "NOT the headline: up to %d steady ticks per launch of tick_fused_kernel, state kept in "
+                         "registers between the ticks of a launch (SURVEY §8(d) excludes this form from the "
+                         "roofline claim); same workload, protocol and statistics check" % FUSED_TICKS,
+                 "value": fl["value"], "ms_per_step": fl["ms_per_step"], "ticks_per_launch": FUSED_TICKS,
+                 "roofline": fl["roofline"], "stats_check": fl["stats_check"],
+                 "timing": fl["timing"]}
 
-    elapsed = median(times)
-    reps = len(times)
-    total_steps = G * world * args.steps
-    value = total_steps / elapsed
-    live_value = None
-    if wl.get("allow_faults"):   # C4REF: only the group-steps of groups not frozen by a fault count
-        mid = sorted(range(reps), key=lambda i: times[i])[reps // 2]
-        live = live_steps[mid]
-        if dist is not None:
-            from raftstep import dist as rdist
-            live = int(sum(rdist.sum_over_ranks(dist, [live])))
-        live_value = live / times[mid]
-        value = live_value
-    # correctness guard on the timed runs: the steady state commits exactly one
-    # entry per group per tick and never faults; under churn nothing faults
-    # and most groups have a leader (REF prefix: faults are the point)
-    expect_commit = G * world * args.steps * E * reps
-    faults = int(stats[STAT_NAMES.index("faults")])
-    if churn:
-        ok = (wl.get("allow_faults") or faults == 0) and \
-            (wl.get("allow_faults") or stats[STAT_NAMES.index("leader_groups")] > 0.5 * G * world * args.steps * reps)
-    else:
-        ok = stats[STAT_NAMES.index("committed")] == expect_commit and faults == 0
-    if world > 1 and not same_dev:
-        # the engine communicator must span every rank, and every window's
-        # stats must have gone through it (ncclAllReduce on the side stream)
-        if nranks != world:
-            raise SystemExit(f"bench: RCCL communicator has {nranks} ranks, WORLD_SIZE is {world}")
-        ok = ok and allreduces > 0
+    extras = {}
+    names = EXTRA_DEFAULT if (args.extra is None and steady_default) else \
+        tuple(x for x in (args.extra or "").split(",") if x and x != "none")
+    if world > 1:
+        names = ()
+    for name in names:
+        if time.perf_counter() - t_start > args.extra_budget:
+            extras[name] = {"skipped": f"extra budget of {args.extra_budget:.0f} s spent"}
+            continue
+        xw = WORKLOADS[name]
+        xR, xE, xK = xw.get("replicas", R_DEFAULT), xw["entries"], xw["ring_depth"]
+        x = measure(ctx, name, xw, xw["groups"], xR, xE, xK, args.steps, args.warmup, args.repeats, tpl=1,
+                    cpu=None if args.no_cpu_baseline else (args.cpu_groups // 4, args.cpu_ticks // 4))
+        ok = ok and x["stats_check"]
+        x.pop("rccl", None)
+        extras[name] = x
 
-    B_survey = algorithmic_bytes(R, E, crc)
-    # the dominant kernel's algorithmic bytes in its own layout: the lean
-    # kernel (compressed steady state) in the two-pass tick, else the
-    # one-pass fast kernel with SURVEY §8(d)'s per-replica SoA accounting
-    fuse = fused_ticks(wl)
-    # a call of K ticks runs ceil(K / fuse) fused launches (K = 20: 16 + 4);
-    # the bytes moved once per launch are priced at the mean ticks per launch
-    tpl = args.steps / -(-args.steps // fuse) if fuse > 1 else 1
-    B = lean_bytes(R, E, crc, segmented="iso" in wl and wl["iso"][0] > 0, fuse=tpl) if two_pass else B_survey
-    avg_kernel_s = kernel_ms / 1e3 / max(kernel_launches, 1)    # steady-state kernel, kernel-exact
-    avg_region_s = region_ms / 1e3 / max(region_launches, 1)    # all launches of a tick + gaps
-    # C4REF: the lean kernel's algorithmic bytes are those of the live groups it
-    # takes (a frozen group is read as 2 B of gmeta and skipped)
-    units = G if live_value is None else live_value * elapsed / world / args.steps
-    achieved = B * units / avg_kernel_s / 1e9
-    workload = f"{wl_key}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}, K={K}"
-    kname = ("tick_fused_kernel" if fuse > 1 else "tick_lean_kernel") if two_pass else "tick_fast_kernel"
-    traffic, traffic_src = load_pmc(workload, kname, tpl)
-    if traffic and fuse > 1:   # (the passes count bytes per launch, mean over launches; the roofline is per tick)
-        traffic /= tpl
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "frac_measured": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
-            "traffic_source": traffic_src,
-            "bytes_per_group_step": B,
-            "bytes_accounting": (("tick_fused_kernel, up to %d steady ticks per launch, %.4g on average over this "
-                                  "call's launches (bench.py lean_bytes)" % (fuse, tpl)
-                                  if fuse > 1 else
-                                  "tick_lean_kernel, compressed steady state (bench.py lean_bytes), every group "
-                                  "counted as taken by the lean pass") if two_pass else
-                                 "SURVEY.md §8(d) B(R,E), per-replica SoA"),
-            "ticks_per_launch": tpl,
-            "max_ticks_per_launch": fuse,
-            "units_per_launch": units,
-            "kernel": ("tick_fused_kernel" if fuse > 1 else "tick_lean_kernel") if two_pass else "tick_fast_kernel",
-            "avg_kernel_us": avg_kernel_s * 1e6, "kernel_launches": kernel_launches,
-            "list_kernel_us": (list_ms * 1e3 / max(list_launches, 1)) if two_pass else None,
-            "avg_region_us_per_tick": avg_region_s * 1e6,
-            "achieved_region": B * units / avg_region_s / 1e9,
-            # SURVEY §8(d)'s per-replica SoA figure at the measured tick rate:
-            # the bandwidth an uncompressed SoA engine would need for this
-            # throughput (above the HBM peak = beyond any per-replica layout)
-            "survey_bytes_per_group_step": B_survey,
-            "survey_equivalent_GBs": B_survey * value / world / 1e9}
     result = {
         "metric": "Raft group-steps/sec at 1M 5-replica groups, 1-8 GPUs; % of HBM peak",
-        "value": value,
+        "value": head["value"],
         "unit": "group-steps/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed * 1e3 / args.steps,
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (seeded splitmix64 trace; %s, SURVEY.md §8(d) %s)"
-                % ("NewNode start + isolation churn" if churn else "post-election steady state", wl_key),
-        "config": {"workload": workload, "groups_per_gpu": G, "groups_total": G * world, "replicas": R,
-                   "entries_per_tick": E, "ring_depth": K, "payload_crc32c": bool(crc), "leader": args.leader,
-                   "seed": hex(wl["seed"]),
-                   "semantics": "RAFT (EXT, Raft paper)" if wl.get("semantics") else "REF (main.go)",
-                   "parallelism": f"group-sharded x{world}"},
-        "timing": {"repeats": reps, "median_s": elapsed, "repeat_ms_per_step": [t * 1e3 / args.steps for t in times]},
-        "roofline": roof,
-        "stats": dict(zip(STAT_NAMES, [int(x) for x in stats])),
+                % ("NewNode start + isolation churn" if wl.get("init") == "new" else "post-election steady state",
+                   wl_key),
+        "config": {"workload": head["workload"], "groups_per_gpu": G, "groups_total": G * world, "replicas": R,
+                   "entries_per_tick": E, "ring_depth": K, "payload_crc32c": bool(wl["crc"]), "leader": args.leader,
+                   "seed": hex(wl["seed"]), "semantics": head["semantics"],
+                   "ticks_per_launch": 1, "parallelism": f"group-sharded x{world}", "engine_env": env},
+        "timing": head["timing"],
+        "roofline": head["roofline"],
+        "stats": head["stats"],
         "stats_check": bool(ok),
     }
-    if wl.get("allow_faults"):   # REF prefix: groups frozen by a main.go panic / deadlock so far
-        fi = STAT_NAMES.index("faults")
-        result["faults_prefix"] = {"groups": G * world, "faulted_before_timed": int(untimed[fi]),
-                                   "faulted_in_timed": int(stats[fi]),
-                                   "frozen_fraction": (int(untimed[fi]) + int(stats[fi])) / (G * world),
-                                   "value_counts": "live (not frozen) group-steps only",
-                                   "live_group_steps_median_repeat": int(round(live_value * elapsed)),
-                                   "all_group_steps_per_s": total_steps / elapsed}
-    if world > 1:
-        from raftstep import dist as rdist
-        ranks = [None] * world
-        dist.all_gather_object(ranks, {"rank": rank, "group_base": base, "groups": G, "rccl_nranks": nranks,
-                                       "stat_allreduces": allreduces})
-        result["multi_gpu"] = {"rccl_nranks": nranks if not same_dev else None,
-                               "engine_communicator": not same_dev,
-                               "per_rank": ranks}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, wl, R, E, K, crc)
-    elif rank == 0:
-        result["cpu_baseline"] = None
+    for k in ("list_kernel", "faults_prefix"):
+        if k in head:
+            result[k] = head[k]
+    if multi:
+        result["multi_gpu"] = multi
+    if rank == 0:
+        result["cpu_baseline"] = head.get("cpu_baseline")
+    if fused:
+        result["fused"] = fused
+    if extras:
+        result["extra_workloads"] = extras
+    result["bench_wall_s"] = time.perf_counter() - t_start
     if rank == 0:
         print(json.dumps(result), flush=True)
-    eng.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RAFT_ABI_VERSION 4u
+#define RAFT_ABI_VERSION 5u
 #define RAFT_MAX_REPLICAS 8u
 
 /* Node.State (main.go:51-57). */
@@ -106,8 +106,19 @@ typedef struct raft_config {
   uint32_t corrupt_per_65536;  /* EXT: probability that an AppendEntries' last entry arrives with a flipped bit */
   uint32_t isolate_leader;     /* EXT: 1 = an isolation window cuts off the group's leader at the window's first
                                   tick (the lowest-id Leader then; no leader: nobody), 0 = a hashed replica */
-  uint32_t reserved[5];
+  uint32_t ticks_per_launch;   /* 1 (default; 0 reads as 1): one tick per kernel launch, every group's state read
+                                  from and written back to HBM every tick (the metric's form).
+                                  2..64: while the steady-state list skip holds (no isolation, no CRC), up to this
+                                  many steady ticks run in one launch of the fused kernel (state kept in registers
+                                  between them; results identical, not the §8(d) form) */
+  uint32_t debug_flags;        /* RAFT_DEBUG_*; 0 in production */
+  uint32_t reserved[3];        /* must be 0 */
 } raft_config;
+
+/* raft_config.debug_flags */
+#define RAFT_DEBUG_ALLOW_WRONG_RESULTS 1u  /* accept the timing-only environment knob RAFTSTEP_DIAG_LEAN, whose modes
+                                              skip work and make results WRONG; without this flag
+                                              raft_engine_create refuses it (RAFT_EINVAL) */
 
 /* Canonical host view of engine state, group-major:
  *   per-replica arrays are indexed [g*R + r], match is [(g*R + leader)*R + peer],
@@ -184,9 +195,10 @@ int raft_nodelog(raft_engine* e, uint64_t group, char* buf, size_t cap);
 int raft_checkpoint_save(raft_engine* e, const char* path);
 int raft_checkpoint_load(raft_engine* e, const char* path);
 
-/* ---- the fused tick (the metric path) -----------------------------------
+/* ---- the tick (the metric path) -----------------------------------------
  * Advances every group by `nticks` ticks starting at virtual tick
- * `first_tick`. One tick per kernel launch; per tick and group, in order:
+ * `first_tick`. One tick per kernel launch (config.ticks_per_launch = 1, the
+ * default; see there for the fused steady form); per tick and group, in order:
  *   1. client append to leaders (main.go:87-93 -> 327-329),
  *   2. replicas in ascending id: leader replication round + commit
  *      (main.go:332-391) / candidate vote round (main.go:253-284), every

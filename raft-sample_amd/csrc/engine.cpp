@@ -122,10 +122,10 @@ struct raft_engine {
   bool gen_pending = false;     // a general kernel is running on gen_stream
   int gen_parity = 0;           // its worklist parity
   uint32_t gen_w0 = 0, gen_w1 = 0;   // its window's stats range (indices into the call's ticks)
+  bool gen_stats = false;       // it counts into those per-tick slots of hist
   int force_general = 0;        // debug: route every group through the general kernel
   int lane_general = 0;         // RAFTSTEP_GENERAL=lane: one-lane-per-group general kernel (A/B) instead of the segment one
   uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
-  int write_through = 0;        // fast kernel stores with sc1 (write-through) instead of write-back
   int debug_work = 0;           // RAFTSTEP_DEBUG_WORK: print each general-kernel worklist size
   int debug_pipe = 0;           // RAFTSTEP_DEBUG_PIPE: print each call's pipeline choice
   // two-pass tick (RAFTSTEP_TWO_PASS, default on): the lean kernel takes the
@@ -139,17 +139,14 @@ struct raft_engine {
   // groups alone, P.glst marks) runs beside it; the lean kernel of t+2 waits
   // for it. Lists and their counters rotate over three sets: lean(t+1) fills
   // one while list(t) reads another and zeroes the third.
-  // RAFTSTEP_PIPELINE=2 (A/B) pipelines a call only while the previous
-  // call's last tick listed at most pipe_max_list groups per 65536 (measured:
-  // no gain — the pipelined tick is faster on C4R's large lists too).
+  // RAFTSTEP_PIPELINE=0 runs the two passes in line (exact either way:
+  // tests/test_gpu_pipeline.py).
   int pipeline = 1;
-  uint32_t pipe_max_list = 1024;   // RAFTSTEP_PIPELINE_MAX_LIST, groups per 65536
-  uint64_t last_list = 0;          // the previous call's check record, CHK_LAST_LIST
-  // Fused steady ticks (RAFTSTEP_FUSE, default 16): while the steady-state list
-  // skip holds (and without payload CRC, whose per-follower verification the
-  // lean kernel does tick by tick), that many ticks run in one launch of
-  // tick_fused_kernel (k_fast.hip)
-  uint32_t fuse = 16;
+  // Fused steady ticks (raft_config.ticks_per_launch, default 1 = off): while
+  // the steady-state list skip holds (and without payload CRC, whose
+  // per-follower verification the lean kernel does tick by tick), up to that
+  // many ticks run in one launch of tick_fused_kernel (k_fast.hip)
+  uint32_t fuse = 1;
   hipStream_t list_stream = nullptr;
   hipEvent_t ev_lean[2] = {nullptr, nullptr};   // engine stream -> list_stream (list(t) after lean(t))
   hipEvent_t ev_list[4] = {nullptr, nullptr, nullptr, nullptr};   // list_stream -> engine stream (list(t) done)
@@ -299,9 +296,14 @@ int settle_check(raft_engine* e) {
   return RAFT_OK;
 }
 
-// State replaced: the list-skip proof and any poison go
+// A call that replaces the state starts by dropping the list-skip proof (the
+// conservative direction, whatever happens next) ...
+void state_replacing(raft_engine* e) { e->steady_origin = e->steady_ok = false; }
+// ... and only once the new state's launches / copies have gone through
+// successfully drops any poison and a still-pending end-of-call check (both
+// describe the old state). A call that fails on the way leaves them as they
+// were: a poisoned engine stays poisoned.
 void state_replaced(raft_engine* e) {
-  e->steady_origin = e->steady_ok = false;
   e->pend_chk = false;
   e->poisoned = false;
   e->poison_msg.clear();
@@ -410,6 +412,7 @@ void raft_config_default(raft_config* c) {
   c->isolate_min_ticks = 8;
   c->isolate_max_ticks = 32;
   c->device = 0;
+  c->ticks_per_launch = 1;         // one tick per launch
 }
 
 const char* raft_last_error(void) { return g_err.c_str(); }
@@ -437,6 +440,17 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (c.isolate_per_65536 &&
       (c.isolate_min_ticks < 1 || c.isolate_max_ticks > 32 || c.isolate_min_ticks > c.isolate_max_ticks))
     return fail(RAFT_EINVAL, "isolation length must satisfy 1 <= min <= max <= 32");
+  if (c.ticks_per_launch > 64) return fail(RAFT_EINVAL, "ticks_per_launch must be 0..64 (0 and 1: one tick per launch)");
+  if (c.debug_flags & ~RAFT_DEBUG_ALLOW_WRONG_RESULTS) return fail(RAFT_EINVAL, "unknown debug_flags bits");
+  for (uint32_t w : c.reserved)
+    if (w) return fail(RAFT_EINVAL, "reserved config words must be 0");
+  // RAFTSTEP_DIAG_LEAN (timing diagnostics of the lean / list kernels) skips
+  // work and makes results wrong: refused unless the caller says so explicitly
+  uint32_t diag_lean = 0;
+  if (const char* dl = getenv("RAFTSTEP_DIAG_LEAN")) diag_lean = uint32_t(atoi(dl));
+  if (diag_lean && !(c.debug_flags & RAFT_DEBUG_ALLOW_WRONG_RESULTS))
+    return fail(RAFT_EINVAL, "RAFTSTEP_DIAG_LEAN=%u makes results wrong; set debug_flags RAFT_DEBUG_ALLOW_WRONG_RESULTS "
+                "to accept it", diag_lean);
   const uint64_t Gp = (c.groups + 255) & ~uint64_t(255);
   // device addressing (raft_device.hpp at(), rix()): 64-bit plane/tile bases,
   // 32-bit per-lane BYTE offsets, so the group records (NPL rows of R 4-B
@@ -459,9 +473,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   const uint64_t R = c.replicas;
   // physical ring slots: 2K where groups can drift out of the global ring
   // phase (EXT isolation churn), so that their rotation can be switched in
-  // place (raft_device.hpp ring_slot); RAFTSTEP_RING_PHYS=1|2 overrides
-  uint64_t phys = c.isolate_per_65536 > 0 ? 2 : 1;
-  if (const char* rp = getenv("RAFTSTEP_RING_PHYS")) phys = atoi(rp) == 2 ? 2 : 1;
+  // place (raft_device.hpp ring_slot)
+  const uint64_t phys = c.isolate_per_65536 > 0 ? 2 : 1;
   const uint64_t K = c.ring_depth * phys;
   e->KP = K;
   const bool raft = c.semantics == RAFT_SEM_RAFT;
@@ -535,15 +548,13 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
   if (const char* gk = getenv("RAFTSTEP_GENERAL")) e->lane_general = std::strcmp(gk, "lane") == 0;
   if (const char* se = getenv("RAFTSTEP_SLOW_EVERY")) e->slow_every = std::max(1, atoi(se));
-  if (const char* wt = getenv("RAFTSTEP_WRITE_THROUGH")) e->write_through = atoi(wt) != 0;
   if (const char* dw = getenv("RAFTSTEP_DEBUG_WORK")) e->debug_work = atoi(dw) != 0;
   if (const char* dp = getenv("RAFTSTEP_DEBUG_PIPE")) e->debug_pipe = atoi(dp) != 0;
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
-  if (const char* dl = getenv("RAFTSTEP_DIAG_LEAN")) e->P.diag = uint32_t(atoi(dl));
+  e->P.diag = diag_lean;
   if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = atoi(og) != 0;
-  if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = std::min(2, std::max(0, atoi(pp)));
-  if (const char* pm = getenv("RAFTSTEP_PIPELINE_MAX_LIST")) e->pipe_max_list = uint32_t(std::max(0, atoi(pm)));
-  if (const char* fu = getenv("RAFTSTEP_FUSE")) e->fuse = uint32_t(std::max(1, atoi(fu)));
+  if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = atoi(pp) != 0;
+  e->fuse = std::max<uint32_t>(1u, c.ticks_per_launch);
   e->P.dbg_pass = 0xFFFFFFFFu;
   if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
     e->diag_print = 1;
@@ -629,22 +640,24 @@ int raft_engine_info(const raft_engine* e, raft_config* cfg_out, uint64_t* devic
 
 int raft_init_new_nodes(raft_engine* e, int64_t tick0) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
-  state_replaced(e);
+  state_replacing(e);
   if (int rc = check_ticks(e, tick0, 1)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   HIPCHK(launch_init_new(e->R, e->P, make_trace(e, tick0), e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  state_replaced(e);
   return RAFT_OK;
 }
 
 int raft_init_steady(raft_engine* e, int32_t leader, int64_t tick0) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
-  state_replaced(e);
-  e->steady_origin = true;   // empty logs; the list skip still needs a call that proves the list empty
+  state_replacing(e);
   if (int rc = check_ticks(e, tick0, 1)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   HIPCHK(launch_init_steady(e->R, e->P, make_trace(e, tick0), leader, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  state_replaced(e);
+  e->steady_origin = true;   // empty logs; the list skip still needs a call that proves the list empty
   return RAFT_OK;
 }
 
@@ -807,7 +820,7 @@ int raft_store_state_range(raft_engine* e, uint64_t first_group, uint64_t n_grou
 }
 
 int raft_load_state(raft_engine* e, const raft_state_view* v) {
-  if (e) state_replaced(e);
+  if (e) state_replacing(e);
   if (!e || !v) return fail(RAFT_EINVAL, "null argument");
   if (!v->role || !v->voted || !v->term || !v->last || !v->commit || !v->deadline || !v->timeout ||
       !v->match || !v->fault || !v->log_term || !v->log_value)
@@ -927,6 +940,7 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.log_value, lv);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(e->stream));
+  state_replaced(e);
   return RAFT_OK;
 }
 
@@ -972,8 +986,14 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (int rc = settle_check(e)) return rc;
   if (int rc = check_ticks(e, first_tick, nticks)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
-  if (e->gen_pending)   // (only after a failed call: every call joins its general kernels)
+  if (e->gen_pending) {   // (only after a failed call: every call joins its general kernels)
     if (int rc = join_general(e, false)) return rc;
+    // its window's per-tick slots were never reduced (the reduce is what
+    // re-zeroes them): zero them, or the next call's stats would include them
+    if (e->gen_stats)
+      HIPCHK(hipMemsetAsync(e->hist + size_t(e->gen_w0) * STAT_SLOTS * NSTAT, 0,
+                            size_t(e->gen_w1 - e->gen_w0 + 1) * STAT_SLOTS * NSTAT * 8, e->stream));
+  }
   // (the per-tick records need nticks slots; the check records exist at any capacity)
   if (int rc = ensure_hist(e, stats ? std::max<uint32_t>(nticks, 1) : 1)) return rc;
   if (!nticks) return RAFT_OK;
@@ -987,13 +1007,11 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   e->skipped_list = skip_list;
   e->n_ticks += nticks;
   if (skip_list) e->n_skip_ticks += nticks;
-  const bool two = e->two_pass && !e->force_general && !e->write_through;
-  const bool pipe = two && !skip_list && !e->debug_work &&
-                    (e->pipeline == 1 ||
-                     (e->pipeline == 2 && e->last_list * 65536ull <= uint64_t(e->pipe_max_list) * e->cfg.groups));
+  const bool two = e->two_pass && !e->force_general;
+  const bool pipe = two && !skip_list && !e->debug_work && e->pipeline;
   if (e->debug_pipe)
-    fprintf(stderr, "raftstep: ticks %lld..%lld pipeline %d (last call's last list %llu)\n", (long long)first_tick,
-            (long long)(first_tick + nticks - 1), int(pipe), (unsigned long long)e->last_list);
+    fprintf(stderr, "raftstep: ticks %lld..%lld pipeline %d\n", (long long)first_tick,
+            (long long)(first_tick + nticks - 1), int(pipe));
   const uint32_t fuse = (two && skip_list && !e->cfg.payload_crc && e->prof != 3) ? e->fuse : 1u;
   // every call that runs list kernels starts with the lists' counters zeroed
   // (a pipelined call's last list kernel leaves the carried list's count)
@@ -1076,8 +1094,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       ++e->lpar;
     } else {
       HIPCHK(launch_tick_fast(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar % NWORK],
-                              e->work_tick[e->wpar % NWORK], cnt, force,
-                              e->write_through, e->stream, a, b));
+                              e->work_tick[e->wpar % NWORK], cnt, force, e->stream, a, b));
     }
     // the previous window's general kernel, overlapped with this tick's fast
     // kernels: the engine stream waits for it, then its window tail clears
@@ -1120,6 +1137,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         e->gen_parity = par;
         e->gen_w0 = stats_first;
         e->gen_w1 = i;
+        e->gen_stats = stats;
         ++e->n_general;
       } else if (!skip_list) {
         if (pipe) HIPCHK(hipStreamWaitEvent(e->stream, e->ev_list[i & 3], 0));
@@ -1189,7 +1207,7 @@ int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_sta
     if (!nticks) return RAFT_OK;
     // one readback per call: the per-tick records (already summed over slots,
     // and over GPUs) and, behind them, the end-of-call check record
-    const bool two = e->two_pass && !e->force_general && !e->write_through;
+    const bool two = e->two_pass && !e->force_general;
     const size_t words = size_t(nticks + (two ? 1 : 0)) * NSTAT;
     HIPCHK(hipMemcpyAsync(e->hrb, e->tstat, words * 8, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -1211,7 +1229,6 @@ int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_sta
       // steady-state list skip: proven for the next call when nothing was
       // listed at the last tick and the last general window took nothing
       if (e->steady_origin) e->steady_ok = c[CHK_LISTED] == 0 && c[CHK_DEFERRED] == 0;
-      e->last_list = c[CHK_LAST_LIST];
     }
   }
   return RAFT_OK;
@@ -1686,7 +1703,7 @@ int raft_checkpoint_save(raft_engine* e, const char* path) {
 }
 
 int raft_checkpoint_load(raft_engine* e, const char* path) {
-  if (e) state_replaced(e);
+  if (e) state_replacing(e);
   if (!e || !path) return fail(RAFT_EINVAL, "null argument");
   const uint64_t G = e->cfg.groups, R = e->cfg.replicas, K = e->cfg.ring_depth;
   File f;

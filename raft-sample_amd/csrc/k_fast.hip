@@ -19,13 +19,9 @@ namespace raftstep {
 // alone until the general kernel has caught it up.
 // MSYNC: after a fast tick every follower's MatchIndex equals its
 // LastApplied (main.go:156 -> 376), so the row is kept implicit.
-// Store policy of the fast kernel: plain (write-back L2) or write-through
-// (agent-scope relaxed atomic store = global_store ... sc1, which drops the
-// line from L2 so that less dirty data is left for the end-of-kernel flush).
-template <bool WT, typename T>
+template <typename T>
 __device__ __forceinline__ void st(T* base, uint32_t idx, T v) {
-  if constexpr (WT) __hip_atomic_store(&at(base, idx), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else at(base, idx) = v;
+  at(base, idx) = v;
 }
 
 // Log ring entries are written once and read, if ever, K or fewer ticks
@@ -33,7 +29,7 @@ __device__ __forceinline__ void st(T* base, uint32_t idx, T v) {
 // ... nt), so the rings stream past the caches and the 256 MiB Infinity
 // Cache keeps the per-group words and records that every tick re-reads
 // (measured: C2 at 2^22 groups, lean kernel 87 -> 62 us; C4 list kernel
-// 111 -> 95 us). Write-through (WT) stores stay as they are.
+// 111 -> 95 us).
 template <typename T>
 __device__ __forceinline__ void ring_st(T* base, uint32_t idx, T v) {
   __builtin_nontemporal_store(v, &base[idx]);
@@ -47,12 +43,6 @@ template <typename T>
 __device__ __forceinline__ T ring_ld(const T* base, uint32_t idx) {
   return __hip_atomic_load(&base[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-template <bool WT, typename T>
-__device__ __forceinline__ void rst(T* base, uint32_t idx, T v) {
-  if constexpr (WT) st<true>(base, idx, v);
-  else ring_st(base, idx, v);
-}
-
 // R copies of one value into R consecutive ring elements (4-B aligned) with
 // the widest non-temporal stores: 16-B pieces, then the remainder (a drifted
 // lane's ring segment: 2 store instructions for R=7 terms instead of 7).
@@ -121,10 +111,9 @@ struct RowAcc {
     if constexpr (LDS) return base[k * R + r];
     else return raftstep::at(base, o + uint32_t(k * R + r));
   }
-  template <bool WT>
   __device__ __forceinline__ void st(int k, int r, int32_t v) const {
     if constexpr (LDS) { base[k * R + r] = v; *dm |= 1u << k; }
-    else raftstep::st<WT>(base, o + uint32_t(k * R + r), v);
+    else raftstep::st(base, o + uint32_t(k * R + r), v);
   }
   __device__ __forceinline__ void load(int k, int (&a)[R]) const {
     if constexpr (LDS) {
@@ -168,10 +157,9 @@ struct WordAcc {
   __device__ __forceinline__ int32_t& sb2() const { if constexpr (LDS) return *sb2_; else return raftstep::at(sb2_, g); }
   __device__ __forceinline__ LxRec& lx() const { if constexpr (LDS) return *lx_; else return lx_[g]; }
   __device__ __forceinline__ SsRec& ss() const { if constexpr (LDS) return *ss_; else return ss_[g]; }
-  template <bool WT>
   __device__ __forceinline__ void st_hb(int32_t v) const {
     if constexpr (LDS) *hb_ = v;
-    else raftstep::st<WT>(hb_, g, v);
+    else raftstep::st(hb_, g, v);
   }
 };
 template <int R>
@@ -259,7 +247,7 @@ __device__ __forceinline__ bool quiet_leaderless(const DevPlanes& P, const Trace
 // over the list of groups the lean kernel passed on (tick_list_kernel, LIST:
 // the lanes of a wave hold scattered groups, so every ring write is the
 // lane's own). Block-uniform control flow (it reduces over the block).
-template <int R, bool WT, bool CRC, int SEM, bool LIST, class Rows, class Words>
+template <int R, bool CRC, int SEM, bool LIST, class Rows, class Words>
 __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                                            int32_t* work_tick, uint32_t* work_count, int force_slow, const uint32_t g,
                                            const uint32_t* tab, const Rows& RW, const Words& GW) {
@@ -333,10 +321,10 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
 #pragma unroll
           for (int p = 0; p < R; ++p) {
             if (p != c && p != xs) {
-              RW.template st<WT>(PL_LMATCH, p, last[p]);
-              RW.template st<WT>(PL_LNEXT, p, last[p] + 1);
+              RW.st(PL_LMATCH, p, last[p]);
+              RW.st(PL_LNEXT, p, last[p] + 1);
             }
-            if (RW.at(PL_HWM, p) < last[p]) RW.template st<WT>(PL_HWM, p, last[p]);
+            if (RW.at(PL_HWM, p) < last[p]) RW.st(PL_HWM, p, last[p]);
           }
           meta &= ~(M_SSYNC | M_MSYNC);
           ss = false;
@@ -527,15 +515,15 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         sv[4] = 0;
         if (n) {
           if (!to_lxs) {
-            RW.template st<WT>(PL_LAST, c, Ll + n);
-            if (Llt != Lt) RW.template st<WT>(PL_LTERM, c, Lt);
+            RW.st(PL_LAST, c, Ll + n);
+            if (Llt != Lt) RW.st(PL_LTERM, c, Lt);
           }
           wr = 1u << c;                                   // only the leader's log grows
           w_term = Lt;
           w_ph = int((uint32_t(Ll) + uint32_t(GW.rot())) & P.kmask);
           w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
         }
-        if (cm != Lc && !to_lxs) RW.template st<WT>(PL_COMMIT, c, cm);
+        if (cm != Lc && !to_lxs) RW.st(PL_COMMIT, c, cm);
         int nm = (meta | M_MSYNC) & ~(M_SSYNC | M_HWX | M_LXS);   // (no truncated log here: hwup == 0)
         if (to_lxs) {
           const int f = c == 0 ? 1 : 0;   // any follower (SSYNC: one length, term, CommitIndex)
@@ -558,13 +546,13 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             mz[p] = 0;                            // w's rows: MatchIndex 0, NextIndex = its length + 1
             nx[p] = fl + 1;
             if (p == c) continue;
-            RW.template st<WT>(PL_TERM, p, nt);
-            RW.template st<WT>(PL_TSTART, p, T.now);   // candidate timer start / vote granted: timer reset
-            RW.template st<WT>(PL_RS, p, p == w ? int32_t(ROLE_L | (uint32_t(w + 1) << 2) | (uint32_t(dc) << 6))
+            RW.st(PL_TERM, p, nt);
+            RW.st(PL_TSTART, p, T.now);   // candidate timer start / vote granted: timer reset
+            RW.st(PL_RS, p, p == w ? int32_t(ROLE_L | (uint32_t(w + 1) << 2) | (uint32_t(dc) << 6))
                                                 : int32_t((rsv[p] & ~0x3F) | ROLE_F | ((w + 1) << 2)));
             // the cut-off leader's rows (implicit: MatchIndex = LastApplied) move to its xmatch / xnext rows
-            st<WT>(prow(P.xmatch, c * R + p, P.Gp), g, last[p]);
-            st<WT>(prow(P.xnext, c * R + p, P.Gp), g, last[p] + 1);
+            st(prow(P.xmatch, c * R + p, P.Gp), g, last[p]);
+            st(prow(P.xnext, c * R + p, P.Gp), g, last[p] + 1);
           }
           RW.store(PL_HWM, hwr);
           RW.store(PL_LMATCH, mz);
@@ -810,10 +798,10 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       if (keep_ss) {
         df |= 262144u;
         GW.ss() = SsRec{Ll + n, Lt, cm, cf};
-        GW.template st_hb<WT>(T.now);                                   // timer.Reset(d) of every follower
+        GW.st_hb(T.now);                                   // timer.Reset(d) of every follower
         if (RAFT && sr >= 0) {   // the returning stale leader stepped down: a follower (term, length: the record)
-          RW.template st<WT>(PL_RS, sr, int32_t(ROLE_F | (uint32_t(sr_dur) << 6)));   // votedFor none, new timer
-          RW.template st<WT>(PL_HWM, sr, sr_hw);   // (its timer starts now: hb)
+          RW.st(PL_RS, sr, int32_t(ROLE_F | (uint32_t(sr_dur) << 6)));   // votedFor none, new timer
+          RW.st(PL_HWM, sr, sr_hw);   // (its timer starts now: hb)
         }
       } else {
       if (ss) {   // leaving the compressed form: the rows as they stood, then the element stores below
@@ -829,8 +817,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         RW.store(PL_COMMIT, crow);
         RW.store(PL_LTERM, trow);
       }
-      const bool last_row = !WT && n && okm == peers;
-      const bool commit_row = !WT && cm != Lc && cch == peers;
+      const bool last_row = n && okm == peers;
+      const bool commit_row = cm != Lc && cch == peers;
       if (last_row || commit_row) {
         int lrow[R], crow[R];
 #pragma unroll
@@ -842,30 +830,30 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         if (commit_row) RW.store(PL_COMMIT, crow);
       }
       if (n) {
-        if (!last_row) RW.template st<WT>(PL_LAST, c, Ll + n);
-        if (Llt != Lt) RW.template st<WT>(PL_LTERM, c, Lt);
+        if (!last_row) RW.st(PL_LAST, c, Ll + n);
+        if (Llt != Lt) RW.st(PL_LTERM, c, Lt);
       }
-      if (cm != Lc && !commit_row) RW.template st<WT>(PL_COMMIT, c, cm);
-      if (xi < 0) GW.template st_hb<WT>(T.now);                         // timer.Reset(d) of every follower
+      if (cm != Lc && !commit_row) RW.st(PL_COMMIT, c, cm);
+      if (xi < 0) GW.st_hb(T.now);                         // timer.Reset(d) of every follower
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == c || !((okm >> p) & 1u)) continue;
-        if (xi >= 0) RW.template st<WT>(PL_TSTART, p, T.now);   // xi isolated: reset each receiver, not hb
-        if (n && !last_row) RW.template st<WT>(PL_LAST, p, last[p]);
-        if (!sync && ((mch >> p) & 1u)) RW.template st<WT>(PL_LMATCH, p, m[p]);
-        if (((cch >> p) & 1u) && !commit_row) RW.template st<WT>(PL_COMMIT, p, commit[p]);
-        if ((ltch >> p) & 1u) RW.template st<WT>(PL_LTERM, p, Lt);
-        if (!RAFT && term[p] != Lt) RW.template st<WT>(PL_TERM, p, Lt);  // main.go:155
-        if (RAFT && !sync && ((mch >> p) & 1u)) RW.template st<WT>(PL_LNEXT, p, m[p] + 1);   // NextIndex explicit too
+        if (xi >= 0) RW.st(PL_TSTART, p, T.now);   // xi isolated: reset each receiver, not hb
+        if (n && !last_row) RW.st(PL_LAST, p, last[p]);
+        if (!sync && ((mch >> p) & 1u)) RW.st(PL_LMATCH, p, m[p]);
+        if (((cch >> p) & 1u) && !commit_row) RW.st(PL_COMMIT, p, commit[p]);
+        if ((ltch >> p) & 1u) RW.st(PL_LTERM, p, Lt);
+        if (!RAFT && term[p] != Lt) RW.st(PL_TERM, p, Lt);  // main.go:155
+        if (RAFT && !sync && ((mch >> p) & 1u)) RW.st(PL_LNEXT, p, m[p] + 1);   // NextIndex explicit too
         if (RAFT && !sync && n) {   // high-water mark = max(itself, new length)
           const int h = ((hwup >> p) & 1u) ? RW.at(PL_HWM, p) : 0;
-          if (h < last[p]) RW.template st<WT>(PL_HWM, p, last[p]);
+          if (h < last[p]) RW.st(PL_HWM, p, last[p]);
         }
       }
       if constexpr (RAFT) {
         if (!sync && n) {   // the leader's high-water mark
           const int h = ((hwup >> c) & 1u) ? RW.at(PL_HWM, c) : 0;
-          if (h < Ll + n) RW.template st<WT>(PL_HWM, c, Ll + n);
+          if (h < Ll + n) RW.st(PL_HWM, c, Ll + n);
         }
         if (stale) {
           // the stale leader's own client append (main.go:327-329) at its own log's end
@@ -880,25 +868,25 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             for (int e = 0; e < n; ++e) {
               const int64_t v = int64_t(sm64(xvb ^ uint64_t(uint32_t(e))) >> 1);
               const uint32_t o = ring_in_tile(g, R, ring_slot(xl + 1 + e, xrot, xrota, xrotb, xsb, xsb2, P.kmask), uint32_t(xi));
-              rst<WT>(P.log_term + tb, o, x_term);
-              rst<WT>(P.log_value + tb, o, v);
-              if constexpr (CRC) rst<WT>(P.log_crc + tb, o, crc_value_final(tab, cs, v));
+              ring_st(P.log_term + tb, o, x_term);
+              ring_st(P.log_value + tb, o, v);
+              if constexpr (CRC) ring_st(P.log_crc + tb, o, crc_value_final(tab, cs, v));
             }
-            RW.template st<WT>(PL_LAST, xi, xl + n);
-            if (sel(lt, xi) != x_term) RW.template st<WT>(PL_LTERM, xi, x_term);
-            if (RW.at(PL_HWM, xi) < xl + n) RW.template st<WT>(PL_HWM, xi, xl + n);
+            RW.st(PL_LAST, xi, xl + n);
+            if (sel(lt, xi) != x_term) RW.st(PL_LTERM, xi, x_term);
+            if (RW.at(PL_HWM, xi) < xl + n) RW.st(PL_HWM, xi, xl + n);
           }
         }
         if (x_fire) {   // the isolated replica became / stays a candidate: Term+1, votedFor itself
-          RW.template st<WT>(PL_TERM, xi, x_term + 1);
-          RW.template st<WT>(PL_RS, xi, int32_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
-          RW.template st<WT>(PL_TSTART, xi, T.now);
+          RW.st(PL_TERM, xi, x_term + 1);
+          RW.st(PL_RS, xi, int32_t(ROLE_C | (uint32_t(xi + 1) << 2) | (uint32_t(x_dur) << 6)));
+          RW.st(PL_TSTART, xi, T.now);
         }
         if (sr >= 0) {   // the returning stale leader stepped down: a follower of the primary's term
-          RW.template st<WT>(PL_TERM, sr, Lt);
-          RW.template st<WT>(PL_RS, sr, int32_t(ROLE_F | (uint32_t(sr_dur) << 6)));   // votedFor none
-          RW.template st<WT>(PL_TSTART, sr, T.now);
-          RW.template st<WT>(PL_HWM, sr, sr_hw);
+          RW.st(PL_TERM, sr, Lt);
+          RW.st(PL_RS, sr, int32_t(ROLE_F | (uint32_t(sr_dur) << 6)));   // votedFor none
+          RW.st(PL_TSTART, sr, T.now);
+          RW.st(PL_HWM, sr, sr_hw);
         }
       }
       }   // !keep_ss
@@ -926,7 +914,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           if (sx) {
             GW.ss() = SsRec{Ll + n, Lt, cm, cf};
             GW.lx() = LxRec{sel(last, xi) + n - (Ll + n), xi};
-            GW.template st_hb<WT>(T.now);   // (the stale leader's timer ignores hb: a leader's start is its own)
+            GW.st_hb(T.now);   // (the stale leader's timer ignores hb: a leader's start is its own)
             nm |= M_SSYNC | M_MSYNC;
             df |= 1u << 30;   // class: entered SXS
           }
@@ -1013,9 +1001,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
               if (p != c && !((okm >> p) & 1u)) continue;
               const int i0 = p == c ? Ll : last[p] - n;
               const uint32_t o = ring_in_tile(g, R, ring_slot(i0 + e + 1, uint32_t(rot), rota, rotb, sb, sb2, P.kmask), uint32_t(p));
-              rst<WT>(P.log_term + tb, o, Lt);
-              rst<WT>(P.log_value + tb, o, v);
-              if constexpr (CRC) rst<WT>(P.log_crc + tb, o, stamp);
+              ring_st(P.log_term + tb, o, Lt);
+              ring_st(P.log_value + tb, o, v);
+              if constexpr (CRC) ring_st(P.log_crc + tb, o, stamp);
             }
           }
         }
@@ -1132,7 +1120,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         uint32_t stamp = 0;
         if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
         const uint32_t o = ring_in_tile(g, R, uint32_t((w_ph + e) & int(P.kmask)), 0u);
-        if (!WT && wr == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
+        if (wr == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
           fill_seg<R>(rt + o, w_term);
           fill_seg<R>(rv + o, v);
           if constexpr (CRC) fill_seg<R>(rc + o, stamp);
@@ -1140,9 +1128,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
 #pragma unroll
           for (int p = 0; p < R; ++p) {
             if (!((wr >> p) & 1u)) continue;
-            rst<WT>(rt, o + p, w_term);
-            rst<WT>(rv, o + p, v);
-            if constexpr (CRC) rst<WT>(rc, o + p, stamp);
+            ring_st(rt, o + p, w_term);
+            ring_st(rv, o + p, v);
+            if constexpr (CRC) ring_st(rc, o + p, stamp);
           }
         }
       }
@@ -1151,9 +1139,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
 #pragma unroll
       for (int k = 0; k < CPS; ++k) {
         if (!con[k]) continue;
-        rst<WT>(P.log_term + ctb[k], cdst[k], ct[k]);
-        rst<WT>(P.log_value + ctb[k], cdst[k], cv[k]);
-        if constexpr (CRC) rst<WT>(P.log_crc + ctb[k], cdst[k], cc[k]);
+        ring_st(P.log_term + ctb[k], cdst[k], ct[k]);
+        ring_st(P.log_value + ctb[k], cdst[k], cv[k]);
+        if constexpr (CRC) ring_st(P.log_crc + ctb[k], cdst[k], cc[k]);
       }
     }
   }
@@ -1200,14 +1188,14 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             if constexpr (CRC) sk = uint32_t(__shfl(int(stamp), k_src[k]));
             if (k_on[k]) {
               const uint32_t o = row + uint32_t(k * 64 + lane);
-              rst<WT>(rt, o, k_term[k]);
-              rst<WT>(rv, o, int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo)));
-              if constexpr (CRC) rst<WT>(rc, o, sk);
+              ring_st(rt, o, k_term[k]);
+              ring_st(rv, o, int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo)));
+              if constexpr (CRC) ring_st(rc, o, sk);
             }
           }
           if (wr != 0 && !coop) {   // drifted lane: its own segment
             const uint32_t o = ring_in_tile(g, R, uint32_t((w_ph + e) & int(P.kmask)), 0u);
-            if (!WT && wr == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
+            if (wr == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
               fill_seg<R>(rt + o, w_term);
               fill_seg<R>(rv + o, v);
               if constexpr (CRC) fill_seg<R>(rc + o, stamp);
@@ -1215,9 +1203,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
 #pragma unroll
               for (int p = 0; p < R; ++p) {
                 if (!((wr >> p) & 1u)) continue;
-                rst<WT>(rt, o + p, w_term);
-                rst<WT>(rv, o + p, v);
-                if constexpr (CRC) rst<WT>(rc, o + p, stamp);
+                ring_st(rt, o + p, w_term);
+                ring_st(rv, o + p, v);
+                if constexpr (CRC) ring_st(rc, o + p, stamp);
               }
             }
           }
@@ -1292,14 +1280,14 @@ __device__ __forceinline__ void stage_crc_tab(const DevPlanes& P, uint32_t* tab)
 }
 
 // Every group, one lane each (the single-pass plan).
-template <int R, bool WT, bool CRC, int SEM>
+template <int R, bool CRC, int SEM>
 __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, unsigned long long* stats,
                                                         uint32_t* work, int32_t* work_tick, uint32_t* work_count,
                                                         int force_slow) {
   __shared__ uint32_t tab[CRC ? 2048 : 1];
   stage_crc_tab<CRC>(P, tab);
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-  fast_group<R, WT, CRC, SEM, false>(P, T, stats, work, work_tick, work_count, force_slow, g, tab,
+  fast_group<R, CRC, SEM, false>(P, T, stats, work, work_tick, work_count, force_slow, g, tab,
                                      rows_global<R>(P, g), words_global(P, g));
 }
 
@@ -1315,7 +1303,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
 // (RowAcc / WordAcc over the __shared__ arrays: ds_ instructions), and
 // writes back the records
 // it may have changed (coalesced) and the per-group words that did change.
-template <int R, bool WT, bool CRC, int SEM, int LB>
+template <int R, bool CRC, int SEM, int LB>
 __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, unsigned long long* stats,
                                                         uint32_t* work, int32_t* work_tick, uint32_t* work_count,
                                                         const uint32_t* list, const uint32_t* count,
@@ -1381,11 +1369,11 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     // (P.diag, timing only, results wrong: 32 = staging alone, 64 = staging and write-back, no tick)
     if (P.diag & 32u) { __syncthreads(); continue; }
     bool wrote = (P.diag & 64u) ? valid
-                                : fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab,
+                                : fast_group<R, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab,
                                                                     rw, gw);
     if (steps > 1) {   // the following tick too, on the staged state (pipelined tick)
       __threadfence_block();   // this step's ring stores, seen by the next step's gathers
-      wrote |= fast_group<R, WT, CRC, SEM, true>(P, T.at_tick(T.tick + 1), nx.stats, nx.work, nx.work_tick,
+      wrote |= fast_group<R, CRC, SEM, true>(P, T.at_tick(T.tick + 1), nx.stats, nx.work, nx.work_tick,
                                                  nx.work_count, 0, g, tab, rw, gw);
     }
     {   // dirty rows -> the 16-B pieces of the record they touch
@@ -1419,33 +1407,6 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       if (s1.last != ss0.last || s1.term != ss0.term || s1.cl != ss0.cl || s1.cf != ss0.cf) P.gss[g] = s1;
     }
     __syncthreads();   // the LDS copies and the body's block reductions are reused next round
-  }
-}
-
-// The same over the list without staging: each lane reads its group's rows
-// and words from HBM itself (A/B: RAFTSTEP_LIST_STAGE=0).
-template <int R, bool WT, bool CRC, int SEM>
-__global__ __launch_bounds__(256) void tick_list_plain_kernel(DevPlanes P, Trace T, unsigned long long* stats,
-                                                              uint32_t* work, int32_t* work_tick, uint32_t* work_count,
-                                                              const uint32_t* list, const uint32_t* count,
-                                                              uint32_t* next_count, int steps, ListNext nx) {
-  __shared__ uint32_t tab[CRC ? 2048 : 1];
-  __shared__ uint32_t pre[NSHARD + 1];
-  shard_zero(next_count);
-  const uint32_t n = shard_prefix(count, pre);
-  if (blockIdx.x * 256u >= n) return;
-  stage_crc_tab<CRC>(P, tab);
-  for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
-    const uint32_t i = base + threadIdx.x;
-    const uint32_t g = i < n ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
-    fast_group<R, WT, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab, rows_global<R>(P, g),
-                                      words_global(P, g));
-    if (steps > 1) {
-      __threadfence_block();
-      fast_group<R, WT, CRC, SEM, true>(P, T.at_tick(T.tick + 1), nx.stats, nx.work, nx.work_tick, nx.work_count, 0, g,
-                                        tab, rows_global<R>(P, g), words_global(P, g));
-    }
-    __syncthreads();   // the body's block reductions reuse their LDS words next round
   }
 }
 
@@ -1966,30 +1927,26 @@ hipError_t launch_tick_fused(int R, int sem, const DevPlanes& P, const Trace& T,
   return hipGetLastError();
 }
 
-template <int R, bool WT, bool CRC, int SEM>
+template <int R, bool CRC, int SEM>
 static void launch_fast_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                           int32_t* work_tick, uint32_t* work_count, int force_slow, hipStream_t s, hipEvent_t a,
                           hipEvent_t b) {
-  hipExtLaunchKernelGGL(tick_fast_kernel<R, WT, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, work,
+  hipExtLaunchKernelGGL(tick_fast_kernel<R, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, work,
                         work_tick, work_count, force_slow);
 }
 hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
-                            int32_t* work_tick, uint32_t* work_count, int force_slow, int write_through, hipStream_t s,
+                            int32_t* work_tick, uint32_t* work_count, int force_slow, hipStream_t s,
                             hipEvent_t ev_start, hipEvent_t ev_stop) {
   const bool crc = P.crc_on != 0;
-#define RAFT_FAST(WT_, CRC_)                                                                                      \
+#define RAFT_FAST(CRC_)                                                                                            \
   if (sem == SEM_RAFT) {                                                                                           \
-    RAFT_DISPATCH_R(R, (launch_fast_t<RR, WT_, CRC_, SEM_RAFT>(P, T, stats, work, work_tick, work_count, force_slow, \
-                                                               s, ev_start, ev_stop)))                              \
+    RAFT_DISPATCH_R(R, (launch_fast_t<RR, CRC_, SEM_RAFT>(P, T, stats, work, work_tick, work_count, force_slow, s, \
+                                                          ev_start, ev_stop)))                                     \
   } else {                                                                                                         \
-    RAFT_DISPATCH_R(R, (launch_fast_t<RR, WT_, CRC_, SEM_REF>(P, T, stats, work, work_tick, work_count, force_slow,  \
-                                                              s, ev_start, ev_stop)))                               \
+    RAFT_DISPATCH_R(R, (launch_fast_t<RR, CRC_, SEM_REF>(P, T, stats, work, work_tick, work_count, force_slow, s,  \
+                                                         ev_start, ev_stop)))                                      \
   }
-  if (write_through) {
-    if (crc) { RAFT_FAST(true, true); } else { RAFT_FAST(true, false); }
-  } else {
-    if (crc) { RAFT_FAST(false, true); } else { RAFT_FAST(false, false); }
-  }
+  if (crc) { RAFT_FAST(true); } else { RAFT_FAST(false); }
 #undef RAFT_FAST
   return hipGetLastError();
 }
@@ -2005,36 +1962,15 @@ template <int R, bool CRC, int SEM>
 static void launch_list_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                           int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
                           uint32_t* next_count, const ListNext* next, hipStream_t s, hipEvent_t c, hipEvent_t d) {
-  static const bool stage = [] {
-    const char* v = getenv("RAFTSTEP_LIST_STAGE");
-    return !v || atoi(v) != 0;
-  }();
   const int steps = next ? 2 : 1;
   const ListNext nx = next ? *next : ListNext{nullptr, nullptr, nullptr, nullptr};
-  // list blocks of four waves (default); RAFTSTEP_LIST_BLOCK=64 for one-wave
-  // blocks (no block barrier waits on another wave): the same list kernel
-  // time on C4, but the following lean kernel measured 15% slower (A/B in
-  // tools/gpu_r2_lb.sh)
-  static const int lb = [] {
-    const char* v = getenv("RAFTSTEP_LIST_BLOCK");
-    return (v && atoi(v) == 64) ? 64 : 256;
-  }();
-  if (stage && lb == 64) {
-    const unsigned blocks = unsigned(
-        std::min<uint64_t>((P.G + 63) / 64, resident_blocks(tick_list_kernel<R, false, CRC, SEM, 64>, 64)));
-    hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM, 64>, dim3(blocks), dim3(64), 0, s, c, d, 0, P, T, stats,
-                          work, work_tick, work_count, list, count, next_count, steps, nx);
-  } else if (stage) {
-    const unsigned blocks = unsigned(
-        std::min<uint64_t>((P.G + 255) / 256, resident_blocks(tick_list_kernel<R, false, CRC, SEM, 256>, 256)));
-    hipExtLaunchKernelGGL(tick_list_kernel<R, false, CRC, SEM, 256>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats,
-                          work, work_tick, work_count, list, count, next_count, steps, nx);
-  } else {
-    const unsigned blocks = unsigned(
-        std::min<uint64_t>((P.G + 255) / 256, resident_blocks(tick_list_plain_kernel<R, false, CRC, SEM>)));
-    hipExtLaunchKernelGGL(tick_list_plain_kernel<R, false, CRC, SEM>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T,
-                          stats, work, work_tick, work_count, list, count, next_count, steps, nx);
-  }
+  // blocks of four waves, a resident grid striding over the list (one-wave
+  // blocks measured the same list kernel time on C4 and a 15% slower lean
+  // kernel beside it, round 2)
+  const unsigned blocks =
+      unsigned(std::min<uint64_t>((P.G + 255) / 256, resident_blocks(tick_list_kernel<R, CRC, SEM, 256>, 256)));
+  hipExtLaunchKernelGGL(tick_list_kernel<R, CRC, SEM, 256>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats, work,
+                        work_tick, work_count, list, count, next_count, steps, nx);
 }
 
 template <int R, bool CRC, int SEM>

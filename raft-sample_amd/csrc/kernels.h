@@ -1,6 +1,6 @@
 // kernels.h — host-side launchers and device argument records of the engine.
 //
-//  tick_fast_kernel<R,WT,CRC,SEM> (k_fast.hip): steady-state tick, one lane
+//  tick_fast_kernel<R,CRC,SEM> (k_fast.hip): steady-state tick, one lane
 //        per group, HBM-bound (~233 B per group-step at R=5, E=1); groups it
 //        cannot take go to a worklist.
 //  tick_slow_kernel<R,SEM> (k_ref.hip / k_raft.hip): the general tick
@@ -41,7 +41,7 @@ struct DevRes {
 // Steady-state fast kernel; groups it does not take are DEFERred to `work`.
 // ev_start/ev_stop (may be null) time the dispatch itself (hipExtLaunchKernel).
 hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
-                            int32_t* work_tick, uint32_t* work_count, int force_slow, int write_through, hipStream_t s,
+                            int32_t* work_tick, uint32_t* work_count, int force_slow, hipStream_t s,
                             hipEvent_t ev_start, hipEvent_t ev_stop);
 // Two-pass tick: tick_lean_kernel takes the compressed steady groups and
 // appends every other live group to `list` (counter `count`), then

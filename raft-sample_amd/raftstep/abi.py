@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-RAFT_ABI_VERSION = 4
+RAFT_ABI_VERSION = 5
 RAFT_MAX_REPLICAS = 8
 
 FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
@@ -25,6 +25,8 @@ OP_CLIENT_APPEND, OP_LEADER_ROUND, OP_CANDIDATE_ROUND, OP_TIMEOUT, OP_LEADER_COM
 
 RAFT_EINVAL, RAFT_ENOMEM, RAFT_ERANGE, RAFT_ENODEV = -22, -12, -34, -19
 RAFT_EINTERNAL = -3000
+
+DEBUG_ALLOW_WRONG_RESULTS = 1   # raft_config.debug_flags: accept RAFTSTEP_DIAG_LEAN (timing only, results wrong)
 
 # raft_diag_read counters (include/raftstep.h enum raft_diag_counter)
 DIAG_COUNTERS = 72
@@ -56,7 +58,8 @@ class Config(C.Structure):
         ("device", C.c_int32),
         ("payload_crc", C.c_uint32), ("corrupt_per_65536", C.c_uint32),
         ("isolate_leader", C.c_uint32),
-        ("reserved", C.c_uint32 * 5),
+        ("ticks_per_launch", C.c_uint32), ("debug_flags", C.c_uint32),
+        ("reserved", C.c_uint32 * 3),
     ]
 
 
@@ -80,6 +83,8 @@ def default_config(**kw):
     c.payload_crc = 0
     c.corrupt_per_65536 = 0
     c.isolate_leader = 0
+    c.ticks_per_launch = 1    # one tick per launch
+    c.debug_flags = 0
     for k, v in kw.items():
         if not hasattr(c, k):
             raise TypeError(f"unknown config field {k!r}")

@@ -27,7 +27,9 @@ import numpy as np
 from . import abi
 
 FORMAT = "raftstep-trace/1"
-CONFIG_FIELDS = [name for name, _ in abi.Config._fields_ if name not in ("abi_version", "reserved")]
+# (execution knobs that cannot change results are not part of a trace)
+CONFIG_FIELDS = [name for name, _ in abi.Config._fields_
+                 if name not in ("abi_version", "reserved", "ticks_per_launch", "debug_flags")]
 
 
 def config_dict(cfg):

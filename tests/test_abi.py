@@ -81,6 +81,8 @@ def test_missing_library_fails_loudly(tmp_path):
     ("replicas", 9, "replicas"),
     ("ring_depth", 24, "power of two"),
     ("isolate_leader", 2, "isolate_leader"),
+    ("ticks_per_launch", 65, "ticks_per_launch"),
+    ("debug_flags", 2, "debug_flags"),
 ])
 def test_engine_create_rejects_bad_configs_before_touching_a_gpu(field, value, msg):
     """Config validation runs before any HIP call, so it is checkable here."""
@@ -134,3 +136,29 @@ def test_coerce_state_checks_dtype_shape_and_optional_fields():
     missing = {k: v for k, v in st.items() if k != "fault"}
     with pytest.raises(KeyError):
         abi.coerce_state(missing, G, R, K)
+
+
+def test_results_altering_env_knob_is_refused_without_the_debug_flag(monkeypatch):
+    """RAFTSTEP_DIAG_LEAN skips work (timing diagnostics): raft_engine_create
+    refuses it unless debug_flags says wrong results are acceptable. The check
+    runs before any HIP call."""
+    lib = engine.load_library()
+    h = C.c_void_p()
+    monkeypatch.setenv("RAFTSTEP_DIAG_LEAN", "64")
+    c = abi.default_config(groups=256)
+    assert lib.raft_engine_create(C.byref(c), C.byref(h)) == abi.RAFT_EINVAL and not h.value
+    assert "RAFTSTEP_DIAG_LEAN" in lib.raft_last_error().decode()
+    c = abi.default_config(groups=256, debug_flags=abi.DEBUG_ALLOW_WRONG_RESULTS)
+    rc = lib.raft_engine_create(C.byref(c), C.byref(h))   # accepted by validation (no device here)
+    assert rc != abi.RAFT_EINVAL or "RAFTSTEP_DIAG_LEAN" not in lib.raft_last_error().decode()
+    if h.value:
+        lib.raft_engine_destroy(h)
+
+
+def test_reserved_config_words_must_be_zero():
+    lib = engine.load_library()
+    c = abi.default_config()
+    c.reserved[1] = 7
+    h = C.c_void_p()
+    assert lib.raft_engine_create(C.byref(c), C.byref(h)) == abi.RAFT_EINVAL
+    assert "reserved" in lib.raft_last_error().decode()

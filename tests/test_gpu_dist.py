@@ -74,16 +74,18 @@ def test_group_base_shards_are_invariant():
     harness.assert_same_state(joined, f, "sharded")
 
 
-def test_fused_steady_ticks_with_communicator():
-    """The steady-state list skip with fused ticks (4 per launch) under a
-    single-rank communicator: per-window stats all-reduced on the side stream
-    equal the oracle's per-tick stats, calls of lengths that split the fused
-    launches and the 8-tick windows differently."""
+@pytest.mark.parametrize("tpl", [1, 4, 16])
+def test_steady_ticks_with_communicator(tpl):
+    """The steady-state list skip under a single-rank communicator, one tick
+    per launch (the default) and fused (raft_config
+    ticks_per_launch 4 and 16): per-window stats all-reduced on the side
+    stream equal the oracle's per-tick stats, calls of lengths that split the
+    fused launches and the 8-tick windows differently."""
     from raftstep import Engine
     import oracle
     import harness
     kw = dict(replicas=5, groups=5000, ring_depth=32, client_period=1, seed=0x5EED0003)
-    e, o = Engine(**kw), oracle.Oracle(**kw)
+    e, o = Engine(ticks_per_launch=tpl, **kw), oracle.Oracle(**kw)
     e.comm_init(1, 0, Engine.comm_unique_id())
     e.init_steady(0, 0)
     o.init_steady(0, 0)

@@ -17,8 +17,14 @@ pytestmark = pytest.mark.gpu
 KW = dict(replicas=5, groups=3000, ring_depth=16, client_period=1, seed=0x5EED0002)
 
 
-def steady_pair():
-    e, o = Engine(**KW), oracle.Oracle(**KW)
+@pytest.fixture(params=[1, 16], ids=["one_tick_per_launch", "fused16"])
+def tpl(request):
+    """raft_config.ticks_per_launch: the §8(d) form and the fused steady ticks"""
+    return request.param
+
+
+def steady_pair(tpl=1):
+    e, o = Engine(ticks_per_launch=tpl, **KW), oracle.Oracle(**KW)
     e.init_steady(0, 0)
     o.init_steady(0, 0)
     assert list(e.tick(1, 6)) == list(o.tick(1, 6))   # proves the list empty: the next calls skip it
@@ -45,8 +51,8 @@ def test_forced_pass_is_exact_while_the_list_kernel_runs():
     assert c["ticks_list_skipped"] == 0, c
 
 
-def test_skip_violation_fails_in_the_call_with_statistics():
-    e, o = steady_pair()
+def test_skip_violation_fails_in_the_call_with_statistics(tpl):
+    e, o = steady_pair(tpl)
     assert list(e.tick(7, 5)) == list(o.tick(7, 5))    # skipped and exact
     assert e.diag_read()["ticks_list_skipped"] == 5
     e.debug_force_pass(42)
@@ -64,8 +70,8 @@ def test_skip_violation_fails_in_the_call_with_statistics():
     H.assert_same_state(e.store_state(), o.store_state(), "after reload")
 
 
-def test_skip_violation_fails_at_the_call_after_a_stats_less_call():
-    e, o = steady_pair()
+def test_skip_violation_fails_at_the_call_after_a_stats_less_call(tpl):
+    e, o = steady_pair(tpl)
     e.tick(7, 5, stats=False)             # skipped, checked at the next call: clean
     e.tick(12, 3, stats=False)
     e.debug_force_pass(99)
@@ -83,8 +89,8 @@ def test_skip_violation_fails_at_the_call_after_a_stats_less_call():
     H.assert_same_state(e.store_state(), o2.store_state(), "after init_steady")
 
 
-def test_stats_less_skipped_calls_stay_exact():
-    e, o = steady_pair()
+def test_stats_less_skipped_calls_stay_exact(tpl):
+    e, o = steady_pair(tpl)
     t = 7
     for k in (5, 1, 13, 2):
         e.tick(t, k, stats=False)
@@ -95,6 +101,32 @@ def test_stats_less_skipped_calls_stay_exact():
     c = e.diag_read()
     assert c["ticks_list_skipped"] == 21 and c["general_launches"] == 0, c
     assert list(e.tick(t, 4)) == list(o.tick(t, 4))
+
+
+def test_failed_state_replacement_keeps_the_poison(tmp_path, tpl):
+    """a call that would replace the state but fails before doing
+    so (missing checkpoint, bad view, out-of-range tick) leaves a poisoned
+    engine poisoned; a successful replacement clears it."""
+    e, o = steady_pair(tpl)
+    assert list(e.tick(7, 5)) == list(o.tick(7, 5))
+    e.debug_force_pass(42)
+    with pytest.raises(RaftError, match="list kernel that did not run"):
+        e.tick(12, 4)
+    e.debug_force_pass(-1)
+    with pytest.raises(RaftError):
+        e.load_checkpoint(tmp_path / "missing.ckpt")
+    with pytest.raises(RaftError):
+        e.init_steady(0, 1 << 40)         # virtual time out of int32: refused before any launch
+    bad = o.store_state()
+    bad["role"] = np.full_like(bad["role"], 9)
+    with pytest.raises(RaftError):
+        e.load_state(bad)
+    with pytest.raises(RaftError, match="engine state is invalid") as ei:
+        e.tick(12, 1)
+    assert ei.value.code == abi.RAFT_EINTERNAL
+    e.load_state(o.store_state())         # replaced: usable again
+    assert list(e.tick(12, 3)) == list(o.tick(12, 3))
+    H.assert_same_state(e.store_state(), o.store_state(), "after the reload")
 
 
 def test_tick_records_refuses_more_than_the_last_call_produced():

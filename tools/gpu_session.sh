@@ -1,0 +1,50 @@
+#!/bin/bash
+# One GPU session (run through gpurun from the repo root): the steps named on
+# the command line, in order, each under its own time limit; the first
+# failure ends the session. Output under gpurun_out/$OUTDIR.
+#   tests     the whole -m gpu suite
+#   bench     bench.py with the driver's protocol (--steps 20 --warmup 5): the
+#             C2 headline + fused block + C4 / C5 extra workloads
+#   prof      rocprofv3 --kernel-trace --stats of the C2 headline line (same
+#             protocol, one repeat; the lean kernel's mean duration)
+#   profc4    the same for C4 (lean + list kernels)
+#   pmc       FETCH_SIZE / WRITE_SIZE passes (separate runs) of the calibration
+#             kernel and of the C2 headline (tools/pmc_summary.py)
+#   pmcc4     the same for C4 (lean and list kernels)
+#   smoke     __graft_entry__.smoke()
+#   bench:ARGS  bench.py with extra arguments (ARGS: comma-separated)
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out/${OUTDIR:-r4}
+mkdir -p "$OUT"
+B="python3 -u bench.py --steps 20 --warmup 5"
+Q="--steps 20 --warmup 5 --repeats 1 --no-cpu-baseline --no-fused --extra none"
+P="timeout -s KILL 120 rocprofv3"
+log() { echo "== $(date +%T) $*" >> "$OUT/progress.log"; }
+n=0
+for s in "$@"; do
+  n=$((n + 1))
+  log "$s"
+  case "$s" in
+    tests) timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+             > "$OUT/gpu_tests.log" 2>&1 ;;
+    smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+    bench) timeout -k 10 600 $B > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    bench:*) a="${s#bench:}"; timeout -k 10 600 $B ${a//,/ } > "$OUT/bench_$n.json" 2> "$OUT/bench_$n.err" ;;
+    prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c2" -o run --output-format csv \
+            -- python3 -u bench.py $Q > "$OUT/prof_c2.log" 2>&1 ;;
+    profc4) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o run --output-format csv \
+              -- python3 -u bench.py --workload C4 $Q > "$OUT/prof_c4.log" 2>&1 ;;
+    pmc) $P --pmc FETCH_SIZE -d "$OUT/pmc_calib_fetch" -o p --output-format csv -- ./tools/pmc_calib > "$OUT/pmc1.log" 2>&1 \
+         && $P --pmc WRITE_SIZE -d "$OUT/pmc_calib_write" -o p --output-format csv -- ./tools/pmc_calib > "$OUT/pmc2.log" 2>&1 \
+         && $P --pmc FETCH_SIZE -d "$OUT/pmc_c2_fetch" -o p --output-format csv -- python3 -u bench.py $Q > "$OUT/pmc3.log" 2>&1 \
+         && $P --pmc WRITE_SIZE -d "$OUT/pmc_c2_write" -o p --output-format csv -- python3 -u bench.py $Q > "$OUT/pmc4.log" 2>&1 ;;
+    pmcc4) $P --pmc FETCH_SIZE -d "$OUT/pmc_c4_fetch" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc5.log" 2>&1 \
+           && $P --pmc WRITE_SIZE -d "$OUT/pmc_c4_write" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc6.log" 2>&1 ;;
+    *) echo "unknown step $s" >&2; exit 2 ;;
+  esac
+  rc=$?
+  if [ $rc -ne 0 ]; then log "$s failed rc=$rc"; echo "step $s failed rc=$rc"; exit $rc; fi
+done
+log done
