@@ -115,13 +115,18 @@ struct raft_engine {
   // kernels, catching its groups up through that tick too (they keep DEFER,
   // so the fast kernels leave them alone); the engine stream then waits for
   // it and runs the window tail (DEFER cleared) before the tick after.
-  // RAFTSTEP_OVERLAP_GENERAL=0 runs it in line (A/B; not with the pipeline).
-  int overlap_general = 1;
+  // RAFTSTEP_OVERLAP_GENERAL=0 runs it in line (not with the pipeline); d >= 1
+  // overlaps it with the next d ticks (it catches its groups up through tick
+  // t+d, the engine stream joins it before tick t+d+1). Exact for every d
+  // (tests/test_gpu_pipeline.py).
+  int overlap_general = 2;
   hipStream_t gen_stream = nullptr;
   hipEvent_t gen_ev[2] = {nullptr, nullptr};   // engine -> gen_stream, gen_stream -> engine
   bool gen_pending = false;     // a general kernel is running on gen_stream
   int gen_parity = 0;           // its worklist parity
   uint32_t gen_w0 = 0, gen_w1 = 0;   // its window's stats range (indices into the call's ticks)
+  uint32_t gen_join = 0;        // the call's tick index after whose launches the engine stream joins it
+  uint32_t gen_top = 0;         // the last tick index it counts stats into
   bool gen_stats = false;       // it counts into those per-tick slots of hist
   int force_general = 0;        // debug: route every group through the general kernel
   int lane_general = 0;         // RAFTSTEP_GENERAL=lane: one-lane-per-group general kernel (A/B) instead of the segment one
@@ -552,7 +557,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* dp = getenv("RAFTSTEP_DEBUG_PIPE")) e->debug_pipe = atoi(dp) != 0;
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
   e->P.diag = diag_lean;
-  if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = atoi(og) != 0;
+  if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = std::min(4, std::max(0, atoi(og)));
   if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = atoi(pp) != 0;
   e->fuse = std::max<uint32_t>(1u, c.ticks_per_launch);
   e->P.dbg_pass = 0xFFFFFFFFu;
@@ -992,7 +997,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     // re-zeroes them): zero them, or the next call's stats would include them
     if (e->gen_stats)
       HIPCHK(hipMemsetAsync(e->hist + size_t(e->gen_w0) * STAT_SLOTS * NSTAT, 0,
-                            size_t(e->gen_w1 - e->gen_w0 + 1) * STAT_SLOTS * NSTAT * 8, e->stream));
+                            size_t(e->gen_top - e->gen_w0 + 1) * STAT_SLOTS * NSTAT * 8, e->stream));
   }
   // (the per-tick records need nticks slots; the check records exist at any capacity)
   if (int rc = ensure_hist(e, stats ? std::max<uint32_t>(nticks, 1) : 1)) return rc;
@@ -1100,7 +1105,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     // kernels: the engine stream waits for it, then its window tail clears
     // its groups' DEFER (before the next tick's lean kernel) and its ticks'
     // records are final
-    if (e->gen_pending)
+    if (e->gen_pending && i >= e->gen_join)
       if (int rc = join_general(e, stats)) return rc;
     // deferred groups catch up every slow_every ticks and at the end of the call
     if ((i + 1) % e->slow_every == 0 || i + 1 == nticks) {
@@ -1124,12 +1129,15 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       // so the pipeline always takes this form)
       const bool overlap = !skip_list && two && (e->overlap_general || pipe) && !last && !e->debug_work;
       if (overlap) {
-        // beside tick t+1's lean and list kernels, through tick t+1 (its groups
-        // keep DEFER, so those kernels leave them alone; tick t+1's deferrals
-        // go to the other worklist)
+        // beside the lean and list kernels of ticks t+1 .. t+d, through tick
+        // t+d (its groups keep DEFER, so those kernels leave them alone; their
+        // deferrals go to the other worklist): d = the overlap depth, within
+        // the call and at most one window (the next window's general kernel
+        // starts after this one has joined)
+        const uint32_t d = std::min<uint32_t>({uint32_t(std::max(e->overlap_general, 1)), e->slow_every, nticks - 1 - i});
         HIPCHK(hipEventRecord(e->gen_ev[0], after));
         HIPCHK(hipStreamWaitEvent(e->gen_stream, e->gen_ev[0], 0));
-        HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t + 1,
+        HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t + int64_t(d),
                                 stats ? e->hist : nullptr, e->work[par], e->work_tick[par], cnt, nullptr,
                                 e->lane_general, e->gen_stream));
         HIPCHK(hipEventRecord(e->gen_ev[1], e->gen_stream));
@@ -1137,6 +1145,8 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         e->gen_parity = par;
         e->gen_w0 = stats_first;
         e->gen_w1 = i;
+        e->gen_join = i + d;
+        e->gen_top = i + d;
         e->gen_stats = stats;
         ++e->n_general;
       } else if (!skip_list) {

@@ -3,6 +3,22 @@
 
 namespace raftstep {
 
+// Diagnostics build only (make DIAG=1 / -DRAFTSTEP_WAVE_PROF): lane 0 of
+// every list-kernel wave adds the cycles (s_memtime) it spent in each phase
+// to the device counters (P.dbg, raft_diag_read) instead of the class
+// counts: [0] staging, [1] step 1, [2] step 2, [3] write-back, [4] waves,
+// [5] max wave cycles, [6..21] log2 histogram of a wave's cycles; inside
+// fast_group (list steps): [32] per-group code, [33] copy gathers, [34] own
+// ring writes, [35] copy scatters, [36] worklist + stats, [37] steps.
+#ifdef RAFTSTEP_WAVE_PROF
+#define WPROF(...) __VA_ARGS__
+__device__ __forceinline__ void wprof_add(unsigned long long* d, int k, uint64_t v) {
+  if (d && (threadIdx.x & 63) == 0) atomicAdd(&d[k], (unsigned long long)v);
+}
+#else
+#define WPROF(...)
+#endif
+
 // ---------------------------------------------------------------------------
 // Steady-state tick (the metric path). A group qualifies when it is STEADY
 // (not frozen, its only leader is its primary, every other replica a
@@ -30,9 +46,48 @@ __device__ __forceinline__ void st(T* base, uint32_t idx, T v) {
 // Cache keeps the per-group words and records that every tick re-reads
 // (measured: C2 at 2^22 groups, lean kernel 87 -> 62 us; C4 list kernel
 // 111 -> 95 us).
+// (A/B builds: RAFTSTEP_RING_STORE=1 write-through sc1, 2 plain)
+#ifndef RAFTSTEP_RING_STORE
+#define RAFTSTEP_RING_STORE 0
+#endif
 template <typename T>
 __device__ __forceinline__ void ring_st(T* base, uint32_t idx, T v) {
+#if RAFTSTEP_RING_STORE == 1
+  __hip_atomic_store(&base[idx], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif RAFTSTEP_RING_STORE == 2
+  base[idx] = v;
+#else
   __builtin_nontemporal_store(v, &base[idx]);
+#endif
+}
+
+// The lean kernel's per-group record and heartbeat stores (A/B builds:
+// RAFTSTEP_REC_STORE=1 non-temporal, 2 write-through sc1; 0 plain).
+#ifndef RAFTSTEP_REC_STORE
+#define RAFTSTEP_REC_STORE 0
+#endif
+__device__ __forceinline__ void rec_st(SsRec* p, const SsRec& v) {
+#if RAFTSTEP_REC_STORE == 1
+  typedef int32_t I4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(I4{v.last, v.term, v.cl, v.cf}, reinterpret_cast<I4*>(p));
+#elif RAFTSTEP_REC_STORE == 2
+  uint64_t* q = reinterpret_cast<uint64_t*>(p);
+  __hip_atomic_store(q, uint64_t(uint32_t(v.last)) | (uint64_t(uint32_t(v.term)) << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, uint64_t(uint32_t(v.cl)) | (uint64_t(uint32_t(v.cf)) << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void hb_st(int32_t* p, int32_t v) {
+#if RAFTSTEP_REC_STORE == 1
+  __builtin_nontemporal_store(v, p);
+#elif RAFTSTEP_REC_STORE == 2
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
 }
 // Ring loads of the list / one-pass kernels: the entries may have been
 // written earlier in the same kernel (a carried group's first step, another
@@ -252,6 +307,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
                                            int32_t* work_tick, uint32_t* work_count, int force_slow, const uint32_t g,
                                            const uint32_t* tab, const Rows& RW, const Words& GW) {
   constexpr bool RAFT = SEM == SEM_RAFT;
+  WPROF(uint64_t wp0 = __builtin_amdgcn_s_memtime(); uint64_t wp1 = wp0, wp2 = wp0, wp3 = wp0;)
   int sv[7] = {0, 0, 0, 0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups, term bumps, votes, won
   bool bail = false;
   const int n = int(T.client_entries());   // entries per leader this tick (wave-uniform)
@@ -1041,6 +1097,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   // entry i+d, read in the same or an earlier pass). Copy and move never
   // meet in one group (a switch needs sr < 0).
   constexpr int CPS = 4;   // entries per lane and pass
+  WPROF(wp1 = __builtin_amdgcn_s_memtime(); uint64_t wg = 0, wo = 0, wsc = 0;)
   int jn = 0, jpre = 0, jtot = 0;   // this lane's job size, exclusive wave prefix, wave total
   if constexpr (RAFT) {
     jn = cp_n > 0 ? cp_n : mv_n;
@@ -1107,6 +1164,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         }
       }
     }
+    WPROF(uint64_t wq0 = __builtin_amdgcn_s_memtime(); if constexpr (RAFT) { int z = 0; for (int k = 0; k < CPS; ++k) z += ct[k]; if (__ballot(z == 0x7FFFFFFF)) wg += 1; } uint64_t wq1 = __builtin_amdgcn_s_memtime(); wg += wq1 - wq0;)
     if (LIST && pass_i == 0 && n && wr != 0) {   // this tick's entries: scattered groups, each lane its own R-contiguous segment
       const uint64_t tb = ring_tile(g, P.KP, R);
       int32_t* const rt = P.log_term + tb;
@@ -1135,6 +1193,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         }
       }
     }
+    WPROF(uint64_t wq2 = __builtin_amdgcn_s_memtime(); wo += wq2 - wq1;)
     if constexpr (RAFT) {
 #pragma unroll
       for (int k = 0; k < CPS; ++k) {
@@ -1144,7 +1203,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         if constexpr (CRC) ring_st(P.log_crc + ctb[k], cdst[k], cc[k]);
       }
     }
+    WPROF(wsc += __builtin_amdgcn_s_memtime() - wq2;)
   }
+  WPROF(wp2 = __builtin_amdgcn_s_memtime();)
   if (!LIST && n) {
     const uint64_t wball = __ballot(wr != 0);
     if (wball) {
@@ -1213,6 +1274,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       }
     }
   }
+#ifndef RAFTSTEP_WAVE_PROF
   if (P.dbg) {   // diagnostics: lanes per class, one atomic per wave and class
     df |= bail ? 2u : 0u;
     df |= (g < P.G) ? 1024u : 0u;
@@ -1225,6 +1287,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[32 + k], (unsigned long long)__popcll(b));
     }
   }
+#endif
   // groups that need the general path go to the sharded worklist: dense
   // launch, block-local prefix over the wave ballots and one atomic on the
   // block's shard; list launch (scattered groups), one atomic per deferred
@@ -1265,6 +1328,11 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       block_stats<4>(v4, idx, stats);
     }
   }
+  WPROF(if (LIST && P.dbg) {
+    wp3 = __builtin_amdgcn_s_memtime();
+    wprof_add(P.dbg, 32, wp1 - wp0); wprof_add(P.dbg, 33, wg); wprof_add(P.dbg, 34, wo); wprof_add(P.dbg, 35, wsc);
+    wprof_add(P.dbg, 36, wp3 - wp2); wprof_add(P.dbg, 37, 1);
+  })
   return stored;
 }
 
@@ -1303,6 +1371,16 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
 // (RowAcc / WordAcc over the __shared__ arrays: ds_ instructions), and
 // writes back the records
 // it may have changed (coalesced) and the per-group words that did change.
+// Active lanes per wave of the list kernel: the listed groups of a tick are
+// few (C4: ~50K of 4M) and the kernel is latency-bound (a chain of dependent
+// loads per group), so spreading them over more waves, each with fewer
+// groups, puts more of those chains in flight at once.
+#ifndef RAFTSTEP_LIST_LANES
+#define RAFTSTEP_LIST_LANES 64
+#endif
+constexpr uint32_t LIST_LANES = RAFTSTEP_LIST_LANES;
+static_assert(LIST_LANES >= 1 && LIST_LANES <= 64, "active lanes per wave");
+
 template <int R, bool CRC, int SEM, int LB>
 __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, unsigned long long* stats,
                                                         uint32_t* work, int32_t* work_tick, uint32_t* work_count,
@@ -1321,14 +1399,18 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
   __shared__ LxRec sglx[LB];
   __shared__ uint8_t sgiso[LB];
   __shared__ uint32_t sdm[LB];   // dirty rows, then dirty 16-B pieces, of each lane's record
+  constexpr uint32_t GPB = uint32_t(LB) / 64u * LIST_LANES;   // groups per block and round
   shard_zero(next_count);
   const uint32_t n = shard_prefix(count, pre);
-  if (blockIdx.x * uint32_t(LB) >= n) return;
+  if (blockIdx.x * GPB >= n) return;
   stage_crc_tab<CRC>(P, tab);
   const uint32_t t = threadIdx.x;
-  for (uint32_t base = blockIdx.x * uint32_t(LB); base < n; base += gridDim.x * uint32_t(LB)) {
-    const uint32_t i = base + t;
-    const uint32_t g = i < n ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
+  const uint32_t lane = t & 63u;
+  WPROF(const uint64_t wk0 = __builtin_amdgcn_s_memtime(); uint64_t wk1 = 0, wk2 = 0, wk3 = 0, wk4 = 0;)
+  for (uint32_t base = blockIdx.x * GPB; base < n; base += gridDim.x * GPB) {
+    WPROF(const uint64_t wi0 = __builtin_amdgcn_s_memtime();)
+    const uint32_t i = base + (t >> 6) * LIST_LANES + lane;
+    const uint32_t g = (lane < LIST_LANES && i < n) ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
     const bool valid = g < P.G;
     sg[t] = g;
     // (each is a separate scattered line per group: only the words most
@@ -1361,6 +1443,7 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       for (uint32_t k = 0; k < RQ; ++k) srec4[t + uint32_t(LB) * k] = v[k];
     }
     __syncthreads();
+    WPROF(const uint64_t wi1 = __builtin_amdgcn_s_memtime(); wk1 += wi1 - wi0;)
     sdm[t] = 0u;
     const RowAcc<R, true> rw{&srec[t * RW], 0u, &sdm[t]};
     const uint32_t gs = valid ? g : 0u;   // (invalid lanes never touch their words)
@@ -1371,11 +1454,13 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     bool wrote = (P.diag & 64u) ? valid
                                 : fast_group<R, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab,
                                                                     rw, gw);
+    WPROF(const uint64_t wi2 = __builtin_amdgcn_s_memtime(); wk2 += wi2 - wi1;)
     if (steps > 1) {   // the following tick too, on the staged state (pipelined tick)
       __threadfence_block();   // this step's ring stores, seen by the next step's gathers
       wrote |= fast_group<R, CRC, SEM, true>(P, T.at_tick(T.tick + 1), nx.stats, nx.work, nx.work_tick,
                                                  nx.work_count, 0, g, tab, rw, gw);
     }
+    WPROF(const uint64_t wi3 = __builtin_amdgcn_s_memtime(); wk3 += wi3 - wi2;)
     {   // dirty rows -> the 16-B pieces of the record they touch
       const uint32_t rows = (valid && wrote) ? sdm[t] : 0u;
       uint32_t pm = 0;
@@ -1407,7 +1492,15 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       if (s1.last != ss0.last || s1.term != ss0.term || s1.cl != ss0.cl || s1.cf != ss0.cf) P.gss[g] = s1;
     }
     __syncthreads();   // the LDS copies and the body's block reductions are reused next round
+    WPROF(wk4 += __builtin_amdgcn_s_memtime() - wi3;)
   }
+  WPROF(if (P.dbg) {
+    const uint64_t tot = __builtin_amdgcn_s_memtime() - wk0;
+    wprof_add(P.dbg, 0, wk1); wprof_add(P.dbg, 1, wk2); wprof_add(P.dbg, 2, wk3); wprof_add(P.dbg, 3, wk4);
+    wprof_add(P.dbg, 4, 1);
+    if ((threadIdx.x & 63) == 0) atomicMax(&P.dbg[5], (unsigned long long)tot);
+    wprof_add(P.dbg, 6 + min(15, 63 - __builtin_clzll(tot | 1ull) - 10), 1);
+  })
 }
 
 // ---------------------------------------------------------------------------
@@ -1628,8 +1721,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
                    : 0u;
       }
       if (take) {
-        if (nl != L || cl2 != s.cl || cf2 != s.cf) P.gss[g] = SsRec{nl, s.term, cl2, cf2};
-        if (hbw) at(P.hb, g) = T.now;                   // timer.Reset(d) of every follower
+        if (nl != L || cl2 != s.cl || cf2 != s.cf) rec_st(&P.gss[g], SsRec{nl, s.term, cl2, cf2});
+        if (hbw) hb_st(&at(P.hb, g), T.now);            // timer.Reset(d) of every follower
         if (RAFT && lxs) P.glx[g] = LxRec{gx.k + n, gx.dl};   // (SXS: unchanged, both logs grow by n)
         if (hwx_clear) at(P.gmeta, g) = uint16_t(meta & ~M_HWX);
         if (sw_d) {   // the new segment starts at this tick's first entry
@@ -1732,7 +1825,11 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       }
     }
   }
+#ifdef RAFTSTEP_WAVE_PROF
+  if (false) {
+#else
   if (P.dbg) {   // diagnostics (same class bits as fast_group): lanes, skipped, taken by the lean pass
+#endif
     df |= (g < P.G) ? 1024u : 0u;
     df |= pass ? 1u << 23 : 0u;
     if (!take) df &= ~0x6780000u;   // the class bits 19-22, 25, 26 count taken ticks only
@@ -1967,8 +2064,9 @@ static void launch_list_t(const DevPlanes& P, const Trace& T, unsigned long long
   // blocks of four waves, a resident grid striding over the list (one-wave
   // blocks measured the same list kernel time on C4 and a 15% slower lean
   // kernel beside it, round 2)
+  constexpr uint64_t GPB = 256 / 64 * LIST_LANES;
   const unsigned blocks =
-      unsigned(std::min<uint64_t>((P.G + 255) / 256, resident_blocks(tick_list_kernel<R, CRC, SEM, 256>, 256)));
+      unsigned(std::min<uint64_t>((P.G + GPB - 1) / GPB, resident_blocks(tick_list_kernel<R, CRC, SEM, 256>, 256)));
   hipExtLaunchKernelGGL(tick_list_kernel<R, CRC, SEM, 256>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats, work,
                         work_tick, work_count, list, count, next_count, steps, nx);
 }

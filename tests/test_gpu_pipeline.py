@@ -3,7 +3,7 @@ overlapped general kernel against the oracle, across the call and window
 shapes where they hand groups from one kernel to another: calls of 1, 2, 7
 and 20 ticks, general-kernel windows of 1, 3 and 8 ticks (window ends inside a
 call, at a call's end, on consecutive ticks), pipeline on and off, in line
-and overlapped general kernel, calls with and without statistics (the
+and overlapped general kernel (overlapping 1, 2 or 3 ticks), calls with and without statistics (the
 stats-less form skips the per-tick records and the list kernel's second-step
 records). Workload: C4's configuration (leader
 isolation, RAFT; elections, first rounds, returns, deferrals) on 2^13 groups
@@ -36,7 +36,10 @@ def _kw(sem):
                                                                ("1", "1", "1", True), ("1", "0", "3", True),
                                                                ("0", "1", "3", True), ("0", "0", "8", True),
                                                                ("1", "1", "8", False), ("1", "1", "3", False),
-                                                               ("0", "1", "3", False)])
+                                                               ("0", "1", "3", False), ("1", "2", "8", True),
+                                                               ("1", "2", "3", True), ("1", "3", "8", True),
+                                                               ("1", "2", "1", True), ("0", "2", "3", True),
+                                                               ("1", "2", "8", False)])
 def test_pipelined_tick_matches_oracle(monkeypatch, sem, pipeline, overlap, slow_every, stats):
     monkeypatch.setenv("RAFTSTEP_PIPELINE", pipeline)
     monkeypatch.setenv("RAFTSTEP_DEBUG_PIPE", "1")
