@@ -229,7 +229,7 @@ class Ctx:
         torch.cuda.synchronize()
 
 
-def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0, cpu=None):
+def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0, cpu=None, list_count=True):
     """One line: `repeats` timed regions of exactly `steps` ticks of workload
     `wl` on this rank's shard (G groups) with `tpl` ticks per launch, then the
     untimed profile passes for the dominant kernel's duration. Returns the
@@ -297,11 +297,12 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
         tick += steps
         list_ms, list_launches = eng.profile_read()
         eng.profile(0)
-        eng.diag_enable(True)   # (separately: the class counters cost time) listed group-steps per launch
-        eng.tick(tick, steps, stats=False)
-        tick += steps
-        list_steps = eng.diag_read()["list_lanes"]
-        eng.diag_enable(False)
+        if list_count:   # (separately: the class counters cost time) listed group-steps per launch
+            eng.diag_enable(True)
+            eng.tick(tick, steps, stats=False)
+            tick += steps
+            list_steps = eng.diag_read()["list_lanes"]
+            eng.diag_enable(False)
     eng.profile(0)
     nranks, _, allreduces = eng.comm_info()
     eng.close()
@@ -432,6 +433,9 @@ def main():
                          "default workload; 'none' to skip)")
     ap.add_argument("--extra-budget", type=float, default=120.0,
                     help="seconds: no further extra workload starts once the run has taken this long")
+    ap.add_argument("--no-list-count", action="store_true",
+                    help="skip the untimed pass that counts the list kernel's group-steps with the class counters "
+                         "(its atomics make that pass slow; profiler runs leave it out)")
     ap.add_argument("--isolate", type=int, default=None,
                     help="diagnostics: override the workload's isolation windows per 65536 epochs (0: none)")
     args = ap.parse_args()
@@ -474,7 +478,7 @@ def main():
     K = args.ring_depth or wl["ring_depth"]
     cpu = None if args.no_cpu_baseline else (args.cpu_groups, args.cpu_ticks)
     head = measure(ctx, wl_key, wl, G, R, E, K, args.steps, args.warmup, args.repeats, tpl=1, leader=args.leader,
-                   cpu=cpu)
+                   cpu=cpu, list_count=not args.no_list_count)
     ok = head["stats_check"]
 
     multi = None
@@ -519,7 +523,8 @@ def main():
         xw = WORKLOADS[name]
         xR, xE, xK = xw.get("replicas", R_DEFAULT), xw["entries"], xw["ring_depth"]
         x = measure(ctx, name, xw, xw["groups"], xR, xE, xK, args.steps, args.warmup, args.repeats, tpl=1,
-                    cpu=None if args.no_cpu_baseline else (args.cpu_groups // 4, args.cpu_ticks // 4))
+                    cpu=None if args.no_cpu_baseline else (args.cpu_groups // 4, args.cpu_ticks // 4),
+                    list_count=not args.no_list_count)
         ok = ok and x["stats_check"]
         x.pop("rccl", None)
         extras[name] = x

@@ -46,48 +46,12 @@ __device__ __forceinline__ void st(T* base, uint32_t idx, T v) {
 // Cache keeps the per-group words and records that every tick re-reads
 // (measured: C2 at 2^22 groups, lean kernel 87 -> 62 us; C4 list kernel
 // 111 -> 95 us).
-// (A/B builds: RAFTSTEP_RING_STORE=1 write-through sc1, 2 plain)
-#ifndef RAFTSTEP_RING_STORE
-#define RAFTSTEP_RING_STORE 0
-#endif
+// (A/B, round 4, C2 one tick per launch: write-through sc1 ring stores 2%
+// slower on C2 and 12% on C4; non-temporal / sc1 record and heartbeat stores
+// 3% / 20% slower than plain ones)
 template <typename T>
 __device__ __forceinline__ void ring_st(T* base, uint32_t idx, T v) {
-#if RAFTSTEP_RING_STORE == 1
-  __hip_atomic_store(&base[idx], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#elif RAFTSTEP_RING_STORE == 2
-  base[idx] = v;
-#else
   __builtin_nontemporal_store(v, &base[idx]);
-#endif
-}
-
-// The lean kernel's per-group record and heartbeat stores (A/B builds:
-// RAFTSTEP_REC_STORE=1 non-temporal, 2 write-through sc1; 0 plain).
-#ifndef RAFTSTEP_REC_STORE
-#define RAFTSTEP_REC_STORE 0
-#endif
-__device__ __forceinline__ void rec_st(SsRec* p, const SsRec& v) {
-#if RAFTSTEP_REC_STORE == 1
-  typedef int32_t I4 __attribute__((ext_vector_type(4)));
-  __builtin_nontemporal_store(I4{v.last, v.term, v.cl, v.cf}, reinterpret_cast<I4*>(p));
-#elif RAFTSTEP_REC_STORE == 2
-  uint64_t* q = reinterpret_cast<uint64_t*>(p);
-  __hip_atomic_store(q, uint64_t(uint32_t(v.last)) | (uint64_t(uint32_t(v.term)) << 32), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(q + 1, uint64_t(uint32_t(v.cl)) | (uint64_t(uint32_t(v.cf)) << 32), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-#else
-  *p = v;
-#endif
-}
-__device__ __forceinline__ void hb_st(int32_t* p, int32_t v) {
-#if RAFTSTEP_REC_STORE == 1
-  __builtin_nontemporal_store(v, p);
-#elif RAFTSTEP_REC_STORE == 2
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-  *p = v;
-#endif
 }
 // Ring loads of the list / one-pass kernels: the entries may have been
 // written earlier in the same kernel (a carried group's first step, another
@@ -1721,8 +1685,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
                    : 0u;
       }
       if (take) {
-        if (nl != L || cl2 != s.cl || cf2 != s.cf) rec_st(&P.gss[g], SsRec{nl, s.term, cl2, cf2});
-        if (hbw) hb_st(&at(P.hb, g), T.now);            // timer.Reset(d) of every follower
+        if (nl != L || cl2 != s.cl || cf2 != s.cf) P.gss[g] = SsRec{nl, s.term, cl2, cf2};
+        if (hbw) at(P.hb, g) = T.now;                   // timer.Reset(d) of every follower
         if (RAFT && lxs) P.glx[g] = LxRec{gx.k + n, gx.dl};   // (SXS: unchanged, both logs grow by n)
         if (hwx_clear) at(P.gmeta, g) = uint16_t(meta & ~M_HWX);
         if (sw_d) {   // the new segment starts at this tick's first entry

@@ -19,7 +19,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${OUTDIR:-r4}
 mkdir -p "$OUT"
 B="python3 -u bench.py --steps 20 --warmup 5"
-Q="--steps 20 --warmup 5 --repeats 1 --no-cpu-baseline --no-fused --extra none"
+Q="--steps 20 --warmup 5 --repeats 1 --no-cpu-baseline --no-fused --extra none --no-list-count"
 P="timeout -s KILL 120 rocprofv3"
 log() { echo "== $(date +%T) $*" >> "$OUT/progress.log"; }
 n=0
@@ -40,6 +40,10 @@ for s in "$@"; do
          && $P --pmc WRITE_SIZE -d "$OUT/pmc_calib_write" -o p --output-format csv -- ./tools/pmc_calib > "$OUT/pmc2.log" 2>&1 \
          && $P --pmc FETCH_SIZE -d "$OUT/pmc_c2_fetch" -o p --output-format csv -- python3 -u bench.py $Q > "$OUT/pmc3.log" 2>&1 \
          && $P --pmc WRITE_SIZE -d "$OUT/pmc_c2_write" -o p --output-format csv -- python3 -u bench.py $Q > "$OUT/pmc4.log" 2>&1 ;;
+    profc5) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv \
+              -- python3 -u bench.py --workload C5 $Q > "$OUT/prof_c5.log" 2>&1 ;;
+    pmcc5) $P --pmc FETCH_SIZE -d "$OUT/pmc_c5_fetch" -o p --output-format csv -- python3 -u bench.py --workload C5 $Q > "$OUT/pmc7.log" 2>&1 \
+           && $P --pmc WRITE_SIZE -d "$OUT/pmc_c5_write" -o p --output-format csv -- python3 -u bench.py --workload C5 $Q > "$OUT/pmc8.log" 2>&1 ;;
     pmcc4) $P --pmc FETCH_SIZE -d "$OUT/pmc_c4_fetch" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc5.log" 2>&1 \
            && $P --pmc WRITE_SIZE -d "$OUT/pmc_c4_write" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc6.log" 2>&1 ;;
     *) echo "unknown step $s" >&2; exit 2 ;;

@@ -30,13 +30,17 @@ def load(dirpath, counter):
             if row.get("Counter_Name") != counter:
                 continue
             name = row.get("Kernel_Name", "")
-            disp = row.get("Dispatch_Id") or row.get("Correlation_Id")
+            disp = int(row.get("Dispatch_Id") or row.get("Correlation_Id"))
             per[name][disp] += float(row["Counter_Value"])
-    return {k: list(v.values()) for k, v in per.items()}
+    return {k: [v[i] for i in sorted(v)] for k, v in per.items()}
 
 
-def mean_for(d, key):
+def mean_for(d, key, skip=0, take=None):
+    """Mean over the dispatches of the kernels whose name contains `key`, in
+    dispatch order, after the first `skip` (e.g. settle and warm-up ticks),
+    at most `take` of them."""
     vals = [v for k, vs in d.items() if key in k for v in vs]
+    vals = vals[skip:skip + take] if take else vals[skip:]
     if not vals:
         raise SystemExit(f"kernel {key!r} not found in {list(d)}")
     return sum(vals) / len(vals), len(vals)
@@ -54,6 +58,8 @@ def main():
     ap.add_argument("--commit", default=None, help="git commit of the build the passes ran on")
     ap.add_argument("--ticks-per-launch", type=float, default=1,
                     help="ticks one launch of the kernel ran (tick_fused_kernel); bench.py matches on it")
+    ap.add_argument("--skip", type=int, default=0, help="leave out the kernel's first SKIP dispatches (settle, warm-up)")
+    ap.add_argument("--take", type=int, default=None, help="then average at most TAKE dispatches (the timed call)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -65,8 +71,8 @@ def main():
         calib[k] = mean_for(cw, k)[0] * 1024 / CALIB_BYTES
     read_corr = calib["read_u32"]
     write_corr = (calib["write_u32"] + calib["write_u64"]) / 2
-    f_kb, nf = mean_for(load(a.fetch, "FETCH_SIZE"), a.kernel)
-    w_kb, nw = mean_for(load(a.write, "WRITE_SIZE"), a.kernel)
+    f_kb, nf = mean_for(load(a.fetch, "FETCH_SIZE"), a.kernel, a.skip, a.take)
+    w_kb, nw = mean_for(load(a.write, "WRITE_SIZE"), a.kernel, a.skip, a.take)
     rd = f_kb * 1024 / read_corr
     wr = w_kb * 1024 / write_corr
     out = {
@@ -78,6 +84,7 @@ def main():
     if a.algorithmic_bytes:
         out["traffic_over_algorithmic"] = (rd + wr) / a.algorithmic_bytes
     out["ticks_per_launch"] = a.ticks_per_launch
+    out["dispatch_window"] = {"skip": a.skip, "take": a.take}
     if a.commit:
         out["commit"] = a.commit
     json.dump(out, open(a.out, "w"), indent=1)
