@@ -1362,6 +1362,8 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
   __shared__ uint16_t smeta[LB], sgrot[LB];
   __shared__ LxRec sglx[LB];
   __shared__ uint8_t sgiso[LB];
+  __shared__ uint16_t sgrota[LB], sgrotb[LB];
+  __shared__ int32_t sgsb[LB], sgsb2[LB];
   __shared__ uint32_t sdm[LB];   // dirty rows, then dirty 16-B pieces, of each lane's record
   constexpr uint32_t GPB = uint32_t(LB) / 64u * LIST_LANES;   // groups per block and round
   shard_zero(next_count);
@@ -1377,10 +1379,12 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     const uint32_t g = (lane < LIST_LANES && i < n) ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
     const bool valid = g < P.G;
     sg[t] = g;
-    // (each is a separate scattered line per group: only the words most
-    // ticks use are staged; the ring segment words, needed on rare paths —
-    // ring reads, segment switches — stay in HBM, read and written there)
-    uint16_t m0 = 0, r0 = 0;
+    // (each is a separate scattered line per group, all loaded in the same
+    // round trip; the ring segment words too: a return or a segment switch
+    // is in most waves of a churn tick, and reading them from HBM there put
+    // one more dependent round trip on every such wave's critical path)
+    uint16_t m0 = 0, r0 = 0, ra0 = 0, rb0 = 0;
+    int32_t sb0 = 0, sc0 = 0;
     uint8_t gi0 = 0;
     int32_t hb0 = 0;
     SsRec ss0{0, 0, 0, 0};
@@ -1390,10 +1394,12 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     LxRec lx0{-2147483647 - 1, -2147483647 - 1};
     if (valid) {
       m0 = at(P.gmeta, g); r0 = at(P.grot, g); hb0 = at(P.hb, g); ss0 = P.gss[g];
+      ra0 = at(P.grota, g); rb0 = at(P.grotb, g); sb0 = at(P.gsb, g); sc0 = at(P.gsb2, g);
       if (T.iso_p) gi0 = at(P.giso, g);
       if (uses_glx(m0)) lx0 = P.glx[g];
     }
     smeta[t] = m0; sgrot[t] = r0; sgiso[t] = gi0; shb[t] = hb0; sgss[t] = ss0; sglx[t] = lx0;
+    sgrota[t] = ra0; sgrotb[t] = rb0; sgsb[t] = sb0; sgsb2[t] = sc0;
     __syncthreads();
     {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
       const int4* grec = reinterpret_cast<const int4*>(P.rec);
@@ -1410,9 +1416,8 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     WPROF(const uint64_t wi1 = __builtin_amdgcn_s_memtime(); wk1 += wi1 - wi0;)
     sdm[t] = 0u;
     const RowAcc<R, true> rw{&srec[t * RW], 0u, &sdm[t]};
-    const uint32_t gs = valid ? g : 0u;   // (invalid lanes never touch their words)
-    const WordAcc<true> gw{&smeta[t], &sgrot[t], &P.grota[gs], &sgiso[t], &shb[t], &P.gsb[gs], &sgss[t], &P.grotb[gs],
-                           &P.gsb2[gs], &sglx[t], g};
+    const WordAcc<true> gw{&smeta[t], &sgrot[t], &sgrota[t], &sgiso[t], &shb[t], &sgsb[t], &sgss[t], &sgrotb[t],
+                           &sgsb2[t], &sglx[t], g};
     // (P.diag, timing only, results wrong: 32 = staging alone, 64 = staging and write-back, no tick)
     if (P.diag & 32u) { __syncthreads(); continue; }
     bool wrote = (P.diag & 64u) ? valid
@@ -1448,6 +1453,10 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     if (valid) {   // per-group words that changed
       if (smeta[t] != m0) at(P.gmeta, g) = smeta[t];
       if (sgrot[t] != r0) at(P.grot, g) = sgrot[t];
+      if (sgrota[t] != ra0) at(P.grota, g) = sgrota[t];
+      if (sgrotb[t] != rb0) at(P.grotb, g) = sgrotb[t];
+      if (sgsb[t] != sb0) at(P.gsb, g) = sgsb[t];
+      if (sgsb2[t] != sc0) at(P.gsb2, g) = sgsb2[t];
       if (sgiso[t] != gi0) at(P.giso, g) = sgiso[t];
       if (shb[t] != hb0) at(P.hb, g) = shb[t];
       const LxRec x1 = sglx[t];
@@ -1513,12 +1522,14 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   const uint64_t key = group_key(T.seed, P.gbase + g);
   uint32_t act = 0, starting = 0, im = 0;
   if (T.iso_p) im = iso_windows<R>(key, T, &act, &starting);
+  bool held = false;
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
     // pipelined tick: a group the last list kernel carries through this tick
-    // too is left alone (its state is being written beside this kernel)
-    const bool held = (lflags & 1) && at(P.glst, g) != 0;
-    if (held) at(P.glst, g) = uint8_t(0);
+    // too is left alone (its state is being written beside this kernel); the
+    // mark is cleared with the kernel's other stores at the end (a store here
+    // made every later load of the lane wait for it: vmcnt counts stores)
+    held = (lflags & 1) && at(P.glst, g) != 0;
     const int c = meta & 0xF;
     const bool skip = held || (meta & M_DEFER) || ((meta >> 4) & 0xF);   // carried / pending catch-up / frozen group
     take = !skip && (meta & M_SSYNC) && c < R && g != P.dbg_pass;   // (test knob: pass one group on)
@@ -1803,6 +1814,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
     }
   }
+  if (held) at(P.glst, g) = uint8_t(0);   // (the mark read above)
   // the rest go to the list kernel: block-local prefix, one atomic per block
   // on the block's shard of the list
   __shared__ uint32_t wn[4], wbase;

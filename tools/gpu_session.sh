@@ -44,6 +44,8 @@ for s in "$@"; do
               -- python3 -u bench.py --workload C5 $Q > "$OUT/prof_c5.log" 2>&1 ;;
     pmcc5) $P --pmc FETCH_SIZE -d "$OUT/pmc_c5_fetch" -o p --output-format csv -- python3 -u bench.py --workload C5 $Q > "$OUT/pmc7.log" 2>&1 \
            && $P --pmc WRITE_SIZE -d "$OUT/pmc_c5_write" -o p --output-format csv -- python3 -u bench.py --workload C5 $Q > "$OUT/pmc8.log" 2>&1 ;;
+    sqc4) $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_IFETCH SQ_INSTS_SMEM \
+            -d "$OUT/sq_c4" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/sq1.log" 2>&1 ;;
     pmcc4) $P --pmc FETCH_SIZE -d "$OUT/pmc_c4_fetch" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc5.log" 2>&1 \
            && $P --pmc WRITE_SIZE -d "$OUT/pmc_c4_write" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc6.log" 2>&1 ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
