@@ -86,6 +86,35 @@ __device__ __forceinline__ void fill_seg(T* p, T v) {
   }
 }
 
+// The list kernel's ring stores (scattered groups: each lane writes its own
+// R-contiguous segment, i.e. partial lines). Its own-segment writes are plain
+// (write-back) stores, so that the partial lines merge in L2 before they go
+// to HBM; its entry copies stay non-temporal. Measured (round 4, interleaved
+// A/B, profiles/r04/README.md): C4R 0.98e10 -> 1.07-1.08e10 (the lean kernel
+// beside it 275-283 -> 236 us), C4 1.82 -> 1.85e10; every list-kernel ring
+// store plain: the same on C4R, C4 within noise; copies alone plain: C4R
+// 1.01-1.06e10. (A/B builds: RAFTSTEP_LIST_PLAIN 0 = all non-temporal, 1 =
+// all plain, 3 = copies plain.)
+#ifndef RAFTSTEP_LIST_PLAIN
+#define RAFTSTEP_LIST_PLAIN 2
+#endif
+// (1: every list-kernel ring store; 2: its own-segment writes only; 3: its
+// entry copies only)
+template <bool LIST, typename T, int KIND = 2>
+__device__ __forceinline__ void ring_stx(T* base, uint32_t idx, T v) {
+  if constexpr (LIST && (RAFTSTEP_LIST_PLAIN == 1 || RAFTSTEP_LIST_PLAIN == KIND)) base[idx] = v;
+  else ring_st(base, idx, v);
+}
+template <bool LIST, int N, typename T>
+__device__ __forceinline__ void fill_segx(T* p, T v) {
+  if constexpr (LIST && (RAFTSTEP_LIST_PLAIN == 1 || RAFTSTEP_LIST_PLAIN == 2)) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = v;
+  } else {
+    fill_seg<N>(p, v);
+  }
+}
+
 // A group's R values of one per-replica plane are contiguous ([Gp][R], rix):
 // a lane moves them with R/4 dwordx4 accesses plus one for the remainder
 // (4-B aligned wide accesses are legal on gfx950) instead of R dword ones,
@@ -888,9 +917,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             for (int e = 0; e < n; ++e) {
               const int64_t v = int64_t(sm64(xvb ^ uint64_t(uint32_t(e))) >> 1);
               const uint32_t o = ring_in_tile(g, R, ring_slot(xl + 1 + e, xrot, xrota, xrotb, xsb, xsb2, P.kmask), uint32_t(xi));
-              ring_st(P.log_term + tb, o, x_term);
-              ring_st(P.log_value + tb, o, v);
-              if constexpr (CRC) ring_st(P.log_crc + tb, o, crc_value_final(tab, cs, v));
+              ring_stx<LIST>(P.log_term + tb, o, x_term);
+              ring_stx<LIST>(P.log_value + tb, o, v);
+              if constexpr (CRC) ring_stx<LIST>(P.log_crc + tb, o, crc_value_final(tab, cs, v));
             }
             RW.st(PL_LAST, xi, xl + n);
             if (sel(lt, xi) != x_term) RW.st(PL_LTERM, xi, x_term);
@@ -1021,9 +1050,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
               if (p != c && !((okm >> p) & 1u)) continue;
               const int i0 = p == c ? Ll : last[p] - n;
               const uint32_t o = ring_in_tile(g, R, ring_slot(i0 + e + 1, uint32_t(rot), rota, rotb, sb, sb2, P.kmask), uint32_t(p));
-              ring_st(P.log_term + tb, o, Lt);
-              ring_st(P.log_value + tb, o, v);
-              if constexpr (CRC) ring_st(P.log_crc + tb, o, stamp);
+              ring_stx<LIST>(P.log_term + tb, o, Lt);
+              ring_stx<LIST>(P.log_value + tb, o, v);
+              if constexpr (CRC) ring_stx<LIST>(P.log_crc + tb, o, stamp);
             }
           }
         }
@@ -1143,16 +1172,16 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
         const uint32_t o = ring_in_tile(g, R, uint32_t((w_ph + e) & int(P.kmask)), 0u);
         if (wr == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
-          fill_seg<R>(rt + o, w_term);
-          fill_seg<R>(rv + o, v);
-          if constexpr (CRC) fill_seg<R>(rc + o, stamp);
+          fill_segx<LIST, R>(rt + o, w_term);
+          fill_segx<LIST, R>(rv + o, v);
+          if constexpr (CRC) fill_segx<LIST, R>(rc + o, stamp);
         } else {
 #pragma unroll
           for (int p = 0; p < R; ++p) {
             if (!((wr >> p) & 1u)) continue;
-            ring_st(rt, o + p, w_term);
-            ring_st(rv, o + p, v);
-            if constexpr (CRC) ring_st(rc, o + p, stamp);
+            ring_stx<LIST>(rt, o + p, w_term);
+            ring_stx<LIST>(rv, o + p, v);
+            if constexpr (CRC) ring_stx<LIST>(rc, o + p, stamp);
           }
         }
       }
@@ -1162,9 +1191,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
 #pragma unroll
       for (int k = 0; k < CPS; ++k) {
         if (!con[k]) continue;
-        ring_st(P.log_term + ctb[k], cdst[k], ct[k]);
-        ring_st(P.log_value + ctb[k], cdst[k], cv[k]);
-        if constexpr (CRC) ring_st(P.log_crc + ctb[k], cdst[k], cc[k]);
+        ring_stx<LIST, int32_t, 3>(P.log_term + ctb[k], cdst[k], ct[k]);
+        ring_stx<LIST, int64_t, 3>(P.log_value + ctb[k], cdst[k], cv[k]);
+        if constexpr (CRC) ring_stx<LIST, uint32_t, 3>(P.log_crc + ctb[k], cdst[k], cc[k]);
       }
     }
     WPROF(wsc += __builtin_amdgcn_s_memtime() - wq2;)
@@ -1213,24 +1242,24 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             if constexpr (CRC) sk = uint32_t(__shfl(int(stamp), k_src[k]));
             if (k_on[k]) {
               const uint32_t o = row + uint32_t(k * 64 + lane);
-              ring_st(rt, o, k_term[k]);
-              ring_st(rv, o, int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo)));
-              if constexpr (CRC) ring_st(rc, o, sk);
+              ring_stx<LIST>(rt, o, k_term[k]);
+              ring_stx<LIST>(rv, o, int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo)));
+              if constexpr (CRC) ring_stx<LIST>(rc, o, sk);
             }
           }
           if (wr != 0 && !coop) {   // drifted lane: its own segment
             const uint32_t o = ring_in_tile(g, R, uint32_t((w_ph + e) & int(P.kmask)), 0u);
             if (wr == (1u << R) - 1u) {   // every replica appends: R-wide vector stores
-              fill_seg<R>(rt + o, w_term);
-              fill_seg<R>(rv + o, v);
-              if constexpr (CRC) fill_seg<R>(rc + o, stamp);
+              fill_segx<LIST, R>(rt + o, w_term);
+              fill_segx<LIST, R>(rv + o, v);
+              if constexpr (CRC) fill_segx<LIST, R>(rc + o, stamp);
             } else {
 #pragma unroll
               for (int p = 0; p < R; ++p) {
                 if (!((wr >> p) & 1u)) continue;
-                ring_st(rt, o + p, w_term);
-                ring_st(rv, o + p, v);
-                if constexpr (CRC) ring_st(rc, o + p, stamp);
+                ring_stx<LIST>(rt, o + p, w_term);
+                ring_stx<LIST>(rv, o + p, v);
+                if constexpr (CRC) ring_stx<LIST>(rc, o + p, stamp);
               }
             }
           }

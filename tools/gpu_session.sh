@@ -46,6 +46,11 @@ for s in "$@"; do
            && $P --pmc WRITE_SIZE -d "$OUT/pmc_c5_write" -o p --output-format csv -- python3 -u bench.py --workload C5 $Q > "$OUT/pmc8.log" 2>&1 ;;
     sqc4) $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_IFETCH SQ_INSTS_SMEM \
             -d "$OUT/sq_c4" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/sq1.log" 2>&1 ;;
+    sqc4r) $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_IFETCH SQ_INSTS_SMEM \
+             -d "$OUT/sq_c4r" -o p --output-format csv -- python3 -u bench.py --workload C4R $Q > "$OUT/sq2.log" 2>&1 ;;
+    sqr2) (cd ablib/r2tree && $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_IFETCH SQ_INSTS_SMEM \
+             -d "../../$OUT/sq_r2_c4r" -o p --output-format csv -- python3 -u bench.py --workload C4R --steps 20 --warmup 5 \
+             --repeats 1 --no-cpu-baseline) > "$OUT/sq3.log" 2>&1 ;;
     pmcc4) $P --pmc FETCH_SIZE -d "$OUT/pmc_c4_fetch" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc5.log" 2>&1 \
            && $P --pmc WRITE_SIZE -d "$OUT/pmc_c4_write" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc6.log" 2>&1 ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
