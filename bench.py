@@ -28,8 +28,11 @@ Protocol: W untimed warm-up ticks, then the timed region of
 exactly K ticks (barrier + synchronize on both sides, max over ranks) is
 repeated --repeats times (default 5) and the median is reported. The
 roofline's `achieved` uses the dominant kernel's own average duration,
-measured by HIP events attached to each of its dispatches on the engine
-stream (profile mode 1) in a separate, untimed pass of K ticks.
+measured by HIP events attached to its dispatches on the engine stream
+(profile mode 1) in a separate, untimed pass of K ticks: for the steady
+lines one pair spanning the call's back-to-back launches (so it matches a
+rocprofv3 kernel trace of the timed call), for the churn lines a pair on
+every dispatch of the lean kernel.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2|C3|C4|C4R|C4REF|C5]
 """

@@ -301,9 +301,12 @@ int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats);
 int raft_comm_info(raft_engine* e, int32_t* nranks, int32_t* rank, uint64_t* allreduces);
 
 /* ---- instrumentation -----------------------------------------------------
- * mode 1: every steady-state tick kernel is timed by events attached to its
- *         own dispatch (hipExtLaunchKernel) — kernel-exact, but the events
- *         cost ~5 us per launch of wall time;
+ * mode 1: the steady-state tick kernel is timed by events attached to its
+ *         dispatches (hipExtLaunchKernel): in a call that runs the lean (or
+ *         fused) kernel alone, one pair spanning the call's back-to-back
+ *         launches (start on the first, stop on the last: the kernels run as
+ *         in an unprofiled call); otherwise a pair on every dispatch
+ *         (kernel-exact, ~5-9 us of wall time between launches);
  * mode 2: one event pair on the engine stream around all launches of each
  *         raft_tick call (no per-launch cost; includes the general kernel and
  *         launch gaps, so it upper-bounds the tick kernel's duration);

@@ -1029,6 +1029,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     if (!ra || !rb) return fail(RAFT_EHIP, "hipEventCreate failed");
     HIPCHK(hipEventRecord(ra, e->stream));
   }
+  hipEvent_t prof_a = nullptr, prof_b = nullptr;   // profile mode 1, steady calls: the span of the call's launches
   for (uint32_t i = 0; i < nticks; ++i) {
     const int64_t t = first_tick + int64_t(i);
     const Trace T = make_trace(e, t);
@@ -1038,7 +1039,23 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     uint32_t* cnt = e->wcount + (e->wpar % NWORK) * SHARD_WORDS;
     hipEvent_t a = nullptr, b = nullptr;
     const bool fused = fuse > 1;
-    if (e->prof == 1 && (!fused || i % fuse == 0)) {
+    if (e->prof == 1 && skip_list) {
+      // steady calls (the lean or fused kernel alone, back to back): one
+      // event pair spanning the call's launches — the start event on the
+      // first dispatch, the stop event on the last — so that the kernels
+      // run exactly as in the timed region (an event pair on every dispatch
+      // puts ~9 us between them, and a kernel that starts on a drained
+      // device runs ~1 us shorter than back to back)
+      const uint32_t last_launch = fused ? (nticks - 1) / fuse * fuse : nticks - 1;
+      if (i == 0) {
+        prof_a = next_event(e);
+        prof_b = next_event(e);
+        if (!prof_a || !prof_b) return fail(RAFT_EHIP, "hipEventCreate failed");
+        e->ev_ticks.push_back(nticks);
+        a = prof_a;
+      }
+      if (i == last_launch) b = prof_b;
+    } else if (e->prof == 1 && (!fused || i % fuse == 0)) {
       a = next_event(e);
       b = next_event(e);
       if (!a || !b) return fail(RAFT_EHIP, "hipEventCreate failed");
