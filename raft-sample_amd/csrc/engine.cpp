@@ -153,6 +153,16 @@ struct raft_engine {
   // many ticks run in one launch of tick_fused_kernel (k_fast.hip)
   uint32_t fuse = 1;
   hipStream_t list_stream = nullptr;
+  // Split steady tick: with the list skipped (lean kernel alone, one tick per
+  // launch), each tick is two launches over the two halves of the groups on
+  // two streams, so that one half's kernel boundary (drain, launch, the
+  // previous kernel's tail) overlaps the other half's streaming. Groups never
+  // address each other, so the halves are independent; they join before every
+  // statistics reduce and at the end of the call. RAFTSTEP_SPLIT_STEADY=0:
+  // one launch per tick (exact either way: tests/test_gpu_engine_checks.py).
+  int split_steady = 1;
+  hipStream_t half_stream = nullptr;
+  hipEvent_t ev_half[2] = {nullptr, nullptr};   // engine -> half stream, half stream -> engine
   hipEvent_t ev_lean[2] = {nullptr, nullptr};   // engine stream -> list_stream (list(t) after lean(t))
   hipEvent_t ev_list[4] = {nullptr, nullptr, nullptr, nullptr};   // list_stream -> engine stream (list(t) done)
   // Steady-state list skip. After init_steady (every log empty, entries
@@ -530,6 +540,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
     hipError_t h = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (h == hipSuccess) h = hipStreamCreateWithFlags(&e->gen_stream, hipStreamNonBlocking);
     if (h == hipSuccess) h = hipStreamCreateWithFlags(&e->list_stream, hipStreamNonBlocking);
+    if (h == hipSuccess) h = hipStreamCreateWithFlags(&e->half_stream, hipStreamNonBlocking);
+    for (int q = 0; q < 2 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->ev_half[q], hipEventDisableTiming);
     for (int q = 0; q < 2 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->gen_ev[q], hipEventDisableTiming);
     for (int q = 0; q < 2 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->ev_lean[q], hipEventDisableTiming);
     for (int q = 0; q < 4 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->ev_list[q], hipEventDisableTiming);
@@ -557,6 +569,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* dp = getenv("RAFTSTEP_DEBUG_PIPE")) e->debug_pipe = atoi(dp) != 0;
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
   e->P.diag = diag_lean;
+  if (const char* sp = getenv("RAFTSTEP_SPLIT_STEADY")) e->split_steady = atoi(sp) != 0;
   if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = std::min(4, std::max(0, atoi(og)));
   if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = atoi(pp) != 0;
   e->fuse = std::max<uint32_t>(1u, c.ticks_per_launch);
@@ -616,6 +629,9 @@ int raft_engine_destroy(raft_engine* e) {
   if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
   if (e->gen_stream) (void)hipStreamSynchronize(e->gen_stream);
   if (e->list_stream) (void)hipStreamSynchronize(e->list_stream);
+  if (e->half_stream) (void)hipStreamSynchronize(e->half_stream);
+  for (hipEvent_t x : e->ev_half)
+    if (x) (void)hipEventDestroy(x);
   for (hipEvent_t x : e->gen_ev)
     if (x) (void)hipEventDestroy(x);
   for (hipEvent_t x : e->ev_lean)
@@ -624,6 +640,7 @@ int raft_engine_destroy(raft_engine* e) {
     if (x) (void)hipEventDestroy(x);
   if (e->gen_stream) (void)hipStreamDestroy(e->gen_stream);
   if (e->list_stream) (void)hipStreamDestroy(e->list_stream);
+  if (e->half_stream) (void)hipStreamDestroy(e->half_stream);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->hist) (void)hipFree(e->hist);
   if (e->tstat) (void)hipFree(e->tstat);
@@ -1018,6 +1035,22 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     fprintf(stderr, "raftstep: ticks %lld..%lld pipeline %d\n", (long long)first_tick,
             (long long)(first_tick + nticks - 1), int(pipe));
   const uint32_t fuse = (two && skip_list && !e->cfg.payload_crc && e->prof != 3) ? e->fuse : 1u;
+  // split steady tick (see raft_engine::split_steady): halves of whole 256-group blocks
+  const uint64_t Gs = e->cfg.groups;
+  const uint64_t half = (Gs / 2) & ~uint64_t(255);
+  const bool split = two && skip_list && fuse == 1 && e->split_steady && half >= 65536;
+  bool half_busy = false;   // the half stream has work the engine stream has not joined
+  auto join_half = [&]() -> int {
+    if (!half_busy) return RAFT_OK;
+    HIPCHK(hipEventRecord(e->ev_half[1], e->half_stream));
+    HIPCHK(hipStreamWaitEvent(e->stream, e->ev_half[1], 0));
+    half_busy = false;
+    return RAFT_OK;
+  };
+  if (split) {   // the half stream starts after everything issued before this call
+    HIPCHK(hipEventRecord(e->ev_half[0], e->stream));
+    HIPCHK(hipStreamWaitEvent(e->half_stream, e->ev_half[0], 0));
+  }
   // every call that runs list kernels starts with the lists' counters zeroed
   // (a pipelined call's last list kernel leaves the carried list's count)
   if (two && !skip_list) HIPCHK(hipMemsetAsync(lcount(e, 0), 0, size_t(NLISTS) * SHARD_WORDS * 4, e->stream));
@@ -1054,7 +1087,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         e->ev_ticks.push_back(nticks);
         a = prof_a;
       }
-      if (i == last_launch) b = prof_b;
+      if (i == last_launch && !split) b = prof_b;
     } else if (e->prof == 1 && (!fused || i % fuse == 0)) {
       a = next_event(e);
       b = next_event(e);
@@ -1110,9 +1143,17 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         if (!c || !d) return fail(RAFT_EHIP, "hipEventCreate failed");
       }
       const uint32_t L = e->lpar % 3;
-      HIPCHK(launch_tick_two_pass(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar % NWORK],
-                                  e->work_tick[e->wpar % NWORK], cnt, e->blist[L], lcount(e, L), lcount(e, (L + 2) % 3),
-                                  e->stream, a, b, c, d, skip_list));
+      if (split) {   // the two halves on two streams (the span's stop event is recorded after the join)
+        HIPCHK(launch_tick_lean(e->R, int(e->cfg.semantics), e->P, T, st, e->blist[L], lcount(e, L), 0, e->stream, a,
+                                nullptr, 0, half));
+        HIPCHK(launch_tick_lean(e->R, int(e->cfg.semantics), e->P, T, st, e->blist[L], lcount(e, L), 0, e->half_stream,
+                                nullptr, nullptr, half, Gs - half));
+        half_busy = true;
+      } else {
+        HIPCHK(launch_tick_two_pass(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar % NWORK],
+                                    e->work_tick[e->wpar % NWORK], cnt, e->blist[L], lcount(e, L),
+                                    lcount(e, (L + 2) % 3), e->stream, a, b, c, d, skip_list));
+      }
       ++e->lpar;
     } else {
       HIPCHK(launch_tick_fast(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar % NWORK],
@@ -1180,12 +1221,16 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       // one GPU nothing overlaps them, so one reduce at the end of the call
       // covers every tick. The last one carries the check record.
       const CallCheck chk{e->wcount, par, skip_list ? 1 : 0, e->tstat + size_t(nticks) * NSTAT, int((e->lpar + 2) % 3)};
-      if (stats && !overlap && (!skip_list || e->comm || last))
+      if (stats && !overlap && (!skip_list || e->comm || last)) {
+        if (int rc = join_half()) return rc;
         if (int rc = flush_window_stats(e, stats_first, i, (last && two) ? &chk : nullptr)) return rc;
+      }
       if (!skip_list || e->comm || last) stats_first = i + 1;
       win_first = t + 1;
     }
   }
+  if (int rc = join_half()) return rc;   // (the check record and the readback come after both halves)
+  if (split && prof_b) HIPCHK(hipEventRecord(prof_b, e->stream));   // the span ends with both halves
   if (stats && e->comm) {   // the engine stream (readback, next call) waits for the last all-reduce
     if (e->comm_ev.size() < 2) {
       hipEvent_t x;

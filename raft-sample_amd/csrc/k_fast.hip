@@ -1529,9 +1529,12 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
 // (a drifted group: its own R-contiguous segment, or a ring segment switch).
 template <int R, bool CRC, int SEM>
 __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, unsigned long long* stats, uint32_t* list,
-                                                        uint32_t* count, int lflags) {
+                                                        uint32_t* count, int lflags, uint32_t gofs) {
   constexpr bool RAFT = SEM == SEM_RAFT;
-  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  // (gofs: the first group of this launch, a multiple of 256 — the steady
+  // tick may run as two launches over the two halves of the groups)
+  const uint32_t gblk = (gofs >> 8) + blockIdx.x;   // this block's 256 groups
+  const uint32_t g = gblk * 256u + threadIdx.x;
   __shared__ uint32_t tab[CRC ? 2048 : 1];
   stage_crc_tab<CRC>(P, tab);
   const int n = int(T.client_entries());
@@ -1849,7 +1852,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   __shared__ uint32_t wn[4], wbase;
   const uint64_t bm = __ballot(pass);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t k = blockIdx.x & uint32_t(NSHARD - 1);
+  const uint32_t k = gblk & uint32_t(NSHARD - 1);   // == shard_home(g)
   if (lane == 0) wn[wave] = uint32_t(__popcll(bm));
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -2055,9 +2058,11 @@ hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, 
 
 template <int R, bool CRC, int SEM>
 static void launch_lean_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
-                          uint32_t* count, int lflags, hipStream_t s, hipEvent_t a, hipEvent_t b) {
-  hipExtLaunchKernelGGL(tick_lean_kernel<R, CRC, SEM>, grid_for(P.G), dim3(256), 0, s, a, b, 0, P, T, stats, list,
-                        count, lflags);
+                          uint32_t* count, int lflags, hipStream_t s, hipEvent_t a, hipEvent_t b, uint64_t g0 = 0,
+                          uint64_t ng = ~0ull) {
+  const uint64_t n = std::min<uint64_t>(ng, P.G - g0);
+  hipExtLaunchKernelGGL(tick_lean_kernel<R, CRC, SEM>, grid_for(n), dim3(256), 0, s, a, b, 0, P, T, stats, list,
+                        count, lflags, uint32_t(g0));
 }
 
 template <int R, bool CRC, int SEM>
@@ -2105,13 +2110,16 @@ hipError_t launch_tick_two_pass(int R, int sem, const DevPlanes& P, const Trace&
   return hipGetLastError();
 }
 hipError_t launch_tick_lean(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
-                            uint32_t* count, int lflags, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
+                            uint32_t* count, int lflags, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop,
+                            uint64_t g0, uint64_t ng) {
   const bool crc = P.crc_on != 0;
 #define RAFT_LEAN(CRC_)                                                                                          \
   if (sem == SEM_RAFT) {                                                                                          \
-    RAFT_DISPATCH_R(R, (launch_lean_t<RR, CRC_, SEM_RAFT>(P, T, stats, list, count, lflags, s, ev_start, ev_stop))) \
+    RAFT_DISPATCH_R(R, (launch_lean_t<RR, CRC_, SEM_RAFT>(P, T, stats, list, count, lflags, s, ev_start, ev_stop,   \
+                                                          g0, ng)))                                               \
   } else {                                                                                                        \
-    RAFT_DISPATCH_R(R, (launch_lean_t<RR, CRC_, SEM_REF>(P, T, stats, list, count, lflags, s, ev_start, ev_stop)))  \
+    RAFT_DISPATCH_R(R, (launch_lean_t<RR, CRC_, SEM_REF>(P, T, stats, list, count, lflags, s, ev_start, ev_stop,    \
+                                                         g0, ng)))                                                \
   }
   if (crc) { RAFT_LEAN(true); } else { RAFT_LEAN(false); }
 #undef RAFT_LEAN

@@ -176,3 +176,30 @@ def test_engine_loads_version_1_checkpoints(tmp_path):
     b.load_checkpoint(p)
     H.assert_same_state(b.store_state(), st, "v1 checkpoint")   # (hashed victims: iso_victim is 0 anyway)
     assert list(a.tick(50, 20)) == list(b.tick(50, 20))
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_split_steady_tick_matches_oracle(monkeypatch, split):
+    """The steady tick split over two streams (engine.cpp split_steady: two
+    launches per tick over the two halves of the groups, joined before every
+    statistics reduce) against the oracle: enough groups for the split
+    (>= 2 x 65536), a count that leaves a partial last block, calls with and
+    without statistics, with the list skipped from the second call on."""
+    monkeypatch.setenv("RAFTSTEP_SPLIT_STEADY", split)
+    kw = dict(replicas=5, groups=(1 << 17) + 300, ring_depth=16, client_period=1, seed=0x5EED0002)
+    e, o = Engine(**kw), oracle.Oracle(**kw)
+    e.init_steady(0, 0)
+    o.init_steady(0, 0)
+    e.diag_enable()
+    t = 1
+    for k, st in ((6, True), (20, True), (7, False), (1, True), (13, False), (9, True)):
+        se = e.tick(t, k, stats=st)
+        so = o.tick(t, k, threads=16)
+        if st:
+            assert list(se) == list(so), f"stats of ticks [{t}, {t + k})"
+        t += k
+    e.sync()
+    assert e.state_digest()[1] == o.state_digest()[1]
+    H.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")
+    c = e.diag_read()
+    assert c["ticks_list_skipped"] >= 40, c
