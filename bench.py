@@ -364,11 +364,16 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
                  "(bench.py lean_bytes; NOT SURVEY §8(d)'s one-tick-per-launch form)" % (tpl, mean_tpl))
                 if fused else
                 ("tick_lean_kernel, one tick per launch, compressed steady state (bench.py lean_bytes), every "
-                 "group counted as taken by the lean pass") if two_pass else
+                 "group counted as taken by the lean pass; steady lines: the tick's launches (two halves of the "
+                 "groups on two streams) timed as one span per call") if two_pass else
                 "SURVEY.md §8(d) B(R,E), per-replica SoA"),
             "units_per_launch": units * (mean_tpl if fused else 1),
             "avg_kernel_us": avg_kernel_s * 1e6 * (mean_tpl if fused else 1),
             "avg_kernel_us_per_tick": avg_kernel_s * 1e6,
+            # the same bytes over the timed region's wall clock (host launch
+            # and readback included): a profiler-free lower bound of `achieved`
+            "achieved_wall": B * value / world / 1e9,
+            "frac_wall": B * value / world / 1e9 / HBM_PEAK_GBS,
             "kernel_launches": kernel_ticks if not fused else -(-kernel_ticks // tpl),
             # SURVEY §8(d)'s per-replica SoA figure at the measured tick rate:
             # the bandwidth an uncompressed SoA engine would need for this
