@@ -99,6 +99,14 @@ struct raft_engine {
   unsigned long long* hist = nullptr;
   unsigned long long* tstat = nullptr;   // [hist_cap + 2][NSTAT]: per-tick records, then two check records
   unsigned long long* hrb = nullptr;     // pinned host copy of tstat (one async readback per call)
+  // host mirror of a call's records (CallCheck::hout): a call whose records
+  // are all reduced by its last launch (no communicator) has that launch write
+  // them into hrb as well and publish `seq` in *hdone; raft_tick then spins on
+  // hdone instead of copying the records back and waiting for the stream
+  uint32_t* hdone = nullptr;             // pinned, coherent
+  unsigned int* dctr = nullptr;          // device block counter of the mirror launch
+  uint32_t seq = 0;
+  bool mirror = false;                   // the current call's records go to hrb directly
   uint32_t hist_cap = 0;
   uint32_t last_stats_n = 0;             // nticks of the last raft_tick call with statistics (0: none yet)
   unsigned long long* cstat = nullptr;   // raft_comm_allreduce_stats staging
@@ -280,7 +288,7 @@ int ensure_hist(raft_engine* e, uint32_t n) {
   const size_t tb = size_t(cap + 2) * NSTAT * 8;   // + the two check records (raft_engine::tstat)
   HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->hist), hb));
   HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->tstat), tb));
-  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&e->hrb), tb, hipHostMallocDefault));
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&e->hrb), tb, hipHostMallocCoherent));
   HIPCHK(hipMemsetAsync(e->hist, 0, hb, e->stream));   // once; the reduce kernel re-zeroes what it reads
   HIPCHK(hipMemsetAsync(e->tstat, 0, tb, e->stream));
   e->hist_cap = cap;
@@ -527,6 +535,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
     A(reinterpret_cast<void**>(&e->work_tick[q]), NSHARD * scap * 4);
   }
   A(reinterpret_cast<void**>(&e->wcount), WCOUNT_WORDS * 4);
+  A(reinterpret_cast<void**>(&e->dctr), 64);
   for (int q = 0; q < 3; ++q) A(reinterpret_cast<void**>(&e->blist[q]), NSHARD * scap * 4);
   A(reinterpret_cast<void**>(&e->P.glst), Gp);
   A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
@@ -604,6 +613,9 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetAsync(e->P.grotb, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gsb2, 0, Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, WCOUNT_WORDS * 4, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->dctr, 0, 64, e->stream) : z;
+  z = z == hipSuccess ? hipHostMalloc(reinterpret_cast<void**>(&e->hdone), 64, hipHostMallocCoherent) : z;
+  if (z == hipSuccess) *e->hdone = 0u;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_term, 0, R * K * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.log_value, 0, R * K * Gp * 8, e->stream) : z;
   if (c.payload_crc) z = z == hipSuccess ? hipMemsetAsync(e->P.log_crc, 0, R * K * Gp * 4, e->stream) : z;
@@ -645,6 +657,7 @@ int raft_engine_destroy(raft_engine* e) {
   if (e->hist) (void)hipFree(e->hist);
   if (e->tstat) (void)hipFree(e->tstat);
   if (e->hrb) (void)hipHostFree(e->hrb);
+  if (e->hdone) (void)hipHostFree(e->hdone);
   if (e->chk_ev) (void)hipEventDestroy(e->chk_ev);
   if (e->cstat) (void)hipFree(e->cstat);
   if (e->stage) (void)hipFree(e->stage);
@@ -1220,7 +1233,17 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       // window's once its general kernel has joined; with the list skipped on
       // one GPU nothing overlaps them, so one reduce at the end of the call
       // covers every tick. The last one carries the check record.
-      const CallCheck chk{e->wcount, par, skip_list ? 1 : 0, e->tstat + size_t(nticks) * NSTAT, int((e->lpar + 2) % 3)};
+      CallCheck chk{e->wcount, par, skip_list ? 1 : 0, e->tstat + size_t(nticks) * NSTAT, int((e->lpar + 2) % 3),
+                    nullptr, nullptr, nullptr, 0u};
+      // the call's only reduce (every record in this launch), no communicator:
+      // the records also go straight to the host (CallCheck::hout)
+      e->mirror = stats && last && two && stats_first == 0 && !e->comm;
+      if (e->mirror) {
+        chk.hout = e->hrb;
+        chk.hdone = e->hdone;
+        chk.ctr = e->dctr;
+        chk.seq = ++e->seq;
+      }
       if (stats && !overlap && (!skip_list || e->comm || last)) {
         if (int rc = join_half()) return rc;
         if (int rc = flush_window_stats(e, stats_first, i, (last && two) ? &chk : nullptr)) return rc;
@@ -1244,7 +1267,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     // no readback in this call: the check record goes to tstat[cap + 1] and
     // its pinned copy is verified by the next call (settle_check)
     const CallCheck chk{e->wcount, int((e->wpar + NWORK - 1) % NWORK), 1, e->tstat + size_t(e->hist_cap + 1) * NSTAT,
-                        int((e->lpar + 2) % 3)};
+                        int((e->lpar + 2) % 3), nullptr, nullptr, nullptr, 0u};
     HIPCHK(launch_stats_reduce(nullptr, nullptr, 0, e->stream, &chk));
     const size_t off = size_t(e->hist_cap + 1) * NSTAT;
     HIPCHK(hipMemcpyAsync(e->hrb + off, e->tstat + off, NSTAT * 8, hipMemcpyDeviceToHost, e->stream));
@@ -1281,7 +1304,19 @@ int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_sta
     // and over GPUs) and, behind them, the end-of-call check record
     const bool two = e->two_pass && !e->force_general;
     const size_t words = size_t(nticks + (two ? 1 : 0)) * NSTAT;
-    HIPCHK(hipMemcpyAsync(e->hrb, e->tstat, words * 8, hipMemcpyDeviceToHost, e->stream));
+    if (e->mirror) {
+      // the records are already in hrb: wait for the launch's completion flag
+      // (spinning; the stream is polled too, so a failed launch ends the wait),
+      // then for the stream (its completion signal follows within microseconds)
+      const volatile uint32_t* done = e->hdone;
+      for (uint32_t k = 1; *done != e->seq; ++k) {
+        __builtin_ia32_pause();
+        if ((k & 1023u) == 0 && hipStreamQuery(e->stream) != hipErrorNotReady) break;
+      }
+      e->mirror = false;
+    } else {
+      HIPCHK(hipMemcpyAsync(e->hrb, e->tstat, words * 8, hipMemcpyDeviceToHost, e->stream));
+    }
     HIPCHK(hipStreamSynchronize(e->stream));
     e->last_stats_n = nticks;
     for (size_t i = 0; i < size_t(nticks) * NSTAT; ++i) out->v[i % NSTAT] += int64_t(e->hrb[i]);

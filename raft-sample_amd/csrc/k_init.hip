@@ -181,6 +181,21 @@ __device__ __forceinline__ void call_check_block(const CallCheck& c) {
                                  : threadIdx.x == CHK_LAST_LIST ? last
                                  : threadIdx.x == CHK_MAGIC ? 0x5241465443484Bull : 0ull;
     c.out[threadIdx.x] = v;
+    if (c.hout) c.hout[size_t(blockIdx.x) * NSTAT + threadIdx.x] = v;   // (the check block is the launch's last index)
+  }
+}
+
+// Host mirror completion (CallCheck::hdone): every block's writes are made
+// visible system-wide, then the last block to finish publishes the call's
+// sequence number.
+__device__ __forceinline__ void host_mirror_done(const CallCheck& c) {
+  if (!c.hout) return;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(c.ctr, 1u) == gridDim.x - 1) {
+    *c.ctr = 0u;
+    __threadfence_system();
+    __hip_atomic_store(c.hdone, c.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -225,6 +240,7 @@ __global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hi
   static_assert(STAT_SLOTS == 64, "one lane per slot");
   if (blockIdx.x == nticks) {
     call_check_block(chk);
+    host_mirror_done(chk);
     return;
   }
   unsigned long long* h = hist + size_t(blockIdx.x) * STAT_SLOTS * NSTAT + threadIdx.x * NSTAT;
@@ -243,7 +259,9 @@ __global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hi
 #pragma unroll
     for (int s = 0; s < NSTAT; ++s) x = (int(threadIdx.x) == s) ? v[s] : x;
     out[size_t(blockIdx.x) * NSTAT + threadIdx.x] = x;
+    if (chk.hout) chk.hout[size_t(blockIdx.x) * NSTAT + threadIdx.x] = x;
   }
+  host_mirror_done(chk);
 }
 hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s,
                                const CallCheck* chk) {

@@ -101,6 +101,16 @@ struct CallCheck {
   int zero_lists;
   unsigned long long* out;      // NSTAT words
   int llast;                    // list set of the call's last tick
+  // host mirror (a call whose records are all reduced by this one launch, no
+  // communicator): every block also writes its record to hout (pinned,
+  // coherent host memory, same layout as `out` of the launch), and the last
+  // block to finish stores `seq` to *hdone (system scope), so that the host
+  // reads the call's records without a device-to-host copy and sees the end
+  // of the call without waiting for the stream's completion signal
+  unsigned long long* hout;
+  uint32_t* hdone;
+  unsigned int* ctr;            // device counter of finished blocks (zero between launches)
+  uint32_t seq;
 };
 // Sums the STAT_SLOTS slots of nticks consecutive per-tick records of `hist`
 // into out[nticks][NSTAT] and zeroes those slots; with `chk` also writes the
