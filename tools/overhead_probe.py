@@ -1,0 +1,45 @@
+"""Per-call host overhead of raft_tick on a C2 engine (median wall time of
+single calls): torch.cuda.synchronize, ticks of 1 / 2 / 20 with and without
+statistics, the split steady tick on / off (RAFTSTEP_SPLIT_STEADY)."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "raft-sample_amd")]
+import torch  # noqa: E402
+import bench  # noqa: E402
+from raftstep import Engine  # noqa: E402
+
+
+def tm(f, n=100):
+    f()
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        f()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return round(ts[n // 2] * 1e6, 1)
+
+
+torch.cuda.init()
+torch.cuda.synchronize()
+print("torch.cuda.synchronize us", tm(torch.cuda.synchronize))
+wl = bench.WORKLOADS["C2"]
+for split in ("1", "0"):
+    os.environ["RAFTSTEP_SPLIT_STEADY"] = split
+    e = Engine(**bench.engine_kwargs(wl, 5, 1 << 20, 0, 32, 1, 0))
+    e.init_steady(0, 0)
+    e.tick(1, 6)
+    t = [7]
+
+    def tk(k, st=True):
+        def f():
+            e.tick(t[0], k, stats=st)
+            if not st:
+                e.sync()
+            t[0] += k
+        return f
+    print("split", split, {f"tick{k}{'' if st else '_nostats'}": tm(tk(k, st)) for k in (1, 2, 20) for st in (True, False)})
+    e.close()
