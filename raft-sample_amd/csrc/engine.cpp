@@ -1048,10 +1048,13 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     fprintf(stderr, "raftstep: ticks %lld..%lld pipeline %d\n", (long long)first_tick,
             (long long)(first_tick + nticks - 1), int(pipe));
   const uint32_t fuse = (two && skip_list && !e->cfg.payload_crc && e->prof != 3) ? e->fuse : 1u;
-  // split steady tick (see raft_engine::split_steady): halves of whole 256-group blocks
+  // split steady tick (see raft_engine::split_steady): halves of whole
+  // 256-group blocks (A/B, round 4: giving the half stream 45% or 40% of the
+  // groups, so that it would run ahead and the call-end join find it done,
+  // was 2% / 9% slower than equal halves)
   const uint64_t Gs = e->cfg.groups;
   const uint64_t half = (Gs / 2) & ~uint64_t(255);
-  const bool split = two && skip_list && fuse == 1 && e->split_steady && half >= 65536;
+  const bool split = two && skip_list && fuse == 1 && e->split_steady && half >= 65536 && Gs - half >= 65536;
   bool half_busy = false;   // the half stream has work the engine stream has not joined
   auto join_half = [&]() -> int {
     if (!half_busy) return RAFT_OK;
