@@ -349,7 +349,8 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     achieved = B * units / avg_kernel_s / 1e9
     workload = f"{wl_key}: {G} x {R}-replica groups per GPU, {wl['desc']}, E={E}, K={K}"
     pmc, pmc_src = load_pmc(workload, kname, mean_tpl)
-    traffic = pmc["hbm_bytes_per_launch"] / mean_tpl if pmc else None   # per tick
+    # per tick (a steady tick is two launches over the halves of the groups)
+    traffic = (pmc.get("hbm_bytes_per_tick") or pmc["hbm_bytes_per_launch"]) / mean_tpl if pmc else None
     B_survey = algorithmic_bytes(R, E, crc)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

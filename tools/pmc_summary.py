@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--commit", default=None, help="git commit of the build the passes ran on")
     ap.add_argument("--ticks-per-launch", type=float, default=1,
                     help="ticks one launch of the kernel ran (tick_fused_kernel); bench.py matches on it")
+    ap.add_argument("--launches-per-tick", type=int, default=1,
+                    help="dispatches of the kernel per tick (2: the split steady tick's two halves)")
     ap.add_argument("--skip", type=int, default=0, help="leave out the kernel's first SKIP dispatches (settle, warm-up)")
     ap.add_argument("--take", type=int, default=None, help="then average at most TAKE dispatches (the timed call)")
     ap.add_argument("--out", required=True)
@@ -81,7 +83,9 @@ def main():
         "calibration_counter_over_true": calib, "read_corr": read_corr, "write_corr": write_corr,
         "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
     }
-    if a.algorithmic_bytes:
+    out["launches_per_tick"] = a.launches_per_tick
+    out["hbm_bytes_per_tick"] = (rd + wr) * a.launches_per_tick
+    if a.algorithmic_bytes:   # (per launch)
         out["traffic_over_algorithmic"] = (rd + wr) / a.algorithmic_bytes
     out["ticks_per_launch"] = a.ticks_per_launch
     out["dispatch_window"] = {"skip": a.skip, "take": a.take}
