@@ -61,6 +61,8 @@ ENV_KNOBS = {
     "RAFTSTEP_GENERAL": "exact: lane = one-lane-per-group general kernel (tests/test_gpu_tick_kat.py)",
     "RAFTSTEP_SLOW_EVERY": "exact: general-kernel window (tests/test_gpu_pipeline.py, test_gpu_dist.py)",
     "RAFTSTEP_PIPELINE": "exact: 0 = two passes in line (tests/test_gpu_pipeline.py)",
+    "RAFTSTEP_PINGPONG": "exact: 0 = pipelined tick on a lean and a list stream instead of ping-pong streams "
+                         "(tests/test_gpu_pipeline.py)",
     "RAFTSTEP_OVERLAP_GENERAL": "exact: 0 = general kernel in line, d = overlapping d ticks (tests/test_gpu_pipeline.py)",
     "RAFTSTEP_SPLIT_STEADY": "exact: 0 = one launch per steady tick instead of two halves on two streams "
                              "(tests/test_gpu_engine_checks.py)",

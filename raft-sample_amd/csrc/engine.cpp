@@ -155,6 +155,16 @@ struct raft_engine {
   // RAFTSTEP_PIPELINE=0 runs the two passes in line (exact either way:
   // tests/test_gpu_pipeline.py).
   int pipeline = 1;
+  // Ping-pong streams (pipelined tick, RAFTSTEP_PINGPONG, default on): tick t
+  // runs lean(t) and list(t) back to back on stream t mod 2 (the engine stream
+  // or list_stream); lean(t) waits for lean(t-1) on the other stream, and for
+  // list(t-2) by stream order. The tick's critical chain, list(t-1) ->
+  // lean(t+1) -> list(t+1), then has no cross-queue wake-up in it (~13 us per
+  // such wait, measured: tools/gap_probe.hip), and list(t) no longer waits for
+  // list(t-1) (their groups are disjoint: lean(t) leaves list(t-1)'s alone).
+  // lean(t) zeroes the counter lean(t+1) fills (read by list(t-2), done).
+  int pingpong = 1;
+  hipEvent_t ev_pp = nullptr;   // list_stream -> engine stream at the end of a ping-pong call
   // Fused steady ticks (raft_config.ticks_per_launch, default 1 = off): while
   // the steady-state list skip holds (and without payload CRC, whose
   // per-follower verification the lean kernel does tick by tick), up to that
@@ -554,6 +564,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
     for (int q = 0; q < 2 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->gen_ev[q], hipEventDisableTiming);
     for (int q = 0; q < 2 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->ev_lean[q], hipEventDisableTiming);
     for (int q = 0; q < 4 && h == hipSuccess; ++q) h = hipEventCreateWithFlags(&e->ev_list[q], hipEventDisableTiming);
+    if (h == hipSuccess) h = hipEventCreateWithFlags(&e->ev_pp, hipEventDisableTiming);
     if (h != hipSuccess) rc = fail(RAFT_EHIP, "hipStreamCreate / hipEventCreate: %s", hipGetErrorString(h));
   }
   if (rc != RAFT_OK) {
@@ -581,6 +592,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* sp = getenv("RAFTSTEP_SPLIT_STEADY")) e->split_steady = atoi(sp) != 0;
   if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = std::min(4, std::max(0, atoi(og)));
   if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = atoi(pp) != 0;
+  if (const char* pg = getenv("RAFTSTEP_PINGPONG")) e->pingpong = atoi(pg) != 0;
   e->fuse = std::max<uint32_t>(1u, c.ticks_per_launch);
   e->P.dbg_pass = 0xFFFFFFFFu;
   if (const char* df = getenv("RAFTSTEP_DEBUG_FAST"); df && atoi(df) != 0) {
@@ -650,6 +662,7 @@ int raft_engine_destroy(raft_engine* e) {
     if (x) (void)hipEventDestroy(x);
   for (hipEvent_t x : e->ev_list)
     if (x) (void)hipEventDestroy(x);
+  if (e->ev_pp) (void)hipEventDestroy(e->ev_pp);
   if (e->gen_stream) (void)hipStreamDestroy(e->gen_stream);
   if (e->list_stream) (void)hipStreamDestroy(e->list_stream);
   if (e->half_stream) (void)hipStreamDestroy(e->half_stream);
@@ -984,17 +997,18 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
 // a communicator, sum those across GPUs on the comm stream (ordered by an
 // event, overlapping the following ticks on the engine stream). The call's
 // last flush also writes the end-of-call check record (chk).
-static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1, const CallCheck* chk) {
+static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1, const CallCheck* chk,
+                              hipStream_t s = nullptr) {
+  if (!s) s = e->stream;
   const uint32_t n = w1 - w0 + 1;
-  HIPCHK(launch_stats_reduce(e->hist + size_t(w0) * STAT_SLOTS * NSTAT, e->tstat + size_t(w0) * NSTAT, n, e->stream,
-                             chk));
+  HIPCHK(launch_stats_reduce(e->hist + size_t(w0) * STAT_SLOTS * NSTAT, e->tstat + size_t(w0) * NSTAT, n, s, chk));
   if (!e->comm) return RAFT_OK;
   if (e->comm_ev.empty()) {
     hipEvent_t x;
     HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
     e->comm_ev.push_back(x);
   }
-  HIPCHK(hipEventRecord(e->comm_ev[0], e->stream));
+  HIPCHK(hipEventRecord(e->comm_ev[0], s));
   HIPCHK(hipStreamWaitEvent(e->comm_stream, e->comm_ev[0], 0));
   RCCLCHK(ncclAllReduce(e->tstat + size_t(w0) * NSTAT, e->tstat + size_t(w0) * NSTAT, size_t(n) * NSTAT, ncclUint64,
                         ncclSum, e->comm, e->comm_stream));
@@ -1008,14 +1022,19 @@ static uint32_t* lcount(raft_engine* e, uint32_t q) { return e->wcount + (NWORK 
 // Join of an overlapped general kernel (see raft_engine::overlap_general):
 // the engine stream waits for gen_stream, the window tail clears the
 // window's DEFER flags and zeroes its worklist, its ticks' records are reduced.
-static int join_general(raft_engine* e, bool stats) {
-  HIPCHK(hipStreamWaitEvent(e->stream, e->gen_ev[1], 0));
-  HIPCHK(launch_window_tail(e->P, e->work[e->gen_parity], e->wcount, e->gen_parity, e->stream));
+// (s: the stream of the next tick's lean kernel, the engine stream by default)
+static int join_general(raft_engine* e, bool stats, hipStream_t s = nullptr) {
+  if (!s) s = e->stream;
+  HIPCHK(hipStreamWaitEvent(s, e->gen_ev[1], 0));
+  HIPCHK(launch_window_tail(e->P, e->work[e->gen_parity], e->wcount, e->gen_parity, s));
   e->gen_pending = false;
   if (stats)
-    if (int rc = flush_window_stats(e, e->gen_w0, e->gen_w1, nullptr)) return rc;
+    if (int rc = flush_window_stats(e, e->gen_w0, e->gen_w1, nullptr, s)) return rc;
   return RAFT_OK;
 }
+
+// Stream of tick i of a ping-pong call (raft_engine::pingpong).
+static hipStream_t pp_stream(const raft_engine* e, uint32_t i) { return (i & 1u) ? e->list_stream : e->stream; }
 
 static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool stats) {
   if (int rc = settle_check(e)) return rc;
@@ -1044,6 +1063,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (skip_list) e->n_skip_ticks += nticks;
   const bool two = e->two_pass && !e->force_general;
   const bool pipe = two && !skip_list && !e->debug_work && e->pipeline;
+  const bool pp = pipe && e->pingpong;
   if (e->debug_pipe)
     fprintf(stderr, "raftstep: ticks %lld..%lld pipeline %d\n", (long long)first_tick,
             (long long)(first_tick + nticks - 1), int(pipe));
@@ -1133,11 +1153,18 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         d = next_event(e);
         if (!c || !d) return fail(RAFT_EHIP, "hipEventCreate failed");
       }
-      if (i >= 2) HIPCHK(hipStreamWaitEvent(e->stream, e->ev_list[(i - 2) & 3], 0));   // carried its groups through t-1
-      HIPCHK(launch_tick_lean(e->R, int(e->cfg.semantics), e->P, T, st, e->blist[L], lcount(e, L), lflags, e->stream,
-                              a, b));
-      HIPCHK(hipEventRecord(e->ev_lean[i & 1], e->stream));
-      HIPCHK(hipStreamWaitEvent(e->list_stream, e->ev_lean[i & 1], 0));
+      // (ping-pong: lean(t) after lean(t-1) on the other stream; list(t-2),
+      // which carried its groups through t-1, is before it on its own)
+      hipStream_t cs = pp ? pp_stream(e, i) : e->stream;
+      if (pp) {
+        if (i >= 1) HIPCHK(hipStreamWaitEvent(cs, e->ev_lean[(i - 1) & 1], 0));
+      } else if (i >= 2) {
+        HIPCHK(hipStreamWaitEvent(e->stream, e->ev_list[(i - 2) & 3], 0));   // carried its groups through t-1
+      }
+      HIPCHK(launch_tick_lean(e->R, int(e->cfg.semantics), e->P, T, st, e->blist[L], lcount(e, L), lflags, cs, a, b, 0,
+                              ~0ull, pp ? lcount(e, (L + 1) % 3) : nullptr));
+      HIPCHK(hipEventRecord(e->ev_lean[i & 1], cs));
+      if (!pp) HIPCHK(hipStreamWaitEvent(e->list_stream, e->ev_lean[i & 1], 0));
       ListNext nx{};
       if (carry) {   // tick t+1: its stats record, the worklist of its window
         const int np = int((e->wpar + ((i + 1) % e->slow_every == 0 ? 1u : 0u)) % NWORK);
@@ -1149,9 +1176,9 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       // end-of-call check counts as listed at the last tick; every pipelined
       // call starts with the three lists' counters zeroed)
       HIPCHK(launch_tick_list(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar % NWORK], e->work_tick[e->wpar % NWORK],
-                              cnt, e->blist[L], lcount(e, L), carry ? lcount(e, (L + 2) % 3) : nullptr,
-                              carry ? &nx : nullptr, e->list_stream, c, d));
-      HIPCHK(hipEventRecord(e->ev_list[i & 3], e->list_stream));
+                              cnt, e->blist[L], lcount(e, L), (carry && !pp) ? lcount(e, (L + 2) % 3) : nullptr,
+                              carry ? &nx : nullptr, pp ? cs : e->list_stream, c, d));
+      HIPCHK(hipEventRecord(e->ev_list[i & 3], pp ? cs : e->list_stream));
       ++e->lpar;
     } else if (two) {
       // lean pass appends to list counter lpar, the list pass zeroes the other one
@@ -1182,8 +1209,12 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     // kernels: the engine stream waits for it, then its window tail clears
     // its groups' DEFER (before the next tick's lean kernel) and its ticks'
     // records are final
-    if (e->gen_pending && i >= e->gen_join)
-      if (int rc = join_general(e, stats)) return rc;
+    if (e->gen_pending && i >= e->gen_join) {
+      // (ping-pong: on the stream of lean(t+1), after lean(t))
+      hipStream_t js = pp ? pp_stream(e, i + 1) : e->stream;
+      if (pp) HIPCHK(hipStreamWaitEvent(js, e->ev_lean[i & 1], 0));
+      if (int rc = join_general(e, stats, js)) return rc;
+    }
     // deferred groups catch up every slow_every ticks and at the end of the call
     if ((i + 1) % e->slow_every == 0 || i + 1 == nticks) {
       if (e->debug_work) {   // diagnostics: worklist size of each general-kernel launch (synchronising)
@@ -1212,8 +1243,13 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         // the call and at most one window (the next window's general kernel
         // starts after this one has joined)
         const uint32_t d = std::min<uint32_t>({uint32_t(std::max(e->overlap_general, 1)), e->slow_every, nticks - 1 - i});
-        HIPCHK(hipEventRecord(e->gen_ev[0], after));
-        HIPCHK(hipStreamWaitEvent(e->gen_stream, e->gen_ev[0], 0));
+        if (pp) {   // ping-pong: list(t) and list(t-1) (tick t's deferrals) are on the two streams
+          HIPCHK(hipStreamWaitEvent(e->gen_stream, e->ev_list[i & 3], 0));
+          if (i >= 1) HIPCHK(hipStreamWaitEvent(e->gen_stream, e->ev_list[(i - 1) & 3], 0));
+        } else {
+          HIPCHK(hipEventRecord(e->gen_ev[0], after));
+          HIPCHK(hipStreamWaitEvent(e->gen_stream, e->gen_ev[0], 0));
+        }
         HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t + int64_t(d),
                                 stats ? e->hist : nullptr, e->work[par], e->work_tick[par], cnt, nullptr,
                                 e->lane_general, e->gen_stream));
@@ -1227,7 +1263,12 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         e->gen_stats = stats;
         ++e->n_general;
       } else if (!skip_list) {
-        if (pipe) HIPCHK(hipStreamWaitEvent(e->stream, e->ev_list[i & 3], 0));
+        if (pp) {   // everything on list_stream (list(t) or list(t-1), a window join) before the engine stream
+          HIPCHK(hipEventRecord(e->ev_pp, e->list_stream));
+          HIPCHK(hipStreamWaitEvent(e->stream, e->ev_pp, 0));
+        } else if (pipe) {
+          HIPCHK(hipStreamWaitEvent(e->stream, e->ev_list[i & 3], 0));
+        }
         HIPCHK(launch_tick_slow(e->R, int(e->cfg.semantics), e->P, T0, first_tick, win_first, t,
                                 stats ? e->hist : nullptr, e->work[par], e->work_tick[par], cnt, nullptr,
                                 e->lane_general, e->stream));

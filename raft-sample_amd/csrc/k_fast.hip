@@ -1529,8 +1529,9 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
 // (a drifted group: its own R-contiguous segment, or a ring segment switch).
 template <int R, bool CRC, int SEM>
 __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, unsigned long long* stats, uint32_t* list,
-                                                        uint32_t* count, int lflags, uint32_t gofs) {
+                                                        uint32_t* count, int lflags, uint32_t gofs, uint32_t* zc) {
   constexpr bool RAFT = SEM == SEM_RAFT;
+  shard_zero(zc);   // (ping-pong pipelined tick: the counter of the next tick's list, read by no running kernel)
   // (gofs: the first group of this launch, a multiple of 256 — the steady
   // tick may run as two launches over the two halves of the groups)
   const uint32_t gblk = (gofs >> 8) + blockIdx.x;   // this block's 256 groups
@@ -2059,10 +2060,10 @@ hipError_t launch_tick_fast(int R, int sem, const DevPlanes& P, const Trace& T, 
 template <int R, bool CRC, int SEM>
 static void launch_lean_t(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
                           uint32_t* count, int lflags, hipStream_t s, hipEvent_t a, hipEvent_t b, uint64_t g0 = 0,
-                          uint64_t ng = ~0ull) {
+                          uint64_t ng = ~0ull, uint32_t* zc = nullptr) {
   const uint64_t n = std::min<uint64_t>(ng, P.G - g0);
   hipExtLaunchKernelGGL(tick_lean_kernel<R, CRC, SEM>, grid_for(n), dim3(256), 0, s, a, b, 0, P, T, stats, list,
-                        count, lflags, uint32_t(g0));
+                        count, lflags, uint32_t(g0), zc);
 }
 
 template <int R, bool CRC, int SEM>
@@ -2111,15 +2112,15 @@ hipError_t launch_tick_two_pass(int R, int sem, const DevPlanes& P, const Trace&
 }
 hipError_t launch_tick_lean(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
                             uint32_t* count, int lflags, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop,
-                            uint64_t g0, uint64_t ng) {
+                            uint64_t g0, uint64_t ng, uint32_t* zero_count) {
   const bool crc = P.crc_on != 0;
 #define RAFT_LEAN(CRC_)                                                                                          \
   if (sem == SEM_RAFT) {                                                                                          \
     RAFT_DISPATCH_R(R, (launch_lean_t<RR, CRC_, SEM_RAFT>(P, T, stats, list, count, lflags, s, ev_start, ev_stop,   \
-                                                          g0, ng)))                                               \
+                                                          g0, ng, zero_count)))                                   \
   } else {                                                                                                        \
     RAFT_DISPATCH_R(R, (launch_lean_t<RR, CRC_, SEM_REF>(P, T, stats, list, count, lflags, s, ev_start, ev_stop,    \
-                                                         g0, ng)))                                                \
+                                                         g0, ng, zero_count)))                                    \
   }
   if (crc) { RAFT_LEAN(true); } else { RAFT_LEAN(false); }
 #undef RAFT_LEAN

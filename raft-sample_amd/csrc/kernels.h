@@ -67,10 +67,11 @@ struct ListNext {
 // compressed steady group in one launch; stats of tick j at stats + j slots.
 hipError_t launch_tick_fused(int R, int sem, const DevPlanes& P, const Trace& T, int nticks, unsigned long long* stats,
                              uint32_t* list, uint32_t* count, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop);
-// (g0, ng: the launch covers groups [g0, g0 + ng) only; g0 a multiple of 256)
+// (g0, ng: the launch covers groups [g0, g0 + ng) only; g0 a multiple of 256;
+// zero_count: list counters the launch zeroes, block 0, before anything else)
 hipError_t launch_tick_lean(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
                             uint32_t* count, int lflags, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop,
-                            uint64_t g0 = 0, uint64_t ng = ~0ull);
+                            uint64_t g0 = 0, uint64_t ng = ~0ull, uint32_t* zero_count = nullptr);
 hipError_t launch_tick_list(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                             int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
                             uint32_t* next_count, const ListNext* next, hipStream_t s, hipEvent_t ev_start,

@@ -3,7 +3,9 @@ overlapped general kernel against the oracle, across the call and window
 shapes where they hand groups from one kernel to another: calls of 1, 2, 7
 and 20 ticks, general-kernel windows of 1, 3 and 8 ticks (window ends inside a
 call, at a call's end, on consecutive ticks), pipeline on and off, in line
-and overlapped general kernel (overlapping 1, 2 or 3 ticks), calls with and without statistics (the
+and overlapped general kernel (overlapping 1, 2 or 3 ticks), the pipelined
+tick on ping-pong streams (default) or lean / list streams
+(RAFTSTEP_PINGPONG=0), calls with and without statistics (the
 stats-less form skips the per-tick records and the list kernel's second-step
 records). Workload: C4's configuration (leader
 isolation, RAFT; elections, first rounds, returns, deferrals) on 2^13 groups
@@ -32,16 +34,17 @@ def _kw(sem):
 
 
 @pytest.mark.parametrize("sem", [1, 0])
-@pytest.mark.parametrize("pipeline,overlap,slow_every,stats", [("1", "1", "8", True), ("1", "1", "3", True),
-                                                               ("1", "1", "1", True), ("1", "0", "3", True),
-                                                               ("0", "1", "3", True), ("0", "0", "8", True),
-                                                               ("1", "1", "8", False), ("1", "1", "3", False),
-                                                               ("0", "1", "3", False), ("1", "2", "8", True),
-                                                               ("1", "2", "3", True), ("1", "3", "8", True),
-                                                               ("1", "2", "1", True), ("0", "2", "3", True),
-                                                               ("1", "2", "8", False)])
-def test_pipelined_tick_matches_oracle(monkeypatch, sem, pipeline, overlap, slow_every, stats):
+@pytest.mark.parametrize("pipeline,overlap,slow_every,stats,pingpong",
+                         [("1", "1", "8", True, "1"), ("1", "1", "3", True, "1"), ("1", "1", "1", True, "1"),
+                          ("1", "0", "3", True, "1"), ("0", "1", "3", True, "1"), ("0", "0", "8", True, "1"),
+                          ("1", "1", "8", False, "1"), ("1", "1", "3", False, "1"), ("0", "1", "3", False, "1"),
+                          ("1", "2", "8", True, "1"), ("1", "2", "3", True, "1"), ("1", "3", "8", True, "1"),
+                          ("1", "2", "1", True, "1"), ("0", "2", "3", True, "1"), ("1", "2", "8", False, "1"),
+                          ("1", "2", "8", True, "0"), ("1", "1", "3", True, "0"), ("1", "2", "1", True, "0"),
+                          ("1", "2", "3", False, "0")])
+def test_pipelined_tick_matches_oracle(monkeypatch, sem, pipeline, overlap, slow_every, stats, pingpong):
     monkeypatch.setenv("RAFTSTEP_PIPELINE", pipeline)
+    monkeypatch.setenv("RAFTSTEP_PINGPONG", pingpong)
     monkeypatch.setenv("RAFTSTEP_DEBUG_PIPE", "1")
     monkeypatch.setenv("RAFTSTEP_OVERLAP_GENERAL", overlap)
     monkeypatch.setenv("RAFTSTEP_SLOW_EVERY", slow_every)
