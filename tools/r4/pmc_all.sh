@@ -1,0 +1,21 @@
+#!/bin/bash
+# PMC summaries (profiles/pmc_*.json) from an evidence session's raw passes:
+#   bash tools/r4/pmc_all.sh gpurun_out/r4m
+set -e
+O=$1; C=$(git rev-parse --short HEAD)
+B=$O/bench.json
+W2=$(python3 -c "import json;print(json.load(open('$B'))['config']['workload'])")
+W4=$(python3 -c "import json;print(json.load(open('$B'))['extra_workloads']['C4']['workload'])")
+W5=$(python3 -c "import json;print(json.load(open('$B'))['extra_workloads']['C5']['workload'])")
+S="python3 tools/pmc_summary.py --calib-fetch $O/pmc_calib_fetch --calib-write $O/pmc_calib_write --commit $C"
+$S --fetch $O/pmc_c2_fetch --write $O/pmc_c2_write --kernel tick_lean_kernel --workload "$W2" \
+   --algorithmic-bytes $((100*1048576/2)) --skip 5 --take 40 --launches-per-tick 2 --out profiles/pmc_C2_lean.json > /dev/null
+$S --fetch $O/pmc_c4_fetch --write $O/pmc_c4_write --kernel tick_lean_kernel --workload "$W4" \
+   --algorithmic-bytes $((128*4194304)) --skip 53 --take 20 --out profiles/pmc_C4_lean.json > /dev/null
+$S --fetch $O/pmc_c4_fetch --write $O/pmc_c4_write --kernel tick_list_kernel --workload "$W4" \
+   --skip 53 --take 20 --out profiles/pmc_C4_list.json > /dev/null
+$S --fetch $O/pmc_c5_fetch --write $O/pmc_c5_write --kernel tick_lean_kernel --workload "$W5" \
+   --algorithmic-bytes $((5160*1048576/2)) --skip 5 --take 40 --launches-per-tick 2 --out profiles/pmc_C5_lean.json > /dev/null
+for f in C2_lean C4_lean C4_list C5_lean; do
+  python3 -c "import json; d=json.load(open('profiles/pmc_$f.json')); print('$f', round(d.get('hbm_bytes_per_tick', d['hbm_bytes_per_launch'])/1e6,1), 'MB/tick', d.get('traffic_over_algorithmic'))"
+done
