@@ -34,12 +34,16 @@ for split in ("1", "0"):
     e.tick(1, 6)
     t = [7]
 
-    def tk(k, st=True):
+    def tk(k, st=True, dev_sync=False):
         def f():
             e.tick(t[0], k, stats=st)
             if not st:
                 e.sync()
+            if dev_sync:   # (bench.py's timed region ends with torch.cuda.synchronize)
+                torch.cuda.synchronize()
             t[0] += k
         return f
-    print("split", split, {f"tick{k}{'' if st else '_nostats'}": tm(tk(k, st)) for k in (1, 2, 20) for st in (True, False)})
+    r = {f"tick{k}{'' if st else '_nostats'}": tm(tk(k, st)) for k in (1, 2, 20) for st in (True, False)}
+    r.update({f"tick{k}_devsync": tm(tk(k, True, True)) for k in (1, 20)})
+    print("split", split, r)
     e.close()
