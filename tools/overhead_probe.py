@@ -46,4 +46,7 @@ for split in ("1", "0"):
     r = {f"tick{k}{'' if st else '_nostats'}": tm(tk(k, st)) for k in (1, 2, 20) for st in (True, False)}
     r.update({f"tick{k}_devsync": tm(tk(k, True, True)) for k in (1, 20)})
     print("split", split, r)
+    if split == "1" and os.environ.get("PROBE_COMM") == "1":   # single-rank RCCL communicator (the N>1 stats path)
+        e.comm_init(1, 0, Engine.comm_unique_id())
+        print("split 1 comm", {f"tick{k}_devsync": tm(tk(k, True, True)) for k in (1, 20)})
     e.close()
