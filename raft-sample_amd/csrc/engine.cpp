@@ -228,6 +228,7 @@ struct raft_engine {
   std::vector<hipEvent_t> comm_ev;
   int nranks = 1, rank = 0;
   uint64_t allreduces = 0;      // ncclAllReduce calls issued (diagnostics)
+  bool comm_side = false;       // a sum on comm_stream the engine stream has not waited for
 };
 
 namespace {
@@ -996,22 +997,36 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
 // once its general kernel has run: reduce them to per-tick records and, with
 // a communicator, sum those across GPUs on the comm stream (ordered by an
 // event, overlapping the following ticks on the engine stream). The call's
-// last flush also writes the end-of-call check record (chk).
+// last flush also writes the end-of-call check record (chk); its sum (call_end)
+// runs on the engine stream itself: nothing follows it to overlap, and the two
+// cross-stream hops cost ~13 us each (round 4) — after the call's earlier sums
+// on the comm stream, so the communicator sees its collectives in issue order.
 static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1, const CallCheck* chk,
-                              hipStream_t s = nullptr) {
+                              hipStream_t s = nullptr, bool call_end = false) {
   if (!s) s = e->stream;
   const uint32_t n = w1 - w0 + 1;
   HIPCHK(launch_stats_reduce(e->hist + size_t(w0) * STAT_SLOTS * NSTAT, e->tstat + size_t(w0) * NSTAT, n, s, chk));
   if (!e->comm) return RAFT_OK;
-  if (e->comm_ev.empty()) {
+  while (e->comm_ev.size() < 2) {
     hipEvent_t x;
     HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
     e->comm_ev.push_back(x);
   }
-  HIPCHK(hipEventRecord(e->comm_ev[0], s));
-  HIPCHK(hipStreamWaitEvent(e->comm_stream, e->comm_ev[0], 0));
+  hipStream_t cs = e->comm_stream;
+  if (call_end) {
+    if (e->comm_side) {
+      HIPCHK(hipEventRecord(e->comm_ev[1], e->comm_stream));
+      HIPCHK(hipStreamWaitEvent(s, e->comm_ev[1], 0));
+      e->comm_side = false;
+    }
+    cs = s;
+  } else {
+    HIPCHK(hipEventRecord(e->comm_ev[0], s));
+    HIPCHK(hipStreamWaitEvent(e->comm_stream, e->comm_ev[0], 0));
+    e->comm_side = true;
+  }
   RCCLCHK(ncclAllReduce(e->tstat + size_t(w0) * NSTAT, e->tstat + size_t(w0) * NSTAT, size_t(n) * NSTAT, ncclUint64,
-                        ncclSum, e->comm, e->comm_stream));
+                        ncclSum, e->comm, cs));
   ++e->allreduces;
   return RAFT_OK;
 }
@@ -1301,7 +1316,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       const bool wflush = !skip_list || last;
       if (stats && !overlap && wflush) {
         if (int rc = join_half()) return rc;
-        if (int rc = flush_window_stats(e, stats_first, i, (last && two) ? &chk : nullptr)) return rc;
+        if (int rc = flush_window_stats(e, stats_first, i, (last && two) ? &chk : nullptr, nullptr, last)) return rc;
       }
       if (wflush) stats_first = i + 1;
       win_first = t + 1;
@@ -1309,14 +1324,10 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   }
   if (int rc = join_half()) return rc;   // (the check record and the readback come after both halves)
   if (split && prof_b) HIPCHK(hipEventRecord(prof_b, e->stream));   // the span ends with both halves
-  if (stats && e->comm) {   // the engine stream (readback, next call) waits for the last all-reduce
-    if (e->comm_ev.size() < 2) {
-      hipEvent_t x;
-      HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
-      e->comm_ev.push_back(x);
-    }
+  if (e->comm && e->comm_side) {   // the engine stream (readback, next call) waits for the side-stream sums
     HIPCHK(hipEventRecord(e->comm_ev[1], e->comm_stream));
     HIPCHK(hipStreamWaitEvent(e->stream, e->comm_ev[1], 0));
+    e->comm_side = false;
   }
   if (!stats && skip_list) {
     // no readback in this call: the check record goes to tstat[cap + 1] and
