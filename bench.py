@@ -71,8 +71,11 @@ ENV_KNOBS = {
     "RAFTSTEP_DEBUG_FAST": "exact: prints class counters after every call (synchronising)",
     "RAFTSTEP_LIB": "path of the library under test",
     "RAFTSTEP_BENCH_SAME_DEVICE": "test hook: N ranks on one GPU, gloo, no engine communicator",
+    "RAFTSTEP_COMM_TIMEOUT_S": "exact: seconds raft_comm_init / a call's all-reduce may take before RAFT_ETIMEDOUT",
 }
 RESULTS_ALTERING = ("RAFTSTEP_DIAG_LEAN",)
+TRAFFIC_SCOPE = ("memory-side bytes per launch (L2 egress: rocprofv3 FETCH_SIZE / WRITE_SIZE, calibrated), "
+                 "Infinity-Cache (L3) hits included -- not HBM-only bytes")
 
 
 def engine_env():
@@ -114,6 +117,12 @@ WORKLOADS = {
                desc="steady-state AppendEntries+commit"),
     "C3": dict(groups=1 << 21, entries=1, ring_depth=32, crc=0, seed=0x5EED0003,
                desc="steady-state AppendEntries+commit, 2^21 groups per GPU (16M over 8 GPUs)"),
+    # C2X: the C2 shape at 2^24 groups on one GPU, so that the
+    # lean kernel's per-group words (40 B x 2^24 = 671 MB) cannot stay resident
+    # in the 256 MiB Infinity Cache between ticks: its roofline fraction is the
+    # HBM fraction (the 2^20 headline's bytes are partly L3-served)
+    "C2X": dict(groups=1 << 24, entries=1, ring_depth=32, crc=0, seed=0x5EED0002,
+                desc="steady-state AppendEntries+commit, C2 shape at 2^24 groups (beyond the Infinity Cache)"),
     "C5": dict(groups=1 << 20, entries=64, ring_depth=128, crc=1, seed=0x5EED0005,
                desc="64-entry AppendEntries batches with per-entry CRC32C stamp+verify"),
     # C4: NewNode start, leader isolation: per 32-tick epoch
@@ -136,36 +145,73 @@ WORKLOADS = {
                   iso=(8192, 8, 32, 1), seed=0x5EED0004, allow_faults=True,
                   desc="NewNode start, leader-isolation churn, REF semantics (prefix; groups freeze on their first fault)"),
 }
-EXTRA_DEFAULT = ("C4", "C5")
+EXTRA_DEFAULT = ("C2X", "C4", "C5")
 
 
-def cpu_baseline(wl, R, E, K, crc, groups, ticks):
+def cpu_baseline(wl, R, E, K, crc, groups, ticks, leader=0, check=None):
     """The oracle (C restatement of main.go's handlers, oracle/) timed on the
-    host cores on a bounded sample of the same workload."""
+    host cores on a bounded sample of the same workload: G groups (scaled
+    down) started at global offset `off`, run from the same start state
+    through the same ticks as the GPU engine (the trace RNG is keyed by the
+    global group id and groups never address each other, main.go:12, 259,
+    334, so the sample evolves exactly like those groups inside the engine).
+
+    check = (engine per-group digests, engine's next tick): the sample is run
+    at least up to the tick the engine stopped at, and there (outside the
+    timed span) its per-group digests are compared with the engine's digests
+    of the same groups -- the line's oracle check (a
+    wrong-but-plausible kernel cannot produce a line). The checker is the
+    oracle only here, in the CPU-baseline leg; the engine never calls it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     G, T = groups, ticks
     if E > 1:   # keep the sample's CPU time and memory bounded for big batches
         G, T = max(1024, 4 * G // E), max(16, T // 4)
+    Geng = wl["groups"] if check is None else len(check[0])
+    G = min(G, Geng)
+    # a seeded, unaligned offset inside the engine's group range
+    off = 0 if G >= Geng else int(np.random.default_rng(wl["seed"]).integers(0, Geng - G + 1))
     if wl.get("init") == "new":
-        G, T = G // 2, T // 2
-        o = oracle.Oracle(**engine_kwargs(wl, R, G, 0, K, E, crc))
+        G, T = max(1, G // 2), max(1, T // 2)
+        o = oracle.Oracle(**engine_kwargs(wl, R, G, off, K, E, crc))
         o.init_new_nodes(0)
         o.tick(0, wl["settle"], threads=threads)
         t_first, start = wl["settle"], "after a NewNode start and %d settle ticks" % wl["settle"]
     else:
-        o = oracle.Oracle(**engine_kwargs(wl, R, G, 0, K, E, crc))
-        o.init_steady(0, 0)
+        o = oracle.Oracle(**engine_kwargs(wl, R, G, off, K, E, crc))
+        o.init_steady(leader, 0)
         t_first, start = 1, "steady state from init_steady"
-    t0 = time.perf_counter()
-    o.tick(t_first, T, threads=threads)
-    dt = time.perf_counter() - t0
+    slice_check = None
+    dt = 0.0
+    t = t_first
+    if check is not None:
+        dig, t_end = check
+        T = max(T, t_end - t_first)
+        t0 = time.perf_counter()
+        o.tick(t, t_end - t, threads=threads)
+        dt += time.perf_counter() - t0
+        t = t_end
+        do, _ = o.state_digest()
+        bad = np.nonzero(np.asarray(dig[off:off + G]) != do)[0]
+        slice_check = {"groups": [off, off + G], "ticks": [0 if wl.get("init") == "new" else 1, t_end],
+                       "digests_equal": int(G - bad.size), "digests_differ": int(bad.size),
+                       "first_bad_group": (off + int(bad[0])) if bad.size else None, "ok": not bad.size,
+                       "what": "per-group state digests (raft_state_digest) of the GPU engine after the line's "
+                               "last call vs the oracle run over the same groups and ticks"}
+    rest = t_first + T - t
+    if rest > 0:
+        t0 = time.perf_counter()
+        o.tick(t, rest, threads=threads)
+        dt += time.perf_counter() - t0
     o.close()
-    return {"value": G * T / dt, "unit": "group-steps/s", "cores": threads, "kind": "port",
-            "sample": f"G scaled down to {G} groups (GPU line: {wl['groups']}) x {T} ticks, R={R}, E={E}, "
-                      f"crc={crc}, {start}; oracle/raft_oracle.c (C restatement of main.go's handlers), "
-                      f"{threads} pthreads over contiguous group ranges ({dt:.2f} s)"}
+    out = {"value": G * T / dt, "unit": "group-steps/s", "cores": threads, "kind": "port",
+           "sample": f"{G} groups [{off}, {off + G}) of the GPU line's {Geng} x {T} ticks, R={R}, E={E}, "
+                     f"crc={crc}, {start}; oracle/raft_oracle.c (C restatement of main.go's handlers), "
+                     f"{threads} pthreads over contiguous group ranges ({dt:.2f} s)"}
+    if slice_check is not None:
+        out["oracle_slice_check"] = slice_check
+    return out
 
 
 def engine_kwargs(wl, R, G, base, K, E, crc):
@@ -266,6 +312,7 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     # timed regions: exactly `steps` ticks each (+ the per-tick stats, reduced
     # on the device and, at N>1, all-reduced by RCCL on the engine's side stream)
     times, stats = [], np.zeros(len(STAT_NAMES), np.int64)
+    local_times = []   # this rank's own wall time per repeat (multi_gpu.per_rank)
     # C4REF (REF prefix): a group frozen by a fault does no work, so the value
     # counts only the live group-steps. With the engine communicator every
     # record is already the sum over all ranks, so the live count is computed
@@ -279,6 +326,7 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
         s = eng.tick(tick, steps, stats=True)
         ctx.barrier()
         el = time.perf_counter() - t0
+        local_times.append(el)
         if wl.get("allow_faults"):   # (outside the timed region) per-tick fault counts
             f = eng.tick_records(steps)[:, fi]
             live_steps.append(live_group_steps(scope, frozen, f))
@@ -312,6 +360,8 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
             eng.diag_enable(False)
     eng.profile(0)
     nranks, _, allreduces = eng.comm_info()
+    do_cpu = cpu and ctx.rank == 0 and world == 1
+    digests = eng.state_digest()[0] if do_cpu else None   # (the CPU leg's oracle check, untimed)
     eng.close()
 
     reps = len(times)
@@ -355,7 +405,7 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     traffic = (pmc.get("hbm_bytes_per_tick") or pmc["hbm_bytes_per_launch"]) / mean_tpl if pmc else None
     B_survey = algorithmic_bytes(R, E, crc)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_scope": TRAFFIC_SCOPE,
             "frac_measured": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
             "traffic_source": pmc_src,
             "kernel": kname,
@@ -419,8 +469,17 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
                                  "value_counts": "live (not frozen) group-steps only",
                                  "live_group_steps_median_repeat": int(round(live_value * elapsed)),
                                  "all_group_steps_per_s": total_steps / elapsed}
-    if cpu and ctx.rank == 0 and world == 1:
-        line["cpu_baseline"] = cpu_baseline(wl, R, E, K, crc, *cpu)
+    # this rank's own numbers (multi_gpu.per_rank: where scaling is lost)
+    line["rank_local"] = {"ms_per_step": median(local_times) * 1e3 / steps,
+                          "repeat_ms_per_step": [x * 1e3 / steps for x in local_times],
+                          "lean_kernel_us_per_tick": avg_kernel_s * 1e6, "stat_allreduces": allreduces}
+    if do_cpu:
+        cb = cpu_baseline(wl, R, E, K, crc, *cpu, leader=leader, check=(digests, tick))
+        line["cpu_baseline"] = cb
+        sc = cb.get("oracle_slice_check")
+        if sc is not None:
+            line["oracle_slice_check"] = sc
+            line["stats_check"] = bool(line["stats_check"] and sc["ok"])
     return line
 
 
@@ -474,12 +533,16 @@ def main():
     if same_dev:
         local = 0
     if world > 1:
+        import datetime
         import torch.distributed as dist
         torch.cuda.set_device(local)
+        # a rank that never arrives ends the run with an error, not a hang
+        # (the engine's own communicator is bounded the same way, raftstep.h)
+        tmo = datetime.timedelta(seconds=float(os.environ.get("RAFTSTEP_COMM_TIMEOUT_S", "300")))
         if same_dev:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
     ctx = Ctx(world, rank, local, dist, same_dev)
 
     wl = WORKLOADS[wl_key]
@@ -497,9 +560,13 @@ def main():
     multi = None
     if world > 1:
         ranks = [None] * world
+        rl = head["rank_local"]
         dist.all_gather_object(ranks, {"rank": rank, "group_base": rank * G, "groups": G,
                                        "rccl_nranks": head["rccl"]["nranks"],
-                                       "stat_allreduces": head["rccl"]["stat_allreduces"]})
+                                       "stat_allreduces": head["rccl"]["stat_allreduces"],
+                                       "ms_per_step": rl["ms_per_step"],
+                                       "repeat_ms_per_step": rl["repeat_ms_per_step"],
+                                       "lean_kernel_us_per_tick": rl["lean_kernel_us_per_tick"]})
         multi = {"rccl_nranks": head["rccl"]["nranks"] if not same_dev else None,
                  "engine_communicator": not same_dev, "per_rank": ranks}
         if not same_dev:
@@ -577,6 +644,18 @@ def main():
         result["fused"] = fused
     if extras:
         result["extra_workloads"] = extras
+        x = extras.get("C2X")
+        if x and "roofline" in x:
+            # the HBM fraction proper: the same kernel and bytes per group-step
+            # at a size whose per-group words cannot stay in the Infinity Cache
+            xr = x["roofline"]
+            result["roofline"]["l3_proof"] = {
+                "workload": x["workload"], "groups": x["groups_per_gpu"], "achieved": xr["achieved"],
+                "frac": xr["frac"], "frac_wall": xr["frac_wall"], "avg_kernel_us_per_tick": xr["avg_kernel_us_per_tick"],
+                "per_group_words_MB": 40 * x["groups_per_gpu"] / 1e6, "infinity_cache_MB": 256 * 1.048576,
+                "note": "the headline's 2^20 groups keep their 40 B of per-group words (42 MB) L3-resident between "
+                        "ticks, so part of its `achieved` is Infinity-Cache-served; this line's frac is the HBM "
+                        "fraction of the same kernel (extra_workloads.C2X)"}
     result["bench_wall_s"] = time.perf_counter() - t_start
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -60,6 +60,7 @@ enum raft_semantics { RAFT_SEM_REF = 0, RAFT_SEM_RAFT = 1 };
 #define RAFT_EINVAL (-22)
 #define RAFT_ENOMEM (-12)
 #define RAFT_ERANGE (-34)
+#define RAFT_ETIMEDOUT (-110) /* a communicator did not complete in time (RAFTSTEP_COMM_TIMEOUT_S) */
 #define RAFT_ENODEV (-19)
 #define RAFT_EHIP (-1000)
 #define RAFT_ERCCL (-2000)
@@ -286,11 +287,16 @@ int raft_group_ops_batch(raft_engine* e, int64_t now_tick, const raft_group_op* 
 
 /* ---- multi-GPU statistics (RCCL over xGMI) -------------------------------
  * Groups shard by id (config.group_base); the only collective is the sum of
- * tick statistics: after each general-kernel window raft_tick reduces the
- * window's per-tick records on the device (NSTAT int64 = 64 B per tick) and
- * all-reduces them on a second HIP stream, ordered by an event, so the sum
- * overlaps the following ticks. Rank 0 creates the id and distributes it out
- * of band. */
+ * tick statistics. raft_tick reduces per-tick records on the device (NSTAT
+ * int64 = 64 B per tick) and all-reduces them: in a call that runs list or
+ * general kernels, once per general-kernel window on a second HIP stream
+ * (ordered by an event, overlapping the following ticks); the call's last sum,
+ * and the only one of a steady call (list skipped), on the engine stream at
+ * the end of the call. Rank 0 creates the id and distributes it out of band.
+ * raft_comm_init and every wait on a call with a communicator are bounded by
+ * RAFTSTEP_COMM_TIMEOUT_S seconds (default 300): a missing rank or ranks that
+ * disagree end in RAFT_ETIMEDOUT with a message (an all-reduce timeout also
+ * aborts the communicator and poisons the engine), never in a hang. */
 int raft_comm_unique_id(uint8_t id_out[128]);
 int raft_comm_init(raft_engine* e, int nranks, int rank, const uint8_t id[128]);
 /* All-reduce `stats` (in/out) over the communicator (sum); no-op without one. */

@@ -9,6 +9,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -80,6 +85,14 @@ inline uint64_t ring_index(uint64_t r, uint64_t g, uint64_t s, uint64_t K, uint6
   return (((g >> 6) * K + s) * 64 + (g & 63)) * R + r;
 }
 
+// RAFTSTEP_COMM_TIMEOUT_S: seconds a communicator's init or a call's
+// all-reduce may take before it fails with RAFT_ETIMEDOUT (default 300)
+double comm_timeout_s() {
+  const char* t = getenv("RAFTSTEP_COMM_TIMEOUT_S");
+  const double v = t ? atof(t) : 300.0;
+  return v > 0 ? v : 300.0;
+}
+
 bool fits32(int64_t v) { return v >= -int64_t(I32) - 1 && v <= int64_t(I32); }
 
 }  // namespace
@@ -136,6 +149,11 @@ struct raft_engine {
   uint32_t gen_join = 0;        // the call's tick index after whose launches the engine stream joins it
   uint32_t gen_top = 0;         // the last tick index it counts stats into
   bool gen_stats = false;       // it counts into those per-tick slots of hist
+  // per-tick atomic slots of hist a call may have counted into and not
+  // reduced (the reduce re-zeroes what it reads): set when a call with
+  // statistics starts launching, cleared when it has issued every reduce; a
+  // call that fails in between leaves it set and the next call zeroes them
+  uint32_t hist_dirty = 0;
   int force_general = 0;        // debug: route every group through the general kernel
   int lane_general = 0;         // RAFTSTEP_GENERAL=lane: one-lane-per-group general kernel (A/B) instead of the segment one
   uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
@@ -591,7 +609,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
   e->P.diag = diag_lean;
   if (const char* sp = getenv("RAFTSTEP_SPLIT_STEADY")) e->split_steady = atoi(sp) != 0;
-  if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = std::min(4, std::max(0, atoi(og)));
+  // (the depths the oracle tests cover: 0..3, tests/test_gpu_pipeline.py)
+  if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = std::min(3, std::max(0, atoi(og)));
   if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = atoi(pp) != 0;
   if (const char* pg = getenv("RAFTSTEP_PINGPONG")) e->pingpong = atoi(pg) != 0;
   e->fuse = std::max<uint32_t>(1u, c.ticks_per_launch);
@@ -1057,15 +1076,20 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   HIPCHK(hipSetDevice(e->cfg.device));
   if (e->gen_pending) {   // (only after a failed call: every call joins its general kernels)
     if (int rc = join_general(e, false)) return rc;
-    // its window's per-tick slots were never reduced (the reduce is what
-    // re-zeroes them): zero them, or the next call's stats would include them
-    if (e->gen_stats)
-      HIPCHK(hipMemsetAsync(e->hist + size_t(e->gen_w0) * STAT_SLOTS * NSTAT, 0,
-                            size_t(e->gen_top - e->gen_w0 + 1) * STAT_SLOTS * NSTAT * 8, e->stream));
+  }
+  if (e->hist_dirty) {
+    // a failed call's per-tick slots were never reduced (the reduce is what
+    // re-zeroes them): zero every slot it may have counted into, after all of
+    // its kernels (on any of the engine's streams) are done, or the next
+    // call's stats would include them
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemsetAsync(e->hist, 0, size_t(e->hist_dirty) * STAT_SLOTS * NSTAT * 8, e->stream));
+    e->hist_dirty = 0;
   }
   // (the per-tick records need nticks slots; the check records exist at any capacity)
   if (int rc = ensure_hist(e, stats ? std::max<uint32_t>(nticks, 1) : 1)) return rc;
   if (!nticks) return RAFT_OK;
+  if (stats) e->hist_dirty = nticks;   // (cleared once every reduce of this call is issued)
   const Trace T0 = make_trace(e, first_tick);
   int64_t win_first = first_tick;   // first tick of the current general-kernel window
   // steady-state list skip (see raft_engine): entries per tick at most E, so
@@ -1316,6 +1340,12 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       const bool wflush = !skip_list || last;
       if (stats && !overlap && wflush) {
         if (int rc = join_half()) return rc;
+        // profile mode 1: the span of the call's launches ends with both
+        // halves, before the reduce (raftstep.h)
+        if (last && split && prof_b) {
+          HIPCHK(hipEventRecord(prof_b, e->stream));
+          prof_b = nullptr;
+        }
         if (int rc = flush_window_stats(e, stats_first, i, (last && two) ? &chk : nullptr, nullptr, last)) return rc;
       }
       if (wflush) stats_first = i + 1;
@@ -1324,6 +1354,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   }
   if (int rc = join_half()) return rc;   // (the check record and the readback come after both halves)
   if (split && prof_b) HIPCHK(hipEventRecord(prof_b, e->stream));   // the span ends with both halves
+  e->hist_dirty = 0;   // every reduce of the call is issued
   if (e->comm && e->comm_side) {   // the engine stream (readback, next call) waits for the side-stream sums
     HIPCHK(hipEventRecord(e->comm_ev[1], e->comm_stream));
     HIPCHK(hipStreamWaitEvent(e->stream, e->comm_ev[1], 0));
@@ -1360,6 +1391,40 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   return RAFT_OK;
 }
 
+// Waits for the engine stream. With a communicator the wait is bounded by
+// RAFTSTEP_COMM_TIMEOUT_S: an all-reduce whose peers never arrive (a rank
+// gone, or ranks issuing different collectives) aborts the communicator and
+// poisons the engine with RAFT_ETIMEDOUT instead of hanging the caller.
+static int wait_stream(raft_engine* e) {
+  if (!e->comm) {
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return RAFT_OK;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const double tmo = comm_timeout_s();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(e->stream);
+    if (q == hipSuccess) return RAFT_OK;
+    if (q != hipErrorNotReady) return fail(RAFT_EHIP, "hipStreamQuery: %s", hipGetErrorString(q));
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > tmo) {
+      (void)ncclCommAbort(e->comm);
+      e->comm = nullptr;
+      e->poisoned = true;
+      e->poison_msg = "RCCL statistics all-reduce did not complete within " + std::to_string(int(tmo)) +
+                      " s (RAFTSTEP_COMM_TIMEOUT_S): communicator aborted";
+      return fail(RAFT_ETIMEDOUT, "%s", e->poison_msg.c_str());
+    }
+    if (el > 2e-3) std::this_thread::yield();
+#if defined(__x86_64__) || defined(__i386__)
+    else __builtin_ia32_pause();
+#endif
+  }
+}
+
+// longest host spin on a mirrored call's completion word (raft_tick)
+constexpr std::chrono::microseconds kMirrorSpin{2000};
+
 int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_stats* out) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
   if (int rc = tick_impl(e, first_tick, nticks, out != nullptr)) return rc;
@@ -1374,16 +1439,23 @@ int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_sta
       // the records are already in hrb: wait for the launch's completion flag
       // (spinning; the stream is polled too, so a failed launch ends the wait),
       // then for the stream (its completion signal follows within microseconds)
+      // The spin is bounded: past kMirrorSpin the host blocks in
+      // hipStreamSynchronize below instead of holding a core for a long call.
       const volatile uint32_t* done = e->hdone;
+      const auto t_spin = std::chrono::steady_clock::now();
       for (uint32_t k = 1; *done != e->seq; ++k) {
+#if defined(__x86_64__) || defined(__i386__)
         __builtin_ia32_pause();
-        if ((k & 1023u) == 0 && hipStreamQuery(e->stream) != hipErrorNotReady) break;
+#endif
+        if ((k & 1023u) == 0 && (hipStreamQuery(e->stream) != hipErrorNotReady ||
+                                 std::chrono::steady_clock::now() - t_spin > kMirrorSpin))
+          break;
       }
       e->mirror = false;
     } else {
       HIPCHK(hipMemcpyAsync(e->hrb, e->tstat, words * 8, hipMemcpyDeviceToHost, e->stream));
     }
-    HIPCHK(hipStreamSynchronize(e->stream));
+    if (int rc = wait_stream(e)) return rc;
     e->last_stats_n = nticks;
     for (size_t i = 0; i < size_t(nticks) * NSTAT; ++i) out->v[i % NSTAT] += int64_t(e->hrb[i]);
     if (two) {
@@ -1554,7 +1626,45 @@ int raft_comm_init(raft_engine* e, int nranks, int rank, const uint8_t id[128]) 
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
   if (!e->comm_stream) HIPCHK(hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
-  RCCLCHK(ncclCommInitRank(&e->comm, nranks, uid, rank));
+  // ncclCommInitRank blocks until every rank has joined: it runs on a helper
+  // thread so that a missing rank, or ranks disagreeing on nranks or the id,
+  // ends in RAFT_ETIMEDOUT with a message instead of a hang (the caller then
+  // exits; a helper still blocked in RCCL is abandoned with the process)
+  struct InitJob {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false;
+    ncclResult_t r = ncclSuccess;
+    ncclComm_t comm = nullptr;
+  };
+  auto job = std::make_shared<InitJob>();
+  const int dev = e->cfg.device;
+  std::thread([job, dev, nranks, rank, uid]() {
+    ncclComm_t c = nullptr;
+    ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclCommInitRank(&c, nranks, uid, rank) : ncclInvalidUsage;
+    std::lock_guard<std::mutex> lk(job->m);
+    job->r = r;
+    job->comm = c;
+    job->done = true;
+    job->cv.notify_all();
+  }).detach();
+  const double tmo = comm_timeout_s();
+  std::unique_lock<std::mutex> lk(job->m);
+  if (!job->cv.wait_for(lk, std::chrono::duration<double>(tmo), [&] { return job->done; }))
+    return fail(RAFT_ETIMEDOUT, "raft_comm_init: ncclCommInitRank(nranks=%d, rank=%d) did not complete within %.0f s "
+                "(RAFTSTEP_COMM_TIMEOUT_S): a rank is missing, or the ranks disagree on nranks or the unique id",
+                nranks, rank, tmo);
+  if (job->r != ncclSuccess)
+    return fail(RAFT_ERCCL, "raft_comm_init: ncclCommInitRank(nranks=%d, rank=%d): %s", nranks, rank,
+                ncclGetErrorString(job->r));
+  e->comm = job->comm;
+  int n = 0, r = -1;
+  if (ncclCommCount(e->comm, &n) != ncclSuccess || ncclCommUserRank(e->comm, &r) != ncclSuccess || n != nranks ||
+      r != rank) {
+    (void)ncclCommAbort(e->comm);
+    e->comm = nullptr;
+    return fail(RAFT_ERCCL, "raft_comm_init: communicator has %d ranks / rank %d, asked for %d / %d", n, r, nranks, rank);
+  }
   e->nranks = nranks;
   e->rank = rank;
   return RAFT_OK;
@@ -1583,7 +1693,7 @@ int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats) {
   HIPCHK(hipMemcpyAsync(e->cstat, h.data(), NSTAT * 8, hipMemcpyHostToDevice, e->stream));
   RCCLCHK(ncclAllReduce(e->cstat, e->cstat, NSTAT, ncclUint64, ncclSum, e->comm, e->stream));
   HIPCHK(hipMemcpyAsync(h.data(), e->cstat, NSTAT * 8, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
+  if (int rc = wait_stream(e)) return rc;
   for (int s = 0; s < NSTAT; ++s) stats->v[s] = int64_t(h[s]);
   return RAFT_OK;
 }

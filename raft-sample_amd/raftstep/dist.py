@@ -21,10 +21,17 @@ def shard(groups_total, world, rank):
 
 
 def exchange_comm_id(dist, rank, make_id):
-    """Rank 0 creates the RCCL unique id; every rank receives it."""
-    box = [make_id() if rank == 0 else None]
+    """Rank 0 creates the RCCL unique id; every rank receives it, with rank
+    0's world size: a rank whose process group disagrees fails here, with a
+    message, before it reaches raft_comm_init (whose own wait is bounded by
+    RAFTSTEP_COMM_TIMEOUT_S)."""
+    world = dist.get_world_size()
+    box = [(make_id(), world) if rank == 0 else None]
     dist.broadcast_object_list(box, src=0)
-    return box[0]
+    uid, world0 = box[0]
+    if world0 != world or not 0 <= rank < world:
+        raise RuntimeError(f"rank {rank}: world size {world}, rank 0 has {world0}")
+    return uid
 
 
 def max_over_ranks(dist, value, device=None):

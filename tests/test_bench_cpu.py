@@ -61,3 +61,37 @@ def test_byte_accounting(R, E, crc, seg, fuse, want):
 def test_survey_bytes():
     assert bench.algorithmic_bytes(5, 1) == 233 and bench.algorithmic_bytes(7, 1) == 331
     assert bench.algorithmic_bytes(5, 64, crc=True) == 5293
+
+
+@pytest.mark.parametrize("name", ["C2", "C4"])
+def test_cpu_leg_oracle_slice_check(name):
+    """the CPU-baseline leg runs its oracle sample over a slice
+    of the GPU line's groups through the same ticks and compares per-group
+    digests. Here the 'engine' digests come from a full oracle of a small
+    engine; one flipped digest inside the slice must fail the check."""
+    import oracle
+    wl = dict(bench.WORKLOADS[name], groups=3000)
+    R = wl.get("replicas", bench.R_DEFAULT)
+    kw = bench.engine_kwargs(wl, R, 3000, 0, wl["ring_depth"], wl["entries"], wl["crc"])
+    full = oracle.Oracle(**kw)
+    churn = wl.get("init") == "new"
+    if churn:
+        full.init_new_nodes(0)
+        full.tick(0, wl["settle"] + 30)
+        t_end = wl["settle"] + 30
+    else:
+        full.init_steady(0, 0)
+        full.tick(1, 40)
+        t_end = 41
+    dig, _ = full.state_digest()
+    full.close()
+    cb = bench.cpu_baseline(wl, R, wl["entries"], wl["ring_depth"], wl["crc"], 1200, 64, check=(dig, t_end))
+    sc = cb["oracle_slice_check"]
+    assert sc["ok"] and sc["digests_differ"] == 0 and sc["digests_equal"] > 0, sc
+    lo, hi = sc["groups"]
+    assert 0 <= lo < hi <= 3000
+    bad = dig.copy()
+    bad[lo + (hi - lo) // 2] ^= 1
+    sc2 = bench.cpu_baseline(wl, R, wl["entries"], wl["ring_depth"], wl["crc"], 1200, 64,
+                             check=(bad, t_end))["oracle_slice_check"]
+    assert not sc2["ok"] and sc2["digests_differ"] == 1

@@ -2,6 +2,8 @@
 # Builds an A/B variant of libraftstep.so with extra compile-time flags into
 # ablib/<name>/ (bench.py / tests pick it with RAFTSTEP_LIB=ablib/<name>/libraftstep.so).
 #   tools/ablib.sh la32 -DRAFTSTEP_LIST_LANES=32
+# ablib/ is in .gpurunignore (it never travels with the snapshot): build the
+# variants ON the GPU box, inside the gpurun command (tools/gpu_ab.sh does).
 set -e
 name=$1; shift
 cd "$(dirname "$0")/../raft-sample_amd/csrc"

@@ -3,6 +3,8 @@
 # lines, one per variant per round ("base" = raft-sample_amd/lib, else
 # ablib/<name>). Then, with TESTS set, the named tests on each non-base variant.
 #   OUTDIR=r4ab VARIANTS="base la32" ARGS="--workload C4" ROUNDS=3 TESTS="tests/test_gpu_fullsize.py" bash tools/gpu_ab.sh
+# BUILD="la32:-DRAFTSTEP_LIST_LANES=32 other:-DX" builds those variants on the box first
+# (tools/ablib.sh; ablib/ does not travel with the snapshot).
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -16,6 +18,10 @@ variant() {   # sets label, lib, envs
   label=${v%%+*}; envs=""; lib=raft-sample_amd/lib/libraftstep.so
   if [[ "$v" == *+* ]]; then envs=$(echo "${v#*+}" | tr '+' ' '); elif [ "$v" != base ]; then lib=ablib/$v/libraftstep.so; fi
 }
+for b in $BUILD; do
+  echo "== $(date +%T) build ${b%%:*}" >> "$OUT/progress.log"
+  timeout -k 10 600 bash tools/ablib.sh "${b%%:*}" $(echo "${b#*:}" | tr ',' ' ') >> "$OUT/build.log" 2>&1 || { echo "build $b failed"; exit 1; }
+done
 for r in $(seq 1 ${ROUNDS:-3}); do
   for v in $VARIANTS; do
     variant "$v"

@@ -11,12 +11,14 @@
 #   pmc       FETCH_SIZE / WRITE_SIZE passes (separate runs) of the calibration
 #             kernel and of the C2 headline (tools/pmc_summary.py)
 #   pmcc4     the same for C4 (lean and list kernels)
+#   profc2x / pmcc2x  kernel trace / PMC passes of C2X (C2 at 2^24 groups, L3-proof)
+#   sqc5      one SQ counter pass of C5 (LDS instructions and waits, busy cycles)
 #   smoke     __graft_entry__.smoke()
 #   bench:ARGS  bench.py with extra arguments (ARGS: comma-separated)
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-OUT=gpurun_out/${OUTDIR:-r4}
+OUT=gpurun_out/${OUTDIR:-r5}
 mkdir -p "$OUT"
 B="python3 -u bench.py --steps 20 --warmup 5"
 Q="--steps 20 --warmup 5 --repeats 1 --no-cpu-baseline --no-fused --extra none --no-list-count"
@@ -40,6 +42,12 @@ for s in "$@"; do
          && $P --pmc WRITE_SIZE -d "$OUT/pmc_calib_write" -o p --output-format csv -- ./tools/pmc_calib > "$OUT/pmc2.log" 2>&1 \
          && $P --pmc FETCH_SIZE -d "$OUT/pmc_c2_fetch" -o p --output-format csv -- python3 -u bench.py $Q > "$OUT/pmc3.log" 2>&1 \
          && $P --pmc WRITE_SIZE -d "$OUT/pmc_c2_write" -o p --output-format csv -- python3 -u bench.py $Q > "$OUT/pmc4.log" 2>&1 ;;
+    profc2x) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c2x" -o run --output-format csv \
+              -- python3 -u bench.py --workload C2X $Q > "$OUT/prof_c2x.log" 2>&1 ;;
+    pmcc2x) $P --pmc FETCH_SIZE -d "$OUT/pmc_c2x_fetch" -o p --output-format csv -- python3 -u bench.py --workload C2X $Q > "$OUT/pmc9.log" 2>&1 \
+            && $P --pmc WRITE_SIZE -d "$OUT/pmc_c2x_write" -o p --output-format csv -- python3 -u bench.py --workload C2X $Q > "$OUT/pmc10.log" 2>&1 ;;
+    sqc5) $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM_WR \
+            -d "$OUT/sq_c5" -o p --output-format csv -- python3 -u bench.py --workload C5 $Q > "$OUT/sq5.log" 2>&1 ;;
     profc5) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv \
               -- python3 -u bench.py --workload C5 $Q > "$OUT/prof_c5.log" 2>&1 ;;
     pmcc5) $P --pmc FETCH_SIZE -d "$OUT/pmc_c5_fetch" -o p --output-format csv -- python3 -u bench.py --workload C5 $Q > "$OUT/pmc7.log" 2>&1 \
@@ -48,9 +56,6 @@ for s in "$@"; do
             -d "$OUT/sq_c4" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/sq1.log" 2>&1 ;;
     sqc4r) $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_IFETCH SQ_INSTS_SMEM \
              -d "$OUT/sq_c4r" -o p --output-format csv -- python3 -u bench.py --workload C4R $Q > "$OUT/sq2.log" 2>&1 ;;
-    sqr2) (cd ablib/r2tree && $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_IFETCH SQ_INSTS_SMEM \
-             -d "../../$OUT/sq_r2_c4r" -o p --output-format csv -- python3 -u bench.py --workload C4R --steps 20 --warmup 5 \
-             --repeats 1 --no-cpu-baseline) > "$OUT/sq3.log" 2>&1 ;;
     pmcc4) $P --pmc FETCH_SIZE -d "$OUT/pmc_c4_fetch" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc5.log" 2>&1 \
            && $P --pmc WRITE_SIZE -d "$OUT/pmc_c4_write" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc6.log" 2>&1 ;;
     *) echo "unknown step $s" >&2; exit 2 ;;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC summaries (profiles/pmc_*.json) from an evidence session's raw passes:
-#   bash tools/r4/pmc_all.sh gpurun_out/r4m
+#   bash tools/pmc_all.sh gpurun_out/r4m
 set -e
 O=$1; C=$(git rev-parse --short HEAD)
 B=$O/bench.json
