@@ -669,18 +669,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           if (p != c && p != xi && P.corrupt_p &&
               (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(T.tick)) & 0xFFFF) < P.corrupt_p)
             cm |= 1u << p;
-        const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
-        const uint32_t cs = crc_term_state(tab, Lt);
-        for (int e = 0; e < n; ++e) {
-          const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
-          const uint32_t stamp = crc_value_final(tab, cs, v);               // leader's stamp
-#pragma unroll
-          for (int p = 0; p < R; ++p) {
-            if (p == c || p == xi) continue;
-            const int64_t rv = v ^ ((((cm >> p) & 1u) && e == n - 1) ? 1 : 0);  // what p received
-            if (crc_value_final(tab, cs, rv) != stamp) crcbad |= 1u << p;
-          }
-        }
+        // (an unaltered copy carries the leader's stamp: CRCs only for cm)
+        if (cm) crcbad = crc_reject_mask(tab, crc_term_state(tab, Lt), rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick)),
+                                         n, cm);
       }
     }
     uint32_t okm = 0, cch = 0, mch = 0, ltch = 0;
@@ -1066,6 +1057,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   if (LIST && (P.diag & 128u)) {   // timing only (results wrong): the per-group code alone
     wr = 0; cp_n = 0; mv_n = 0;
   }
+  if (LIST && (P.diag & 512u)) {   // timing only (results wrong): no entry copies or moves
+    cp_n = 0; mv_n = 0;
+  }
   // ---- this tick's log entries into the rings (all lanes of the wave) ----
   // Ring row of one slot = 64 lanes x R replicas, contiguous. The lanes of
   // the wave that append at the wave's common slot s0 (logs in step: the
@@ -1397,7 +1391,7 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
   constexpr uint32_t GPB = uint32_t(LB) / 64u * LIST_LANES;   // groups per block and round
   shard_zero(next_count);
   const uint32_t n = shard_prefix(count, pre);
-  if (blockIdx.x * GPB >= n) return;
+  if (blockIdx.x * GPB >= n || (P.diag & 256u)) return;   // (diag 256, timing only: no list work at all)
   stage_crc_tab<CRC>(P, tab);
   const uint32_t t = threadIdx.x;
   const uint32_t lane = t & 63u;
@@ -1704,19 +1698,10 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
             for (int p = 0; p < R; ++p)
               if (p != c && P.corrupt_p && (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(T.tick)) & 0xFFFF) < P.corrupt_p)
                 cm |= 1u << p;
-            uint32_t bad = 0;   // (as fast_group: each follower checks the copy it received)
-            const uint32_t cs = crc_term_state(tab, s.term);
-            for (int e = 0; e < n; ++e) {
-              const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
-              const uint32_t stamp = crc_value_final(tab, cs, v);   // leader's stamp
-#pragma unroll
-              for (int p = 0; p < R; ++p) {
-                if (p == c) continue;
-                const int64_t rv = v ^ ((((cm >> p) & 1u) && e == n - 1) ? 1 : 0);   // what p received
-                if (crc_value_final(tab, cs, rv) != stamp) bad |= 1u << p;
-              }
-            }
-            take &= bad == 0u;
+            // (as fast_group: each follower checks the copy it received; an
+            // unaltered copy carries the leader's stamp, so only cm's need a
+            // CRC — the stamps themselves are computed once, in the row stores)
+            if (cm) take &= crc_reject_mask(tab, crc_term_state(tab, s.term), vb, n, cm) == 0u;
           }
         }
         nl = L + n;

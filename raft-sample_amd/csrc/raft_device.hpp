@@ -366,6 +366,20 @@ __device__ __forceinline__ uint32_t crc_entry(const uint32_t* T, int term, int64
   return crc_value_final(T, crc_term_state(T, term), value);
 }
 
+// The followers' verification of one AppendEntries batch of n entries (value
+// stream vb, the term's CRC state cs) against the leader's stamps, with the
+// CRC computed once per entry: every follower receives the
+// leader's bytes (main.go:148-149 appends what it received), so an unaltered
+// copy has exactly the leader's stamp and needs no CRC; only the followers of
+// `cm` receive an altered copy (EXT corruption: the batch's last value with
+// bit 0 flipped), each checked against the leader's stamp of that entry.
+// Returns the followers whose copy fails (a subset of cm).
+__device__ __forceinline__ uint32_t crc_reject_mask(const uint32_t* T, uint32_t cs, uint64_t vb, int n, uint32_t cm) {
+  if (!cm || n <= 0) return 0u;
+  const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(n - 1))) >> 1);
+  return crc_value_final(T, cs, v ^ 1) != crc_value_final(T, cs, v) ? cm : 0u;
+}
+
 // ------------------------------------------------- register-array helpers --
 // Runtime-indexed access to a register array without letting LLVM fold the
 // select chain into a dynamic GEP (which would demote the whole Group to
