@@ -1551,7 +1551,14 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   if (T.iso_p) im = iso_windows<R>(key, T, &act, &starting);
   bool held = false;
   if (g < P.G) {
+    // gmeta and, speculatively, the record, the ring rotation and the segment
+    // boundary go out together: one round trip instead of two for the groups
+    // the lean pass takes (nearly all of them; round 5, C2 at 2^24 groups,
+    // where these reads miss the Infinity Cache)
     const int meta = at(P.gmeta, g);
+    const SsRec s = P.gss[g];
+    const int rot = at(P.grot, g);
+    const int sb0 = P.KP > P.K ? at(P.gsb, g) : 0;
     // pipelined tick: a group the last list kernel carries through this tick
     // too is left alone (its state is being written beside this kernel); the
     // mark is cleared with the kernel's other stores at the end (a store here
@@ -1564,11 +1571,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     df |= (!skip && g == P.dbg_pass) ? 1u << 24 : 0u;
     df |= skip ? 1u : 0u;
     if (take) {
-      const SsRec s = P.gss[g];
       const LxRec gx = (RAFT && uses_glx(meta)) ? P.glx[g] : LxRec{0, 0};
       uint32_t gi = (RAFT && T.iso_p && act && uses_glx(meta)) ? uint32_t(at(P.giso, g)) : 0u;
-      const int rot = at(P.grot, g);
-      const int sb0 = P.KP > P.K ? at(P.gsb, g) : 0;
       int hwmx = 0;   // RAFT HWX: the highest high-water mark (the hwm plane)
       if (RAFT && (meta & M_HWX)) {
         int hw[R];

@@ -16,7 +16,9 @@ B="python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fused --extr
 variant() {   # sets label, lib, envs
   local v=$1
   label=${v%%+*}; envs=""; lib=raft-sample_amd/lib/libraftstep.so
-  if [[ "$v" == *+* ]]; then envs=$(echo "${v#*+}" | tr '+' ' '); elif [ "$v" != base ]; then lib=ablib/$v/libraftstep.so; fi
+  if [[ "$v" == *+* ]]; then envs=$(echo "${v#*+}" | tr '+' ' ');
+  elif [ -f "raft-sample_amd/lib/ab/$v/libraftstep.so" ]; then lib=raft-sample_amd/lib/ab/$v/libraftstep.so;   # (pushed prebuilt)
+  elif [ "$v" != base ]; then lib=ablib/$v/libraftstep.so; fi
 }
 for b in $BUILD; do
   echo "== $(date +%T) build ${b%%:*}" >> "$OUT/progress.log"

@@ -18,6 +18,8 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
+# LIB=path: run every step with that build of libraftstep.so (A/B evidence)
+[ -n "$LIB" ] && export RAFTSTEP_LIB="$LIB"
 OUT=gpurun_out/${OUTDIR:-r5}
 mkdir -p "$OUT"
 B="python3 -u bench.py --steps 20 --warmup 5"
@@ -46,6 +48,8 @@ for s in "$@"; do
               -- python3 -u bench.py --workload C2X $Q > "$OUT/prof_c2x.log" 2>&1 ;;
     pmcc2x) $P --pmc FETCH_SIZE -d "$OUT/pmc_c2x_fetch" -o p --output-format csv -- python3 -u bench.py --workload C2X $Q > "$OUT/pmc9.log" 2>&1 \
             && $P --pmc WRITE_SIZE -d "$OUT/pmc_c2x_write" -o p --output-format csv -- python3 -u bench.py --workload C2X $Q > "$OUT/pmc10.log" 2>&1 ;;
+    sqc2x) $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM_WR \
+            -d "$OUT/sq_c2x" -o p --output-format csv -- python3 -u bench.py --workload C2X $Q > "$OUT/sq2x.log" 2>&1 ;;
     sqc5) $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM_WR \
             -d "$OUT/sq_c5" -o p --output-format csv -- python3 -u bench.py --workload C5 $Q > "$OUT/sq5.log" 2>&1 ;;
     profc5) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv \
