@@ -473,6 +473,17 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     line["rank_local"] = {"ms_per_step": median(local_times) * 1e3 / steps,
                           "repeat_ms_per_step": [x * 1e3 / steps for x in local_times],
                           "lean_kernel_us_per_tick": avg_kernel_s * 1e6, "stat_allreduces": allreduces}
+    if world == 1 and not churn and not crc and E == 1 and not fused:
+        # this device's sustained rate for the lean kernel's byte mix and access
+        # shape at the same size (raft_stream_probe: fresh buffers, no Raft
+        # state): the practical roofline of this kernel on this box
+        from raftstep import stream_probe
+        pus, pby = stream_probe(ctx.local, R, G, 10)
+        roof["stream_probe"] = {"GBs": pby / pus / 1e3, "us_per_pass": pus, "bytes_per_pass": pby,
+                                "what": "raft_stream_probe: per element 20 B read in one round trip, 40 + 12R B "
+                                        "(100 B at R=5) moved, record / heartbeat / whole-ring-row stores, on "
+                                        "fresh buffers of the line's group count"}
+        roof["frac_of_stream_probe"] = achieved / (pby / pus / 1e3)
     if do_cpu:
         cb = cpu_baseline(wl, R, E, K, crc, *cpu, leader=leader, check=(digests, tick))
         line["cpu_baseline"] = cb
@@ -652,6 +663,8 @@ def main():
             result["roofline"]["l3_proof"] = {
                 "workload": x["workload"], "groups": x["groups_per_gpu"], "achieved": xr["achieved"],
                 "frac": xr["frac"], "frac_wall": xr["frac_wall"], "avg_kernel_us_per_tick": xr["avg_kernel_us_per_tick"],
+                "stream_probe_GBs": (xr.get("stream_probe") or {}).get("GBs"),
+                "frac_of_stream_probe": xr.get("frac_of_stream_probe"),
                 "per_group_words_MB": 40 * x["groups_per_gpu"] / 1e6, "infinity_cache_MB": 256 * 1.048576,
                 "note": "the headline's 2^20 groups keep their 40 B of per-group words (42 MB) L3-resident between "
                         "ticks, so part of its `achieved` is Infinity-Cache-served; this line's frac is the HBM "

@@ -383,6 +383,20 @@ int raft_debug_force_pass(raft_engine* e, int64_t group);
  * compressed record gss[4], glx[2], grot, grota, gsb, grotb, gsb2). */
 #define RAFT_DEBUG_GROUP_WORDS 14u
 int raft_debug_group_words(raft_engine* e, uint64_t group, int32_t* out, uint32_t n);
+/* Timing diagnostics (results WRONG while non-zero): replaces the engine's
+ * kernel diagnostic mode (RAFTSTEP_DIAG_LEAN's bits) from the next call on,
+ * e.g. after a settle; RAFT_EINVAL unless the engine was created with
+ * debug_flags RAFT_DEBUG_ALLOW_WRONG_RESULTS. 0 restores exact ticks (the
+ * state is then whatever the diagnostic ticks left). */
+int raft_debug_diag_mode(raft_engine* e, uint32_t mode);
+/* Measurement: the steady lean kernel's byte mix and access shape (per
+ * element 20 B read in one round trip, 20 B of record + heartbeat and R ring
+ * entries of 12 B written as whole rows; 20 + 20 + 12 R bytes) over `elems`
+ * fresh elements on `device`, no Raft state: one untimed pass, then `reps`
+ * back-to-back passes between HIP events. Returns the mean pass time and the
+ * bytes per pass (bench.py: the device's sustained rate for that pattern). */
+int raft_stream_probe(int device, uint32_t replicas, uint64_t elems, uint32_t reps, double* us_per_pass,
+                      double* bytes_per_pass);
 
 #ifdef __cplusplus
 }

@@ -1795,6 +1795,65 @@ int raft_debug_group_words(raft_engine* e, uint64_t group, int32_t* out, uint32_
   return RAFT_OK;
 }
 
+int raft_stream_probe(int device, uint32_t replicas, uint64_t elems, uint32_t reps, double* us_per_pass,
+                      double* bytes_per_pass) {
+  if (!us_per_pass || !bytes_per_pass) return fail(RAFT_EINVAL, "null argument");
+  if (replicas < 1 || replicas > RAFT_MAX_REPLICAS || elems < 64 || elems > (1ull << 26) || reps < 1)
+    return fail(RAFT_EINVAL, "replicas 1..8, elems 64..2^26, reps >= 1");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return fail(RAFT_ENODEV, "no such device");
+  HIPCHK(hipSetDevice(device));
+  const uint64_t n = (elems + 255) & ~uint64_t(255), R = replicas, KS = 2;
+  std::vector<void*> mem;
+  auto alloc = [&](size_t bytes) -> void* {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    mem.push_back(p);
+    return hipMemset(p, 0, bytes) == hipSuccess ? p : nullptr;
+  };
+  auto* a = static_cast<uint16_t*>(alloc(n * 2));
+  auto* b = static_cast<SsRec*>(alloc(n * sizeof(SsRec)));
+  auto* c = static_cast<uint16_t*>(alloc(n * 2));
+  auto* d = static_cast<int32_t*>(alloc(n * 4));
+  auto* rt = static_cast<int32_t*>(alloc(n * KS * R * 4));
+  auto* rv = static_cast<int64_t*>(alloc(n * KS * R * 8));
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = RAFT_OK;
+  if (!a || !b || !c || !d || !rt || !rv) rc = fail(RAFT_ENOMEM, "stream probe: hipMalloc failed");
+  if (rc == RAFT_OK && (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+                        hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess))
+    rc = fail(RAFT_EHIP, "stream probe: stream / event creation failed");
+  float ms = 0.f;
+  if (rc == RAFT_OK) {
+    hipError_t h = launch_stream_probe(int(R), a, b, c, d, rt, rv, uint32_t(n), 1u, uint32_t(KS), s);
+    if (h == hipSuccess) h = hipEventRecord(e0, s);
+    for (uint32_t i = 0; i < reps && h == hipSuccess; ++i)
+      h = launch_stream_probe(int(R), a, b, c, d, rt, rv, uint32_t(n), i & 1u, uint32_t(KS), s);
+    if (h == hipSuccess) h = hipEventRecord(e1, s);
+    if (h == hipSuccess) h = hipEventSynchronize(e1);
+    if (h == hipSuccess) h = hipEventElapsedTime(&ms, e0, e1);
+    if (h != hipSuccess) rc = fail(RAFT_EHIP, "stream probe: %s", hipGetErrorString(h));
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (s) (void)hipStreamDestroy(s);
+  for (void* p : mem) (void)hipFree(p);
+  if (rc != RAFT_OK) return rc;
+  *us_per_pass = double(ms) * 1e3 / reps;
+  *bytes_per_pass = double(n) * double(40 + 12 * R);
+  return RAFT_OK;
+}
+
+int raft_debug_diag_mode(raft_engine* e, uint32_t mode) {
+  if (!e) return fail(RAFT_EINVAL, "null engine");
+  if (mode && !(e->cfg.debug_flags & RAFT_DEBUG_ALLOW_WRONG_RESULTS))
+    return fail(RAFT_EINVAL, "diagnostic mode %u makes results wrong; create the engine with debug_flags "
+                "RAFT_DEBUG_ALLOW_WRONG_RESULTS", mode);
+  e->P.diag = mode;
+  return RAFT_OK;
+}
+
 int raft_debug_force_pass(raft_engine* e, int64_t group) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
   if (group >= int64_t(e->cfg.groups)) return fail(RAFT_EINVAL, "group out of range");

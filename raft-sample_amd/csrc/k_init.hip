@@ -311,4 +311,48 @@ hipError_t launch_digest(int R, const DevPlanes& P, int raft, uint64_t* per_grou
   return hipGetLastError();
 }
 
+// Stream probe (measurement only; no Raft state): the steady lean kernel's
+// byte mix and access shape on fresh buffers of n elements. Per element it
+// reads 2 + 16 + 2 B (gmeta, the 16-B record, the ring rotation) in one round
+// trip and writes the record 16 B, the heartbeat 4 B and R entries of 12 B as
+// whole ring rows (a wave's 64 elements x R contiguous per plane, streaming
+// stores to the slot `slot` of `kslots`) — 20 + 20 + 12 R B, 100 B at R = 5.
+// bench.py times it on the same GPU as the lean kernel, so the lean kernel's
+// rate can be read against what this device sustains for that pattern.
+template <int R>
+__global__ __launch_bounds__(256) void stream_probe_kernel(const uint16_t* a, SsRec* b, const uint16_t* c, int32_t* d,
+                                                           int32_t* rt, int64_t* rv, uint32_t n, uint32_t slot,
+                                                           uint32_t kslots) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  SsRec s{0, 0, 0, 0};
+  uint32_t x = 0;
+  if (g < n) {
+    x = uint32_t(a[g]) ^ (uint32_t(c[g]) << 16);
+    s = b[g];
+  }
+  const int lane = int(threadIdx.x & 63u);
+  const uint64_t tb = (uint64_t(g >> 6) * kslots + slot) * 64u * R;
+  const int32_t v32 = s.term ^ int32_t(x);
+  const int64_t v64 = (int64_t(s.last) << 32) ^ int64_t(uint32_t(s.cl) + x);
+  const int vlo = int(uint32_t(uint64_t(v64))), vhi = int(uint32_t(uint64_t(v64) >> 32));
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int src = (k * 64 + lane) / R;
+    const int t = __shfl(v32, src), lo = __shfl(vlo, src), hi = __shfl(vhi, src);
+    __builtin_nontemporal_store(t, &rt[tb + uint64_t(k * 64 + lane)]);
+    __builtin_nontemporal_store(int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo)), &rv[tb + uint64_t(k * 64 + lane)]);
+  }
+  if (g < n) {
+    b[g] = SsRec{s.last + 1, s.term, s.cl + 1, s.cf + 1};
+    d[g] = s.term + int32_t(slot);
+  }
+}
+
+hipError_t launch_stream_probe(int R, const uint16_t* a, SsRec* b, const uint16_t* c, int32_t* d, int32_t* rt,
+                               int64_t* rv, uint32_t n, uint32_t slot, uint32_t kslots, hipStream_t s) {
+  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(stream_probe_kernel<RR>, grid_for(n), dim3(256), 0, s, a, b, c, d, rt, rv, n,
+                                        slot, kslots));
+  return hipGetLastError();
+}
+
 }  // namespace raftstep

@@ -122,5 +122,7 @@ hipError_t launch_window_tail(const DevPlanes& P, const uint32_t* work, uint32_t
 hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s,
                                const CallCheck* chk = nullptr);
 hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s);
+hipError_t launch_stream_probe(int R, const uint16_t* a, SsRec* b, const uint16_t* c, int32_t* d, int32_t* rt,
+                               int64_t* rv, uint32_t n, uint32_t slot, uint32_t kslots, hipStream_t s);
 
 }  // namespace raftstep

@@ -214,6 +214,9 @@ SIGNATURES = {
     "raft_diag_enable": (C.c_int, [P, C.c_int]),
     "raft_diag_read": (C.c_int, [P, P, C.c_uint32]),
     "raft_debug_force_pass": (C.c_int, [P, C.c_int64]),
+    "raft_debug_diag_mode": (C.c_int, [P, C.c_uint32]),
+    "raft_stream_probe": (C.c_int, [C.c_int, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(C.c_double),
+                                    C.POINTER(C.c_double)]),
     "raft_debug_group_words": (C.c_int, [P, C.c_uint64, P, C.c_uint32]),
 }
 

@@ -38,6 +38,15 @@ def _check(rc):
         raise RaftError(rc, load_library().raft_last_error().decode(errors="replace"))
 
 
+def stream_probe(device=0, replicas=5, elems=1 << 24, reps=10):
+    """The steady lean kernel's byte mix on fresh buffers (raft_stream_probe):
+    (us per pass, bytes per pass)."""
+    lib = load_library()
+    us, by = C.c_double(), C.c_double()
+    _check(lib.raft_stream_probe(int(device), int(replicas), int(elems), int(reps), C.byref(us), C.byref(by)))
+    return us.value, by.value
+
+
 def _ptr(a):
     return a.ctypes.data if a is not None and a.size else None
 
@@ -233,6 +242,11 @@ class Engine:
         names = ("meta", "giso", "hb", "ss_last", "ss_term", "ss_cl", "ss_cf", "lx_k", "lx_dl", "rot", "rota", "sb",
                  "rotb", "sb2")
         return dict(zip(names, list(buf)))
+
+    def debug_diag_mode(self, mode):
+        """Timing diagnostics (results wrong while non-zero; engine created with
+        debug_flags=abi.DEBUG_ALLOW_WRONG_RESULTS)."""
+        _check(self.lib.raft_debug_diag_mode(self.h, int(mode)))
 
     def debug_force_pass(self, group):
         """Test knob: the lean kernel passes `group` (-1: none) to the list kernel."""

@@ -1,9 +1,12 @@
-"""Timing-only diagnostics of the C4 lean kernel (results are WRONG in the
-diag modes; never a bench line): for each RAFTSTEP_DIAG_LEAN mode (0 = the
-product kernel; 4 = whole ring rows written, no holes; 8 = no stale-column
-writes; 12 = both) and pipeline on/off, the lean and list kernels' mean
-durations and the tick's wall time over TICKS ticks after the bench's settle
-and warm-up.
+"""Timing-only diagnostics of the C4 lean and list kernels (results are WRONG
+in the diag modes; never a bench line): for each diagnostic mode (0 = the
+product kernels; lean: 4 = whole ring rows written, no holes, 8 = no
+stale-column writes; list: 32 = staging alone, 64 = staging and write-back,
+128 = the per-group code alone, 256 = no list work, 512 = no entry copies or
+moves) and pipeline on/off, the lean and list kernels' mean durations and the
+tick's wall time over TICKS ticks. The mode is switched on after the bench's
+settle and warm-up ticks (raft_debug_diag_mode), so those run exactly and the
+measured ticks start from the benchmark's state.
     python tools/lean_diag.py [--workload C4] [--modes 0,4] [--pipeline 1,0]"""
 import argparse
 import json
@@ -27,7 +30,6 @@ R = wl.get("replicas", 5)
 out = []
 for pipe in a.pipeline.split(","):
     for mode in a.modes.split(","):
-        os.environ["RAFTSTEP_DIAG_LEAN"] = mode
         os.environ["RAFTSTEP_PIPELINE"] = pipe
         e = Engine(debug_flags=abi.DEBUG_ALLOW_WRONG_RESULTS,
                    **bench.engine_kwargs(wl, R, wl["groups"], 0, wl["ring_depth"], wl["entries"], wl["crc"]))
@@ -36,6 +38,7 @@ for pipe in a.pipeline.split(","):
         t = wl["settle"]
         e.tick(t, 5)
         t += 5
+        e.debug_diag_mode(int(mode))
         e.sync()
         t0 = time.perf_counter()
         e.tick(t, a.ticks)
@@ -53,4 +56,4 @@ for pipe in a.pipeline.split(","):
         out.append({"pipeline": pipe, "diag": mode, "tick_us": wall * 1e6, "lean_us": lms * 1e3 / max(ln, 1),
                     "list_us": lsm * 1e3 / max(lsn, 1)})
         print(json.dumps(out[-1]), flush=True)
-os.environ.pop("RAFTSTEP_DIAG_LEAN")
+
