@@ -473,7 +473,7 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     line["rank_local"] = {"ms_per_step": median(local_times) * 1e3 / steps,
                           "repeat_ms_per_step": [x * 1e3 / steps for x in local_times],
                           "lean_kernel_us_per_tick": avg_kernel_s * 1e6, "stat_allreduces": allreduces}
-    if world == 1 and not churn and not crc and E == 1 and not fused:
+    if world == 1 and not churn and not crc and E == 1 and not fused and hasattr(eng.lib, "raft_stream_probe"):
         # this device's sustained rate for the lean kernel's byte mix and access
         # shape at the same size (raft_stream_probe: fresh buffers, no Raft
         # state): the practical roofline of this kernel on this box

@@ -221,8 +221,15 @@ SIGNATURES = {
 }
 
 
+# measurement / diagnostics entry points added in round 5: an older build
+# loaded through RAFTSTEP_LIB (A/B runs) may lack them
+OPTIONAL = ("raft_debug_diag_mode", "raft_stream_probe")
+
+
 def bind(lib):
     for name, (res, args) in SIGNATURES.items():
+        if name in OPTIONAL and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
