@@ -565,7 +565,9 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   }
   A(reinterpret_cast<void**>(&e->wcount), WCOUNT_WORDS * 4);
   A(reinterpret_cast<void**>(&e->dctr), 64);
-  for (int q = 0; q < 3; ++q) A(reinterpret_cast<void**>(&e->blist[q]), NSHARD * scap * 4);
+  // (each list: the group ids, then the words the lean kernel read for them,
+  // raft_device.hpp LIST_WORDS: the list kernel stages those coalesced)
+  for (int q = 0; q < 3; ++q) A(reinterpret_cast<void**>(&e->blist[q]), NSHARD * scap * 4 * LIST_WORDS);
   A(reinterpret_cast<void**>(&e->P.glst), Gp);
   A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.log_value), R * K * Gp * 8);
@@ -600,6 +602,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->P.KP = uint32_t(K);
   e->P.kmask = uint32_t(K) - 1;
   e->P.crc_on = c.payload_crc;
+  e->P.rec_nt = Gp * 40 > (uint64_t(256) << 20) ? 1u : 0u;   // (raft_device.hpp DevPlanes::rec_nt)
   e->P.corrupt_p = c.corrupt_per_65536;
   if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
   if (const char* gk = getenv("RAFTSTEP_GENERAL")) e->lane_general = std::strcmp(gk, "lane") == 0;

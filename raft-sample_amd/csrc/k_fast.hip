@@ -308,9 +308,17 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   uint32_t wr = 0;      // replicas that append this tick's entries (leader + accepting followers)
   int w_term = 0, w_ph = 0;    // their term and the ring slot of the first entry
   uint64_t w_vb = 0;    // value stream base of this tick's entries
-  int cp_n = 0, cp_from = 0, cp_sb = 0, cp_sb2 = 0;   // RAFT: a returning stale leader's catch-up copy (ring writes)
-  int mv_n = 0, mv_d = 0, mv_rot = 0, mv_col = 0, mv_from = 0;   // RAFT: a stale leader's entries above a segment switch (moved)
-  uint32_t cp_cs = 0, cp_rot = 0, cp_rotb = 0;
+  // RAFT entry job of this lane (written by the whole wave below): a
+  // returning stale leader's catch-up (the primary's entries L0+1..Ll into
+  // its column) or a stale leader's entries above a ring segment switch (to
+  // the new segment's slots). Either is one leader's own client appends, one
+  // batch per client tick up to the present (a leader appends at every client
+  // tick, main.go:327-329, and a cut-off one too), so entry jb_from+j is its
+  // appender's global client entry jb_q0+j: the entries are regenerated from
+  // the trace RNG (value stream jb_kv, term jb_term) instead of read back.
+  int jb_n = 0, jb_from = 0, jb_term = 0, jb_sb = 0, jb_sb2 = 0;
+  uint32_t jb_col = 0, jb_rot = 0, jb_rotb = 0;   // destination column; ring words (rot | rota << 16, rotb)
+  uint64_t jb_q0 = 0, jb_kv = 0;
   uint32_t df = 0;      // diagnostics: lane class bits (P.dbg)
   bool stored = false;  // the group's rows may have been written (returned)
   // deferral-reason bits 11-15 only in a diagnostics build (make DIAG=1),
@@ -758,13 +766,18 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       if (!bail) {
         df |= (1u << 21) | (ls > L0 ? 1u << 22 : 0u);   // class: stale leader's return (its log truncated at L0)
         // the primary's entries after L0 (at most K): copied below by the whole wave
-        cp_n = Ll - L0;
-        cp_from = L0 + 1;
-        cp_cs = uint32_t(c) | (uint32_t(sr) << 4);
-        cp_rot = rot | (rota << 16);
-        cp_rotb = rotb;
-        cp_sb = sbo;
-        cp_sb2 = sb2;
+        // (entries L0+1..Ll: the primary's own appends since its election, the
+        // last one at the client tick before this one)
+        jb_n = Ll - L0;
+        jb_from = L0 + 1;
+        jb_col = uint32_t(sr);
+        jb_term = Lt;
+        jb_q0 = T.entries_before(T.tick) - uint64_t(jb_n);
+        jb_kv = sm64(key ^ ((uint64_t(ST_VALUE) << 32) | uint32_t(c)));
+        jb_rot = rot | (rota << 16);
+        jb_rotb = rotb;
+        jb_sb = sbo;
+        jb_sb2 = sb2;
         sr_dur = T.f_min + int(uint32_t(rng_k(key, uint32_t(sr), ST_TIMER_F, uint64_t(T.tick)) >> 32) %
                                uint32_t(T.f_span));
         const int nl = Ll + n;
@@ -1010,11 +1023,18 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             if (hi <= Ll && ok) {
               df |= 32u | ((sbo <= 1 || sbo <= lo - int(P.K) + 1) ? 0u : 1u << 25);   // (+ the previous segment stays live)
               if (stale && xtop > Ll) {   // the stale leader's entries Ll+1..xtop: slot (i-1+rot) -> (i-1+rot+d)
-                mv_n = xtop - Ll;
-                mv_from = Ll + 1;
-                mv_d = int(d);
-                mv_rot = rot;
-                mv_col = xi;
+                // (its entries above Ll: its own appends since it was cut off,
+                // the last ones this tick; every index uses the new rotation)
+                jb_n = xtop - Ll;
+                jb_from = Ll + 1;
+                jb_col = uint32_t(xi);
+                jb_term = x_term;
+                jb_q0 = T.entries_before(T.tick + 1) - uint64_t(jb_n);
+                jb_kv = sm64(key ^ ((uint64_t(ST_VALUE) << 32) | uint32_t(xi)));
+                jb_rot = uint32_t((rot + int(d)) & int(P.kmask));
+                jb_rotb = 0;
+                jb_sb = -2147483647 - 1;
+                jb_sb2 = -2147483647 - 1;
                 df |= 1u << 31;
               }
               GW.rotb() = uint16_t(rota);   // the three segments shift
@@ -1055,10 +1075,10 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     stored = !skip && !bail;
   }
   if (LIST && (P.diag & 128u)) {   // timing only (results wrong): the per-group code alone
-    wr = 0; cp_n = 0; mv_n = 0;
+    wr = 0; jb_n = 0;
   }
   if (LIST && (P.diag & 512u)) {   // timing only (results wrong): no entry copies or moves
-    cp_n = 0; mv_n = 0;
+    jb_n = 0;
   }
   // ---- this tick's log entries into the rings (all lanes of the wave) ----
   // Ring row of one slot = 64 lanes x R replicas, contiguous. The lanes of
@@ -1070,24 +1090,18 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   // entry. Every other writing lane stores its own R-contiguous segment.
   // s0: the global phase entries_before(tick) (groups rotated at their first
   // entry, init_steady) or the first writer's slot, whichever more lanes share.
-  // Entry copies (RAFT): a returning stale leader's catch-up (entries
-  // L0+1..Ll of the primary's column into its own, same slots) and a stale
-  // leader's entries above a segment switch (entry i of its column from slot
-  // (i-1+rot) to (i-1+rot+d), from the top down). The wave gathers every
-  // entry of all its lanes' jobs with loads issued together (CPS entries per
-  // lane and pass, in registers), then writes this tick's own entries, then
-  // scatters the gathered ones: one load round trip per pass for the whole
-  // wave, instead of a store->load chain per 64-entry step (vmcnt counts
-  // stores too). Within a pass every load completes before any store, so a
-  // move's overlapping source and destination slots are safe; across passes
-  // a move goes from the top down (entry i's destination is the source of
-  // entry i+d, read in the same or an earlier pass). Copy and move never
-  // meet in one group (a switch needs sr < 0).
+  // Entry jobs (RAFT, see jb_*): every entry of all the wave's jobs is
+  // spread over its lanes (CPS per lane and pass), regenerated from the trace
+  // RNG and stored after this tick's own entries — no ring reads (round 5:
+  // reading them back cost two scattered line fetches per entry, a quarter of
+  // C4's tick in a diagnostic run). A move's new slots never hold a live entry
+  // of its column (ring_switch_ok), and copy and move never meet in one group
+  // (a switch needs sr < 0).
   constexpr int CPS = 4;   // entries per lane and pass
   WPROF(wp1 = __builtin_amdgcn_s_memtime(); uint64_t wg = 0, wo = 0, wsc = 0;)
   int jn = 0, jpre = 0, jtot = 0;   // this lane's job size, exclusive wave prefix, wave total
   if constexpr (RAFT) {
-    jn = cp_n > 0 ? cp_n : mv_n;
+    jn = jb_n;
     jpre = jn;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {   // inclusive scan
@@ -1096,13 +1110,11 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     }
     jtot = __shfl(jpre, 63);
     jpre -= jn;
-    if (jtot && __ballot(mv_n > 0)) __threadfence_block();   // the stale leader's entries stored this tick (moved)
   }
   const int passes = RAFT ? (jtot + 64 * CPS - 1) / (64 * CPS) : 0;   // (wave-uniform)
   for (int pass_i = 0; pass_i < (passes > 0 ? passes : 1); ++pass_i) {
     int32_t ct[CPS];
     int64_t cv[CPS];
-    uint32_t cc[CPS];
     uint32_t cdst[CPS];      // destination element offset inside the ring (64-bit tile base below)
     uint64_t ctb[CPS];
     bool con[CPS];
@@ -1112,7 +1124,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       for (int k = 0; k < CPS; ++k) {
         const int e = pass_i * 64 * CPS + k * 64 + lane;
         con[k] = e < jtot;
-        ct[k] = 0; cv[k] = 0; cc[k] = 0; cdst[k] = 0; ctb[k] = 0;
+        ct[k] = 0; cv[k] = 0; cdst[k] = 0; ctb[k] = 0;
         // owner: the last lane whose prefix is <= e (its job holds entry e)
         int o = 0;
 #pragma unroll
@@ -1121,33 +1133,24 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         const int j = e - __shfl(jpre, o);
         // (every shuffle unconditional: a shuffle reading a lane that is off
         // in a divergent branch returns 0)
-        const int kcp = __shfl(cp_n, o);
-        const int cpf = __shfl(cp_from, o), mvf = __shfl(mv_from, o);
-        const int cnt = __shfl(jn, o);
+        const int from = __shfl(jb_from, o), term = __shfl(jb_term, o);
+        const uint32_t col = uint32_t(__shfl(int(jb_col), o));
         const uint32_t gg = uint32_t(__shfl(int(g), o));
-        const uint32_t cpr = uint32_t(__shfl(int(cp_rot), o)), mvr = uint32_t(__shfl(mv_rot, o));
-        const int from = kcp > 0 ? cpf : mvf;
-        const uint32_t rr = kcp > 0 ? cpr : mvr;
-        const uint32_t rb = uint32_t(__shfl(int(cp_rotb), o));
-        const int sb_ = __shfl(cp_sb, o), sb2_ = __shfl(cp_sb2, o), dd = __shfl(mv_d, o);
-        const uint32_t cs = uint32_t(__shfl(int(cp_cs), o)), mcol = uint32_t(__shfl(mv_col, o));
+        const uint32_t rr = uint32_t(__shfl(int(jb_rot), o)), rb = uint32_t(__shfl(int(jb_rotb), o));
+        const int sb_ = __shfl(jb_sb, o), sb2_ = __shfl(jb_sb2, o);
+        const uint64_t q0 = (uint64_t(uint32_t(__shfl(int(uint32_t(jb_q0 >> 32)), o))) << 32) |
+                            uint32_t(__shfl(int(uint32_t(jb_q0)), o));
+        const uint64_t kv = (uint64_t(uint32_t(__shfl(int(uint32_t(jb_kv >> 32)), o))) << 32) |
+                            uint32_t(__shfl(int(uint32_t(jb_kv)), o));
         if (con[k]) {
-          const uint64_t tb = ring_tile(gg, P.KP, R);
-          uint32_t osrc, odst;
-          if (kcp > 0) {   // catch-up: same slot, the primary's column into the stale leader's
-            const uint32_t o0 = ring_in_tile(gg, R, ring_slot(from + j, rr & 0xFFFFu, rr >> 16, rb, sb_, sb2_, P.kmask), 0u);
-            osrc = o0 + (cs & 15u);
-            odst = o0 + (cs >> 4);
-          } else {         // move: from the top down, same column
-            const int idx = from + cnt - 1 - j;
-            osrc = ring_in_tile(gg, R, uint32_t(idx - 1 + int(rr)) & P.kmask, mcol);
-            odst = ring_in_tile(gg, R, uint32_t(idx - 1 + int(rr) + dd) & P.kmask, mcol);
-          }
-          ct[k] = ring_ld(P.log_term + tb, osrc);
-          cv[k] = ring_ld(P.log_value + tb, osrc);
-          if constexpr (CRC) cc[k] = ring_ld(P.log_crc + tb, osrc);
-          cdst[k] = odst;
-          ctb[k] = tb;
+          // global client entry q: tick (q / E) * period, entry q mod E of that tick
+          const uint64_t q = q0 + uint64_t(j);
+          const uint64_t qt = T.entries == 1u ? q : q / T.entries;
+          const uint32_t qe = T.entries == 1u ? 0u : uint32_t(q - qt * T.entries);
+          ct[k] = term;
+          cv[k] = int64_t(sm64(sm64(kv ^ (qt * T.period)) ^ uint64_t(qe)) >> 1);
+          ctb[k] = ring_tile(gg, P.KP, R);
+          cdst[k] = ring_in_tile(gg, R, ring_slot(from + j, rr & 0xFFFFu, rr >> 16, rb, sb_, sb2_, P.kmask), col);
         }
       }
     }
@@ -1187,7 +1190,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         if (!con[k]) continue;
         ring_stx<LIST, int32_t, 3>(P.log_term + ctb[k], cdst[k], ct[k]);
         ring_stx<LIST, int64_t, 3>(P.log_value + ctb[k], cdst[k], cv[k]);
-        if constexpr (CRC) ring_stx<LIST, uint32_t, 3>(P.log_crc + ctb[k], cdst[k], cc[k]);
+        if constexpr (CRC)
+          ring_stx<LIST, uint32_t, 3>(P.log_crc + ctb[k], cdst[k], crc_value_final(tab, crc_term_state(tab, ct[k]), cv[k]));
       }
     }
     WPROF(wsc += __builtin_amdgcn_s_memtime() - wq2;)
@@ -1399,7 +1403,9 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
   for (uint32_t base = blockIdx.x * GPB; base < n; base += gridDim.x * GPB) {
     WPROF(const uint64_t wi0 = __builtin_amdgcn_s_memtime();)
     const uint32_t i = base + (t >> 6) * LIST_LANES + lane;
-    const uint32_t g = (lane < LIST_LANES && i < n) ? list[shard_locate(pre, P.scap, i)] : 0xFFFFFFFFu;
+    const bool in = lane < LIST_LANES && i < n;
+    const uint32_t slot = in ? shard_locate(pre, P.scap, i) : 0u;
+    const uint32_t g = in ? list[slot] : 0xFFFFFFFFu;
     const bool valid = g < P.G;
     sg[t] = g;
     // (each is a separate scattered line per group, all loaded in the same
@@ -1416,8 +1422,15 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     // entry, whatever its value) is written back
     LxRec lx0{-2147483647 - 1, -2147483647 - 1};
     if (valid) {
-      m0 = at(P.gmeta, g); r0 = at(P.grot, g); hb0 = at(P.hb, g); ss0 = P.gss[g];
-      ra0 = at(P.grota, g); rb0 = at(P.grotb, g); sb0 = at(P.gsb, g); sc0 = at(P.gsb2, g);
+      // gmeta, grot, gsb and gss from the list entry (the lean kernel's reads,
+      // LIST_WORDS: coalesced by slot), the other words from their planes
+      const uint64_t cap = uint64_t(NSHARD) * P.scap;
+      uint32_t* const lst = const_cast<uint32_t*>(list);
+      const uint32_t mr = list_mr(lst, cap)[slot];
+      m0 = uint16_t(mr); r0 = uint16_t(mr >> 16); ss0 = list_ss(lst, cap)[slot];
+      sb0 = P.KP > P.K ? list_sb(lst, cap)[slot] : at(P.gsb, g);
+      hb0 = at(P.hb, g);
+      ra0 = at(P.grota, g); rb0 = at(P.grotb, g); sc0 = at(P.gsb2, g);
       if (T.iso_p) gi0 = at(P.giso, g);
       if (uses_glx(m0)) lx0 = P.glx[g];
     }
@@ -1521,6 +1534,14 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
 // Per group it reads gmeta 2 B + gss 16 B + grot 2 B and writes gss 16 B,
 // hb 4 B and the entries (12·n·R B, +4·n·R with CRC32C) as whole ring rows
 // (a drifted group: its own R-contiguous segment, or a ring segment switch).
+// A/B hooks (round 5, interleaved A/Bs in profiles/r05/ab/): LEAN_HOIST_LX=1
+// reads glx / giso for every lane with gmeta instead of after it for the lanes
+// that use them (C4: neutral, 9 B more per group); hoisting HWX's
+// high-water-mark row the same way was 35% slower (C4's per-group words then
+// no longer stay in the Infinity Cache)
+#ifndef RAFTSTEP_LEAN_HOIST_LX
+#define RAFTSTEP_LEAN_HOIST_LX 0
+#endif
 template <int R, bool CRC, int SEM>
 __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, unsigned long long* stats, uint32_t* list,
                                                         uint32_t* count, int lflags, uint32_t gofs, uint32_t* zc) {
@@ -1550,6 +1571,9 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   uint32_t act = 0, starting = 0, im = 0;
   if (T.iso_p) im = iso_windows<R>(key, T, &act, &starting);
   bool held = false;
+  uint32_t p_mr = 0;            // a passed group's words as read here, for its list entry
+  int32_t p_sb = 0;
+  SsRec p_ss{0, 0, 0, 0};
   if (g < P.G) {
     // gmeta and, speculatively, the record, the ring rotation and the segment
     // boundary go out together: one round trip instead of two for the groups
@@ -1559,6 +1583,19 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     const SsRec s = P.gss[g];
     const int rot = at(P.grot, g);
     const int sb0 = P.KP > P.K ? at(P.gsb, g) : 0;
+    p_mr = uint32_t(meta) | (uint32_t(rot) << 16);
+    p_sb = sb0;
+    p_ss = s;
+    // RAFT under isolation churn, glx (and giso while a window is active) in
+    // the same round trip: an LXS or SXS lane is in most waves of such a tick,
+    // and each such wave waited a second round trip for them
+    const bool hl = RAFT && RAFTSTEP_LEAN_HOIST_LX && T.iso_p;
+    LxRec gx_h{0, 0};
+    uint32_t gi_h = 0;
+    if (hl) {
+      gx_h = P.glx[g];
+      if (act) gi_h = at(P.giso, g);
+    }
     // pipelined tick: a group the last list kernel carries through this tick
     // too is left alone (its state is being written beside this kernel); the
     // mark is cleared with the kernel's other stores at the end (a store here
@@ -1571,8 +1608,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     df |= (!skip && g == P.dbg_pass) ? 1u << 24 : 0u;
     df |= skip ? 1u : 0u;
     if (take) {
-      const LxRec gx = (RAFT && uses_glx(meta)) ? P.glx[g] : LxRec{0, 0};
-      uint32_t gi = (RAFT && T.iso_p && act && uses_glx(meta)) ? uint32_t(at(P.giso, g)) : 0u;
+      const LxRec gx = (RAFT && uses_glx(meta)) ? (hl ? gx_h : P.glx[g]) : LxRec{0, 0};
+      uint32_t gi = (RAFT && T.iso_p && act && uses_glx(meta)) ? (hl ? gi_h : uint32_t(at(P.giso, g))) : 0u;
       int hwmx = 0;   // RAFT HWX: the highest high-water mark (the hwm plane)
       if (RAFT && (meta & M_HWX)) {
         int hw[R];
@@ -1718,8 +1755,15 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
                    : 0u;
       }
       if (take) {
-        if (nl != L || cl2 != s.cl || cf2 != s.cf) P.gss[g] = SsRec{nl, s.term, cl2, cf2};
-        if (hbw) at(P.hb, g) = T.now;                   // timer.Reset(d) of every follower
+        if (P.rec_nt) {   // (per-group words beyond the Infinity Cache: streamed, DevPlanes::rec_nt)
+          typedef int32_t i4 __attribute__((ext_vector_type(4)));
+          if (nl != L || cl2 != s.cl || cf2 != s.cf)
+            __builtin_nontemporal_store(i4{nl, s.term, cl2, cf2}, reinterpret_cast<i4*>(&P.gss[g]));
+          if (hbw) __builtin_nontemporal_store(int32_t(T.now), &P.hb[g]);   // timer.Reset(d) of every follower
+        } else {
+          if (nl != L || cl2 != s.cl || cf2 != s.cf) P.gss[g] = SsRec{nl, s.term, cl2, cf2};
+          if (hbw) at(P.hb, g) = T.now;                   // timer.Reset(d) of every follower
+        }
         if (RAFT && lxs) P.glx[g] = LxRec{gx.k + n, gx.dl};   // (SXS: unchanged, both logs grow by n)
         if (hwx_clear) at(P.gmeta, g) = uint16_t(meta & ~M_HWX);
         if (sw_d) {   // the new segment starts at this tick's first entry
@@ -1854,6 +1898,11 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     uint32_t off = k * P.scap + wbase + uint32_t(__popcll(bm & ((1ull << lane) - 1ull)));
     for (int w = 0; w < wave; ++w) off += wn[w];
     list[off] = g;
+    // the words read above, for the list kernel's coalesced staging (LIST_WORDS)
+    const uint64_t cap = uint64_t(NSHARD) * P.scap;
+    list_mr(list, cap)[off] = p_mr;
+    list_sb(list, cap)[off] = p_sb;
+    list_ss(list, cap)[off] = p_ss;
     if (lflags & 2) at(P.glst, g) = uint8_t(1);   // the list kernel carries it through the next tick too
   }
   if (stats) {
@@ -1995,7 +2044,9 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
       if (b1) atomicAdd(&P.dbg[23], (unsigned long long)__popcll(b1));
     }
   }
-  // passed on (the skip's proof violated): one atomic per passing lane
+  // passed on (the skip's proof violated): one atomic per passing lane (the
+  // id only: no list kernel runs in a list-skipping call, and the end-of-call
+  // check turns any such entry into RAFT_EINTERNAL before one could)
   if (pass) {
     const uint32_t k = blockIdx.x & uint32_t(NSHARD - 1);
     list[k * P.scap + atomicAdd(&count[k * SHARD_STRIDE], 1u)] = g;

@@ -139,6 +139,11 @@ struct DevPlanes {
   uint32_t scap;       // capacity of one shard of a sharded group list (see below)
   uint8_t* glst;       // [Gp] two-step list marks: 1 = passed by the last lean kernel to a list kernel that
                        // also runs this tick for it (the lean kernel leaves the group alone and clears the mark)
+  // the lean kernel's record / heartbeat stores are non-temporal when the
+  // per-group words cannot stay in the 256 MiB Infinity Cache between ticks
+  // anyway (engine.cpp: 40 B x Gp above it; round 5, C2 at 2^24: +2%);
+  // below that, plain stores keep them resident (C2 at 2^20: nt 3% slower)
+  uint32_t rec_nt;
   uint32_t diag;       // timing-only diagnostics (RAFTSTEP_DIAG_LEAN; results are wrong when set): 1 = drifted
                        // lanes of the lean kernel skip their ring writes, 2 = they write the wave's common row
                        // (list kernel: 32 = staging alone, 64 = no tick, 128 = no ring writes / copies)
@@ -192,6 +197,16 @@ __device__ __forceinline__ uint32_t shard_locate(const uint32_t* pre, uint32_t s
     if (pre[k + step] <= i) k += step;
   return k * scap + (i - pre[k]);
 }
+
+// Two-pass list entry: the list of cap = NSHARD * scap slots holds the group
+// ids, then, per slot, the words the lean kernel already read for that group
+// (gmeta | grot << 16, the segment boundary gsb, the 16-B record gss): the
+// list kernel stages them with loads coalesced by list slot instead of three
+// or four scattered lines per group (round 5).
+constexpr uint32_t LIST_WORDS = 8;   // [cap] ids, [cap] meta|rot, [cap] gsb, [cap] pad, [cap] SsRec (4 words)
+__device__ __forceinline__ uint32_t* list_mr(uint32_t* list, uint64_t cap) { return list + cap; }
+__device__ __forceinline__ int32_t* list_sb(uint32_t* list, uint64_t cap) { return reinterpret_cast<int32_t*>(list + 2 * cap); }
+__device__ __forceinline__ SsRec* list_ss(uint32_t* list, uint64_t cap) { return reinterpret_cast<SsRec*>(list + 4 * cap); }
 __device__ __forceinline__ void shard_zero(uint32_t* cnt) {   // block 0, threads 0..NSHARD-1 (cnt null: nothing)
   if (cnt && blockIdx.x == 0 && threadIdx.x < uint32_t(NSHARD)) cnt[threadIdx.x * SHARD_STRIDE] = 0;
 }

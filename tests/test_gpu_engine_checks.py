@@ -203,3 +203,29 @@ def test_split_steady_tick_matches_oracle(monkeypatch, split):
     H.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")
     c = e.diag_read()
     assert c["ticks_list_skipped"] >= 40, c
+
+
+def test_debug_diag_mode_needs_the_wrong_results_flag():
+    """raft_debug_diag_mode (timing diagnostics, results wrong) is refused
+    unless the engine was created with RAFT_DEBUG_ALLOW_WRONG_RESULTS; mode 0
+    (exact) is always accepted."""
+    e = Engine(**KW)
+    with pytest.raises(RaftError) as ei:
+        e.debug_diag_mode(512)
+    assert ei.value.code == -22
+    e.debug_diag_mode(0)
+    d = Engine(debug_flags=abi.DEBUG_ALLOW_WRONG_RESULTS, **KW)
+    d.debug_diag_mode(512)
+    d.debug_diag_mode(0)
+
+
+def test_stream_probe_reports_its_bytes():
+    """raft_stream_probe: the lean kernel's byte mix on fresh buffers (bench.py
+    prices the lean kernel against it): 40 + 12 R bytes per element."""
+    from raftstep import stream_probe
+    us, by = stream_probe(0, 5, 1 << 20, 3)
+    assert by == (1 << 20) * 100 and 0 < us < 1e5
+    us7, by7 = stream_probe(0, 7, 1000, 2)
+    assert by7 == 1024 * 124 and us7 > 0
+    with pytest.raises(RaftError):
+        stream_probe(0, 9, 1 << 20, 1)
