@@ -197,6 +197,11 @@ struct raft_engine {
   // statistics reduce and at the end of the call. RAFTSTEP_SPLIT_STEADY=0:
   // one launch per tick (exact either way: tests/test_gpu_engine_checks.py).
   int split_steady = 1;
+  // Steady kernel (RAFTSTEP_STEADY): 0 runs the list-skipping one-tick calls
+  // on the lean kernel, 1 / 2 on tick_steady_kernel with that many groups per
+  // lane (k_fast.hip; payload CRC keeps the lean kernel). Exact either way
+  // (tests/test_gpu_engine_checks.py).
+  int steady_gpl = 0;
   hipStream_t half_stream = nullptr;
   hipEvent_t ev_half[2] = {nullptr, nullptr};   // engine -> half stream, half stream -> engine
   hipEvent_t ev_lean[2] = {nullptr, nullptr};   // engine stream -> list_stream (list(t) after lean(t))
@@ -612,6 +617,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
   e->P.diag = diag_lean;
   if (const char* sp = getenv("RAFTSTEP_SPLIT_STEADY")) e->split_steady = atoi(sp) != 0;
+  if (const char* sk = getenv("RAFTSTEP_STEADY")) e->steady_gpl = std::min(2, std::max(0, atoi(sk)));
   // (the depths the oracle tests cover: 0..3, tests/test_gpu_pipeline.py)
   if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = std::min(3, std::max(0, atoi(og)));
   if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = atoi(pp) != 0;
@@ -1117,6 +1123,8 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   const uint64_t Gs = e->cfg.groups;
   const uint64_t half = (Gs / 2) & ~uint64_t(255);
   const bool split = two && skip_list && fuse == 1 && e->split_steady && half >= 65536 && Gs - half >= 65536;
+  // the list-skipping one-tick form on tick_steady_kernel (raft_engine::steady_gpl)
+  const bool steady_k = two && skip_list && fuse == 1 && e->steady_gpl > 0 && !e->cfg.payload_crc;
   bool half_busy = false;   // the half stream has work the engine stream has not joined
   auto join_half = [&]() -> int {
     if (!half_busy) return RAFT_OK;
@@ -1235,12 +1243,22 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
         if (!c || !d) return fail(RAFT_EHIP, "hipEventCreate failed");
       }
       const uint32_t L = e->lpar % 3;
-      if (split) {   // the two halves on two streams (the span's stop event is recorded after the join)
-        HIPCHK(launch_tick_lean(e->R, int(e->cfg.semantics), e->P, T, st, e->blist[L], lcount(e, L), 0, e->stream, a,
+      const int sem = int(e->cfg.semantics);
+      if (split && steady_k) {   // the two halves on two streams (the span's stop event is recorded after the join)
+        HIPCHK(launch_tick_steady(e->R, sem, e->steady_gpl, e->P, T, st, e->blist[L], lcount(e, L), e->stream, a,
+                                  nullptr, 0, half));
+        HIPCHK(launch_tick_steady(e->R, sem, e->steady_gpl, e->P, T, st, e->blist[L], lcount(e, L), e->half_stream,
+                                  nullptr, nullptr, half, Gs - half));
+        half_busy = true;
+      } else if (split) {
+        HIPCHK(launch_tick_lean(e->R, sem, e->P, T, st, e->blist[L], lcount(e, L), 0, e->stream, a,
                                 nullptr, 0, half));
-        HIPCHK(launch_tick_lean(e->R, int(e->cfg.semantics), e->P, T, st, e->blist[L], lcount(e, L), 0, e->half_stream,
+        HIPCHK(launch_tick_lean(e->R, sem, e->P, T, st, e->blist[L], lcount(e, L), 0, e->half_stream,
                                 nullptr, nullptr, half, Gs - half));
         half_busy = true;
+      } else if (steady_k) {
+        HIPCHK(launch_tick_steady(e->R, sem, e->steady_gpl, e->P, T, st, e->blist[L], lcount(e, L), e->stream, a, b, 0,
+                                  Gs));
       } else {
         HIPCHK(launch_tick_two_pass(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar % NWORK],
                                     e->work_tick[e->wpar % NWORK], cnt, e->blist[L], lcount(e, L),

@@ -1922,6 +1922,133 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   }
 }
 
+// Steady tick (the steady-state list skip, engine.cpp; one tick per launch):
+// every live group is proven compressed (SSYNC), in the global ring phase and
+// takeable, and no isolation or corruption is configured, so the tick of
+// every group is the lean kernel's normal class — client append of n entries
+// (main.go:327-329), one accepted AppendEntries per follower (341-372 ->
+// 121-156), the responses (375-378), the commit rule (381-391), one heartbeat
+// time for every follower — and nothing else needs a branch. Each lane runs
+// GPL groups (GPL consecutive 64-group tiles per wave) with all their loads
+// issued in one round trip, so a wave keeps GPL times the lean kernel's bytes
+// in flight. Per group it reads gmeta 2 B + gss 16 B + grot 2 B and writes
+// gss 16 B, hb 4 B and 12 n R B of entries as whole ring rows: the lean
+// kernel's bytes. A group that is not takeable (which the skip's proof
+// excludes) is passed to the list, which the end-of-call check turns into
+// RAFT_EINTERNAL.
+template <int R, int SEM, int GPL>
+__global__ __launch_bounds__(256) void tick_steady_kernel(DevPlanes P, Trace T, unsigned long long* stats,
+                                                          uint32_t* list, uint32_t* count, uint32_t gofs,
+                                                          uint32_t ng) {
+  constexpr bool RAFT = SEM == SEM_RAFT;
+  const int lane = int(threadIdx.x & 63u);
+  const uint32_t wv = blockIdx.x * 4u + (threadIdx.x >> 6);          // this wave of the launch
+  const uint32_t g0 = gofs + wv * 64u * GPL;                          // its first group (a tile boundary)
+  const uint32_t gend = gofs + ng;
+  const int n = int(T.client_entries());
+  const int ph = int(T.entries_before(T.tick) & P.kmask);
+  int meta[GPL], rot[GPL];
+  SsRec s[GPL];
+#pragma unroll
+  for (int q = 0; q < GPL; ++q) {   // every load of the lane in one round trip
+    const uint32_t g = g0 + uint32_t(q * 64 + lane);
+    meta[q] = 0xFFFF; rot[q] = 0; s[q] = SsRec{0, 0, 0, 0};
+    if (g < gend) { meta[q] = at(P.gmeta, g); s[q] = P.gss[g]; rot[q] = at(P.grot, g); }
+  }
+  int k_src[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) k_src[k] = (k * 64 + lane) / R;
+  int committed = 0, taken = 0, passed = 0;
+#pragma unroll
+  for (int q = 0; q < GPL; ++q) {
+    const uint32_t g = g0 + uint32_t(q * 64 + lane);
+    const bool valid = g < gend;
+    const int mt = meta[q], c = mt & 0xF;
+    const bool skip = !valid || (mt & M_DEFER) || ((mt >> 4) & 0xF);
+    const SsRec x = s[q];
+    const int L = x.last;
+    // (as the fused kernel: SSYNC, no LXS / SXS / HWX, in phase, within range)
+    const bool take = !skip && (mt & M_SSYNC) && c < R && !uses_glx(mt) && !(RAFT && (mt & M_HWX)) &&
+                      g != P.dbg_pass && L > 0 && int64_t(L) + n <= I32MAX && n < int(P.K) && x.cl <= L + n &&
+                      (n == 0 || ((L + rot[q]) & int(P.kmask)) == ph);
+    const bool pass = !skip && !take;
+    int nl = L, cl2 = x.cl, cf2 = x.cf;
+    if (take) {
+      nl = L + n;
+      if (RAFT ? nl > x.cl : (2 * (R - 1) > R && nl > x.cl)) cl2 = nl;
+      cf2 = x.cl > x.cf ? x.cl : x.cf;
+      committed += cl2 - x.cl;
+      ++taken;
+    }
+    if (n && __ballot(take)) {   // this tick's entries as whole ring rows of this tile
+      const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g0 + uint32_t(q * 64)), P.KP, R);
+      int32_t* const rt = P.log_term + tb;
+      int64_t* const rv = P.log_value + tb;
+      const uint64_t vb = take ? rng_k(group_key(T.seed, P.gbase + g), uint32_t(c), ST_VALUE, uint64_t(T.tick)) : 0ull;
+      int k_term[R];
+      bool k_on[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        k_term[k] = __shfl(x.term, k_src[k]);
+        k_on[k] = __shfl(take ? 1 : 0, k_src[k]) != 0;
+      }
+      for (int e = 0; e < n; ++e) {
+        const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+        const uint32_t row = uint32_t((ph + e) & int(P.kmask)) * 64u * R;
+        const int vlo = int(uint32_t(uint64_t(v))), vhi = int(uint32_t(uint64_t(v) >> 32));
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const int lo = __shfl(vlo, k_src[k]), hi = __shfl(vhi, k_src[k]);
+          if (k_on[k]) {
+            const uint32_t o = row + uint32_t(k * 64 + lane);
+            ring_st(rt, o, k_term[k]);
+            ring_st(rv, o, int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo)));
+          }
+        }
+      }
+    }
+    if (take) {
+      if (P.rec_nt) {   // (DevPlanes::rec_nt)
+        typedef int32_t i4 __attribute__((ext_vector_type(4)));
+        if (nl != L || cl2 != x.cl || cf2 != x.cf)
+          __builtin_nontemporal_store(i4{nl, x.term, cl2, cf2}, reinterpret_cast<i4*>(&P.gss[g]));
+        __builtin_nontemporal_store(int32_t(T.now), &P.hb[g]);   // timer.Reset(d) of every follower
+      } else {
+        if (nl != L || cl2 != x.cl || cf2 != x.cf) P.gss[g] = SsRec{nl, x.term, cl2, cf2};
+        at(P.hb, g) = T.now;   // timer.Reset(d) of every follower
+      }
+    }
+    if (pass) {   // (the skip's proof violated: the id only, one atomic per lane; see tick_fused_kernel)
+      const uint32_t k = shard_home(g);
+      list[k * P.scap + atomicAdd(&count[k * SHARD_STRIDE], 1u)] = g;
+      ++passed;
+    }
+  }
+  if (P.dbg) {   // diagnostics (lean kernel counters): lanes, compressed ticks taken, passed on
+    const long long tk = wave_sum(taken), ps = wave_sum(passed);
+    if (lane == 0) {
+      uint32_t nv = 0;
+#pragma unroll
+      for (int q = 0; q < GPL; ++q) nv += (g0 + uint32_t(q * 64) < gend) ? min(gend - (g0 + uint32_t(q * 64)), 64u) : 0u;
+      atomicAdd(&P.dbg[10], (unsigned long long)nv);
+      if (tk) atomicAdd(&P.dbg[18], (unsigned long long)tk);
+      if (ps) atomicAdd(&P.dbg[23], (unsigned long long)ps);
+    }
+  }
+  if (stats) {
+    const int t = taken;
+    if constexpr (RAFT) {
+      const int v[5] = {committed, t * (R - 1), 0, t, 0};
+      const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
+      block_stats<5>(v, idx, stats);
+    } else {
+      const int v[4] = {committed, t * (R - 1), 0, t};
+      const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
+      block_stats<4>(v, idx, stats);
+    }
+  }
+}
+
 // Fused steady ticks (the steady-state list skip, engine.cpp): every live
 // group is proven compressed and takeable and no isolation or corruption is
 // configured, so the lean kernel's normal class is the whole tick of every
@@ -2164,6 +2291,25 @@ hipError_t launch_tick_lean(int R, int sem, const DevPlanes& P, const Trace& T, 
   }
   if (crc) { RAFT_LEAN(true); } else { RAFT_LEAN(false); }
 #undef RAFT_LEAN
+  return hipGetLastError();
+}
+hipError_t launch_tick_steady(int R, int sem, int gpl, const DevPlanes& P, const Trace& T, unsigned long long* stats,
+                              uint32_t* list, uint32_t* count, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop,
+                              uint64_t g0, uint64_t ng) {
+  if (!ng) return hipSuccess;
+  const dim3 grid(unsigned((ng + 256u * uint64_t(gpl) - 1) / (256u * uint64_t(gpl))));
+#define RAFT_STEADY(GPL_)                                                                                       \
+  if (sem == SEM_RAFT) {                                                                                         \
+    RAFT_DISPATCH_R(R, hipExtLaunchKernelGGL((tick_steady_kernel<RR, SEM_RAFT, GPL_>), grid, dim3(256), 0, s,   \
+                                             ev_start, ev_stop, 0, P, T, stats, list, count, uint32_t(g0),       \
+                                             uint32_t(ng)))                                                      \
+  } else {                                                                                                       \
+    RAFT_DISPATCH_R(R, hipExtLaunchKernelGGL((tick_steady_kernel<RR, SEM_REF, GPL_>), grid, dim3(256), 0, s,    \
+                                             ev_start, ev_stop, 0, P, T, stats, list, count, uint32_t(g0),       \
+                                             uint32_t(ng)))                                                      \
+  }
+  if (gpl == 2) { RAFT_STEADY(2); } else { RAFT_STEADY(1); }
+#undef RAFT_STEADY
   return hipGetLastError();
 }
 hipError_t launch_tick_list(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,

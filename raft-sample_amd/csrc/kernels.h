@@ -72,6 +72,11 @@ hipError_t launch_tick_fused(int R, int sem, const DevPlanes& P, const Trace& T,
 hipError_t launch_tick_lean(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
                             uint32_t* count, int lflags, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop,
                             uint64_t g0 = 0, uint64_t ng = ~0ull, uint32_t* zero_count = nullptr);
+// Steady tick (list skipped, no payload CRC): tick_steady_kernel, gpl groups
+// per lane (1 or 2), over groups [g0, g0 + ng) (g0 a multiple of 64)
+hipError_t launch_tick_steady(int R, int sem, int gpl, const DevPlanes& P, const Trace& T, unsigned long long* stats,
+                              uint32_t* list, uint32_t* count, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop,
+                              uint64_t g0, uint64_t ng);
 hipError_t launch_tick_list(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                             int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
                             uint32_t* next_count, const ListNext* next, hipStream_t s, hipEvent_t ev_start,
