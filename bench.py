@@ -66,8 +66,8 @@ ENV_KNOBS = {
     "RAFTSTEP_OVERLAP_GENERAL": "exact: 0 = general kernel in line, d = overlapping d ticks (tests/test_gpu_pipeline.py)",
     "RAFTSTEP_SPLIT_STEADY": "exact: 0 = one launch per steady tick instead of two halves on two streams "
                              "(tests/test_gpu_engine_checks.py)",
-    "RAFTSTEP_STEADY": "exact: list-skipping one-tick calls on tick_steady_kernel with 1 / 2 groups per lane, "
-                       "0 = the lean kernel (tests/test_gpu_engine_checks.py)",
+    "RAFTSTEP_VX": "exact: 0 = no virtual log suffixes (C4's stale leaders' entries stored and copied back at "
+                   "their return; tests/test_gpu_fullsize.py, test_gpu_pipeline.py)",
     "RAFTSTEP_DEBUG_WORK": "exact: prints worklist sizes, synchronises (in-line form)",
     "RAFTSTEP_DEBUG_PIPE": "exact: prints the pipeline choice",
     "RAFTSTEP_DEBUG_FAST": "exact: prints class counters after every call (synchronising)",

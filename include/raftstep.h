@@ -345,6 +345,9 @@ enum raft_diag_counter {
   RAFT_DIAG_LEAN_FORCED = 24,         /* groups passed by raft_debug_force_pass */
   RAFT_DIAG_LEAN_SXS = 25,            /* new leader replicating while the stale one is cut off (SXS) taken */
   RAFT_DIAG_LEAN_SXS_STALE_IN_ROW = 26,/* ... with the stale leader's entry inside the common ring row */
+  RAFT_DIAG_LEAN_SXS_VX = 27,         /* SXS ticks whose stale leader holds a virtual suffix (whole rows) */
+  RAFT_DIAG_LIST_RETURN_VX = 28,      /* stale leaders' returns with a virtual suffix (no entry copy) */
+  RAFT_DIAG_LIST_LXS_VX = 29,         /* LXS entered with a virtual suffix */
   RAFT_DIAG_LEAN_SWITCH = 5,          /* ring segment switches */
   /* full fast-path body (list kernel / one-pass kernel): 32 + bit */
   RAFT_DIAG_LIST_LANES = 42,          /* groups looked at */

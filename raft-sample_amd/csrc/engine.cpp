@@ -154,6 +154,11 @@ struct raft_engine {
   // statistics starts launching, cleared when it has issued every reduce; a
   // call that fails in between leaves it set and the next call zeroes them
   uint32_t hist_dirty = 0;
+  // VX (raft_device.hpp M_VX): groups may hold virtual suffixes (P.vx and a
+  // call has run since the last flush); they are defined by the client ticks
+  // before vx_tick (-1: unknown, a call failed mid-way: the engine is poisoned)
+  bool vx_live = false;
+  int64_t vx_tick = 0;
   int force_general = 0;        // debug: route every group through the general kernel
   int lane_general = 0;         // RAFTSTEP_GENERAL=lane: one-lane-per-group general kernel (A/B) instead of the segment one
   uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
@@ -197,11 +202,6 @@ struct raft_engine {
   // statistics reduce and at the end of the call. RAFTSTEP_SPLIT_STEADY=0:
   // one launch per tick (exact either way: tests/test_gpu_engine_checks.py).
   int split_steady = 1;
-  // Steady kernel (RAFTSTEP_STEADY): 0 runs the list-skipping one-tick calls
-  // on the lean kernel, 1 / 2 on tick_steady_kernel with that many groups per
-  // lane (k_fast.hip; payload CRC keeps the lean kernel). Exact either way
-  // (tests/test_gpu_engine_checks.py).
-  int steady_gpl = 0;
   hipStream_t half_stream = nullptr;
   hipEvent_t ev_half[2] = {nullptr, nullptr};   // engine -> half stream, half stream -> engine
   hipEvent_t ev_lean[2] = {nullptr, nullptr};   // engine stream -> list_stream (list(t) after lean(t))
@@ -355,7 +355,10 @@ int settle_check(raft_engine* e) {
 
 // A call that replaces the state starts by dropping the list-skip proof (the
 // conservative direction, whatever happens next) ...
-void state_replacing(raft_engine* e) { e->steady_origin = e->steady_ok = false; }
+void state_replacing(raft_engine* e) {
+  e->steady_origin = e->steady_ok = false;
+  e->vx_live = false;   // (the state is being replaced: no suffix survives)
+}
 // ... and only once the new state's launches / copies have gone through
 // successfully drops any poison and a still-pending end-of-call check (both
 // describe the old state). A call that fails on the way leaves them as they
@@ -364,6 +367,26 @@ void state_replaced(raft_engine* e) {
   e->pend_chk = false;
   e->poisoned = false;
   e->poison_msg.clear();
+}
+
+// VX: every group's virtual suffix into its ring, before anything but the
+// tick path reads or changes the state (host views, digests, handler batches)
+// or a call starts at a tick other than the one after the last call.
+int vx_flush(raft_engine* e) {
+  if (!e->vx_live) return RAFT_OK;
+  if (e->vx_tick < 0) {
+    e->poisoned = true;
+    e->steady_ok = false;
+    e->poison_msg = "a failed raft_tick call left virtual log suffixes undefined (state must be replaced)";
+    return fail(RAFT_EINTERNAL, "%s", e->poison_msg.c_str());
+  }
+  const uint64_t per = e->cfg.client_period, E = e->cfg.entries_per_tick;
+  const int64_t t = e->vx_tick;
+  const uint64_t Qb = (per && t > 0) ? uint64_t((t + int64_t(per) - 1) / int64_t(per)) * E : 0u;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  HIPCHK(launch_vx_flush(e->R, e->P, Qb, uint32_t(E), uint32_t(per), e->cfg.seed, e->stream));
+  e->vx_live = false;
+  return RAFT_OK;
 }
 
 hipEvent_t next_event(raft_engine* e) {
@@ -608,6 +631,9 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->P.kmask = uint32_t(K) - 1;
   e->P.crc_on = c.payload_crc;
   e->P.rec_nt = Gp * 40 > (uint64_t(256) << 20) ? 1u : 0u;   // (raft_device.hpp DevPlanes::rec_nt)
+  // virtual suffixes (M_VX): RAFT leader isolation without payload CRC; RAFTSTEP_VX=0 turns them off
+  e->P.vx = (raft && c.isolate_per_65536 && c.isolate_leader && !c.payload_crc) ? 1u : 0u;
+  if (const char* vx = getenv("RAFTSTEP_VX"); vx && atoi(vx) == 0) e->P.vx = 0;
   e->P.corrupt_p = c.corrupt_per_65536;
   if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
   if (const char* gk = getenv("RAFTSTEP_GENERAL")) e->lane_general = std::strcmp(gk, "lane") == 0;
@@ -617,7 +643,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   if (const char* tp = getenv("RAFTSTEP_TWO_PASS")) e->two_pass = atoi(tp) != 0;
   e->P.diag = diag_lean;
   if (const char* sp = getenv("RAFTSTEP_SPLIT_STEADY")) e->split_steady = atoi(sp) != 0;
-  if (const char* sk = getenv("RAFTSTEP_STEADY")) e->steady_gpl = std::min(2, std::max(0, atoi(sk)));
+
   // (the depths the oracle tests cover: 0..3, tests/test_gpu_pipeline.py)
   if (const char* og = getenv("RAFTSTEP_OVERLAP_GENERAL")) e->overlap_general = std::min(3, std::max(0, atoi(og)));
   if (const char* pp = getenv("RAFTSTEP_PIPELINE")) e->pipeline = atoi(pp) != 0;
@@ -815,7 +841,7 @@ int store_range(raft_engine* e, uint64_t g0, uint64_t n, raft_state_view* v) {
     const bool msync = meta[g] & M_MSYNC;
     const LxRec lxg = (meta[g] & M_SSYNC) ? glx[g] : LxRec{0, 0};
     const uint64_t gt = g0 + g - t0 * 64;   // group index inside the copied ring tiles
-    if (v->fault) v->fault[g] = uint8_t((meta[g] >> 4) & 0xF);
+    if (v->fault) v->fault[g] = uint8_t((meta[g] >> 4) & 7);
     if (v->iso_victim) v->iso_victim[g] = giso[g];
     for (uint64_t r = 0; r < R; ++r) {
       const uint64_t d = g * R + r, c = g * R + r;   // per-replica planes are group-major (rix)
@@ -884,6 +910,7 @@ extern "C" {
 int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!e || !v) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
+  if (int rc = vx_flush(e)) return rc;
   return store_range(e, 0, e->cfg.groups, v);
 }
 
@@ -893,6 +920,7 @@ int raft_store_state_range(raft_engine* e, uint64_t first_group, uint64_t n_grou
     return fail(RAFT_ERANGE, "groups [%llu, +%llu) outside the engine's %llu", (unsigned long long)first_group,
                 (unsigned long long)n_groups, (unsigned long long)e->cfg.groups);
   if (int rc = settle_check(e)) return rc;
+  if (int rc = vx_flush(e)) return rc;
   return store_range(e, first_group, n_groups, v);
 }
 
@@ -1098,7 +1126,14 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   // (the per-tick records need nticks slots; the check records exist at any capacity)
   if (int rc = ensure_hist(e, stats ? std::max<uint32_t>(nticks, 1) : 1)) return rc;
   if (!nticks) return RAFT_OK;
+  // virtual suffixes are defined by consecutive calls: another first tick flushes them first
+  if (e->vx_live && first_tick != e->vx_tick)
+    if (int rc = vx_flush(e)) return rc;
   if (stats) e->hist_dirty = nticks;   // (cleared once every reduce of this call is issued)
+  if (e->P.vx) {   // (unknown until the call has issued all its launches)
+    e->vx_live = true;
+    e->vx_tick = -1;
+  }
   const Trace T0 = make_trace(e, first_tick);
   int64_t win_first = first_tick;   // first tick of the current general-kernel window
   // steady-state list skip (see raft_engine): entries per tick at most E, so
@@ -1123,8 +1158,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   const uint64_t Gs = e->cfg.groups;
   const uint64_t half = (Gs / 2) & ~uint64_t(255);
   const bool split = two && skip_list && fuse == 1 && e->split_steady && half >= 65536 && Gs - half >= 65536;
-  // the list-skipping one-tick form on tick_steady_kernel (raft_engine::steady_gpl)
-  const bool steady_k = two && skip_list && fuse == 1 && e->steady_gpl > 0 && !e->cfg.payload_crc;
+
   bool half_busy = false;   // the half stream has work the engine stream has not joined
   auto join_half = [&]() -> int {
     if (!half_busy) return RAFT_OK;
@@ -1244,21 +1278,12 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       }
       const uint32_t L = e->lpar % 3;
       const int sem = int(e->cfg.semantics);
-      if (split && steady_k) {   // the two halves on two streams (the span's stop event is recorded after the join)
-        HIPCHK(launch_tick_steady(e->R, sem, e->steady_gpl, e->P, T, st, e->blist[L], lcount(e, L), e->stream, a,
-                                  nullptr, 0, half));
-        HIPCHK(launch_tick_steady(e->R, sem, e->steady_gpl, e->P, T, st, e->blist[L], lcount(e, L), e->half_stream,
-                                  nullptr, nullptr, half, Gs - half));
-        half_busy = true;
-      } else if (split) {
+      if (split) {   // the two halves on two streams (the span's stop event is recorded after the join)
         HIPCHK(launch_tick_lean(e->R, sem, e->P, T, st, e->blist[L], lcount(e, L), 0, e->stream, a,
                                 nullptr, 0, half));
         HIPCHK(launch_tick_lean(e->R, sem, e->P, T, st, e->blist[L], lcount(e, L), 0, e->half_stream,
                                 nullptr, nullptr, half, Gs - half));
         half_busy = true;
-      } else if (steady_k) {
-        HIPCHK(launch_tick_steady(e->R, sem, e->steady_gpl, e->P, T, st, e->blist[L], lcount(e, L), e->stream, a, b, 0,
-                                  Gs));
       } else {
         HIPCHK(launch_tick_two_pass(e->R, int(e->cfg.semantics), e->P, T, st, e->work[e->wpar % NWORK],
                                     e->work_tick[e->wpar % NWORK], cnt, e->blist[L], lcount(e, L),
@@ -1376,6 +1401,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (int rc = join_half()) return rc;   // (the check record and the readback come after both halves)
   if (split && prof_b) HIPCHK(hipEventRecord(prof_b, e->stream));   // the span ends with both halves
   e->hist_dirty = 0;   // every reduce of the call is issued
+  if (e->P.vx) e->vx_tick = first_tick + int64_t(nticks);
   if (e->comm && e->comm_side) {   // the engine stream (readback, next call) waits for the side-stream sums
     HIPCHK(hipEventRecord(e->comm_ev[1], e->comm_stream));
     HIPCHK(hipStreamWaitEvent(e->stream, e->comm_ev[1], 0));
@@ -1524,6 +1550,7 @@ int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_re
                               const raft_log_entry* entries, size_t n_entries_total, raft_ae_resp* out) {
   if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
+  if (int rc = vx_flush(e)) return rc;
   e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &reqs[0].group, sizeof(raft_ae_req), n)) return rc;
@@ -1577,6 +1604,7 @@ int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_re
                             raft_vote_resp* out) {
   if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
+  if (int rc = vx_flush(e)) return rc;
   e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &reqs[0].group, sizeof(raft_vote_req), n)) return rc;
@@ -1608,6 +1636,7 @@ int raft_group_ops_batch(raft_engine* e, int64_t now_tick, const raft_group_op* 
                          raft_op_result* out) {
   if (!e || (n && (!ops_in || !out))) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
+  if (int rc = vx_flush(e)) return rc;
   e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &ops_in[0].group, sizeof(raft_group_op), n)) return rc;
@@ -1793,6 +1822,7 @@ int raft_diag_read(raft_engine* e, uint64_t* counters, uint32_t n) {
 int raft_debug_group_words(raft_engine* e, uint64_t group, int32_t* out, uint32_t n) {
   if (!e || (n && !out)) return fail(RAFT_EINVAL, "null argument");
   if (group >= e->cfg.groups) return fail(RAFT_EINVAL, "group out of range");
+  if (int rc = vx_flush(e)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   uint16_t meta = 0, rot = 0, rota = 0, rotb = 0;
   uint8_t iso = 0;
@@ -1846,11 +1876,13 @@ int raft_stream_probe(int device, uint32_t replicas, uint64_t elems, uint32_t re
                         hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess))
     rc = fail(RAFT_EHIP, "stream probe: stream / event creation failed");
   float ms = 0.f;
+  // (RAFTSTEP_PROBE_MODE, diagnostics: bit 0 plain ring stores, bit 1 non-temporal record stores)
+  const uint32_t mode = getenv("RAFTSTEP_PROBE_MODE") ? uint32_t(atoi(getenv("RAFTSTEP_PROBE_MODE"))) : 0u;
   if (rc == RAFT_OK) {
-    hipError_t h = launch_stream_probe(int(R), a, b, c, d, rt, rv, uint32_t(n), 1u, uint32_t(KS), s);
+    hipError_t h = launch_stream_probe(int(R), a, b, c, d, rt, rv, uint32_t(n), 1u, uint32_t(KS), s, mode);
     if (h == hipSuccess) h = hipEventRecord(e0, s);
     for (uint32_t i = 0; i < reps && h == hipSuccess; ++i)
-      h = launch_stream_probe(int(R), a, b, c, d, rt, rv, uint32_t(n), i & 1u, uint32_t(KS), s);
+      h = launch_stream_probe(int(R), a, b, c, d, rt, rv, uint32_t(n), i & 1u, uint32_t(KS), s, mode);
     if (h == hipSuccess) h = hipEventRecord(e1, s);
     if (h == hipSuccess) h = hipEventSynchronize(e1);
     if (h == hipSuccess) h = hipEventElapsedTime(&ms, e0, e1);
@@ -1887,6 +1919,7 @@ int raft_debug_force_pass(raft_engine* e, int64_t group) {
 int raft_state_digest(raft_engine* e, uint64_t* per_group, uint64_t* total) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
   if (int rc = settle_check(e)) return rc;
+  if (int rc = vx_flush(e)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   const uint64_t G = e->cfg.groups;
   uint64_t* d_pg = nullptr;

@@ -320,6 +320,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   uint32_t jb_col = 0, jb_rot = 0, jb_rotb = 0;   // destination column; ring words (rot | rota << 16, rotb)
   uint64_t jb_q0 = 0, jb_kv = 0;
   uint32_t df = 0;      // diagnostics: lane class bits (P.dbg)
+  uint32_t vxf = 0;     // diagnostics: 1 = a return with a virtual suffix (no copy), 2 = LXS entered with one
   bool stored = false;  // the group's rows may have been written (returned)
   // deferral-reason bits 11-15 only in a diagnostics build (make DIAG=1),
   // so the product kernel carries no extra instructions for them
@@ -332,7 +333,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     int meta = GW.meta();
     const int meta_st = meta;   // as stored (meta may drop the compressed-form flags below)
     const int c = meta & 0xF;
-    const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);   // pending catch-up / frozen group
+    const bool skip = (meta & M_DEFER) || ((meta >> 4) & 7);   // pending catch-up / frozen group
     // RAFT also takes ONECAND groups (their candidate must be isolated this tick, checked below)
     bail = !skip && (force_slow || !(meta & (RAFT ? (M_STEADY | M_ONECAND | M_ONESTALE) : M_STEADY)));
     if (bail && !force_slow && c == NO_PRIMARY) {   // leaderless: a quiet tick needs no general kernel
@@ -550,6 +551,10 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         else if (N == Ll) cm = Llt == Lt ? N : Lc;        // the cached last-entry term
         else bail = true;                                 // would need a ring read: general path
       }
+      // VX (M_VX): a virtual suffix is kept only in LXS and through the
+      // election into ONESTALE; a cut-off leader leaving the compressed form
+      // without an election goes to the general kernel (which materialises it)
+      if (RAFT && (meta & M_VX) && w < 0 && !(ss && T.iso_leader && Llt == Lt)) bail = true;
       if (!bail) {
         df |= 131072u;
         // a compressed group stays compressed (LXS: the record holds the
@@ -591,6 +596,13 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           GW.ss() = SsRec{sel(last, f), Lt, cm, sel(commit, f)};
           GW.lx() = LxRec{Ll + n - sel(last, f), dmin};
           nm |= M_SSYNC | M_LXS;
+          // entering LXS from the steady form (the leader's log was the
+          // followers'): its entries from this tick on are its own client
+          // appends, one batch per client tick — a virtual suffix (M_VX)
+          if (P.vx && !(meta & M_LXS) && Ll == sel(last, f)) {
+            nm |= M_VX;
+            vxf |= 2u;
+          }
         }
         if (w >= 0) {   // the election (see above)
           const int nt = Lt + 1, fl = sel(last, w);
@@ -762,13 +774,17 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       if (L0 >= 1) bail |= (L0 == Ll ? Llt : tc0) != (L0 == ls ? sel(lt, sr) : ts0);
       // the first conflict must be at L0+1 (else r_deliver_ae skips the entries present);
       // sr's entry L0+1 is from its ring or the one its own client append adds this tick
-      bail |= (L0 + 1 <= Ll ? tc1 : Lt) == (L0 + 1 <= ls ? ts1 : sel(term, sr));
+      // (VX: sr's entries above L0 = xlo are virtual, of its own term)
+      bail |= (L0 + 1 <= Ll ? tc1 : Lt) == ((L0 + 1 <= ls && !(meta & M_VX)) ? ts1 : sel(term, sr));
       if (!bail) {
         df |= (1u << 21) | (ls > L0 ? 1u << 22 : 0u);   // class: stale leader's return (its log truncated at L0)
         // the primary's entries after L0 (at most K): copied below by the whole wave
         // (entries L0+1..Ll: the primary's own appends since its election, the
         // last one at the client tick before this one)
-        jb_n = Ll - L0;
+        // (VX: sr's column already holds them — every write of the primary's
+        // entries since the election included it — so there is nothing to copy)
+        jb_n = (meta & M_VX) ? 0 : Ll - L0;
+        vxf |= (meta & M_VX) ? 1u : 0u;
         jb_from = L0 + 1;
         jb_col = uint32_t(sr);
         jb_term = Lt;
@@ -918,7 +934,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             const int xsb = GW.sb(), xsb2 = GW.sb2();
             uint32_t cs = 0;
             if constexpr (CRC) cs = crc_term_state(tab, x_term);
-            for (int e = 0; e < n; ++e) {
+            // (VX: its entries are virtual — its column mirrors the primary's)
+            for (int e = 0; e < ((meta & M_VX) ? 0 : n); ++e) {
               const int64_t v = int64_t(sm64(xvb ^ uint64_t(uint32_t(e))) >> 1);
               const uint32_t o = ring_in_tile(g, R, ring_slot(xl + 1 + e, xrot, xrota, xrotb, xsb, xsb2, P.kmask), uint32_t(xi));
               ring_stx<LIST>(P.log_term + tb, o, x_term);
@@ -950,6 +967,10 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       nm = keep_ss ? (nm | M_SSYNC) : (nm & ~M_SSYNC);
       if (x_fire) nm = (nm & ~M_STEADY) | M_ONECAND;
       if (sr >= 0) nm = (nm & ~M_ONESTALE) | M_STEADY;   // one leader, every other replica a follower
+      // (a virtual suffix lives only with a cut-off leader: LXS / ONESTALE;
+      // the return truncates it away, and any other way out of those forms
+      // bailed above while the suffix was non-empty)
+      if (!(nm & (M_LXS | M_ONESTALE))) nm &= ~M_VX;
       // SXS after this tick (RAFT; the rows were stored explicitly above and are
       // now stale but for the stale leader's): every follower of the primary
       // accepted, every log but the stale leader's ends at Ll+n with an entry
@@ -990,6 +1011,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         }
         if (same) {
           wr = okm | (1u << c);
+          if (stale && (meta & M_VX)) wr |= 1u << xi;   // VX: the stale leader's column mirrors the primary's
           w_term = Lt;
           w_ph = (Ll + rot) & int(P.kmask);
           w_vb = vb;
@@ -1022,7 +1044,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             df |= ok ? 0u : 128u;
             if (hi <= Ll && ok) {
               df |= 32u | ((sbo <= 1 || sbo <= lo - int(P.K) + 1) ? 0u : 1u << 25);   // (+ the previous segment stays live)
-              if (stale && xtop > Ll) {   // the stale leader's entries Ll+1..xtop: slot (i-1+rot) -> (i-1+rot+d)
+              // (VX: the stale leader's entries are virtual: nothing to move)
+              if (stale && xtop > Ll && !(meta & M_VX)) {   // its entries Ll+1..xtop: slot (i-1+rot) -> (i-1+rot+d)
                 // (its entries above Ll: its own appends since it was cut off,
                 // the last ones this tick; every index uses the new rotation)
                 jb_n = xtop - Ll;
@@ -1056,10 +1079,12 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
             uint32_t stamp = 0;
             if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+            // (VX: the stale leader's column mirrors the primary's entries)
+            const uint32_t mir = (stale && (meta & M_VX)) ? 1u << xi : 0u;
 #pragma unroll
             for (int p = 0; p < R; ++p) {
-              if (p != c && !((okm >> p) & 1u)) continue;
-              const int i0 = p == c ? Ll : last[p] - n;
+              if (p != c && !((okm >> p) & 1u) && !((mir >> p) & 1u)) continue;
+              const int i0 = (p == c || ((mir >> p) & 1u)) ? Ll : last[p] - n;
               const uint32_t o = ring_in_tile(g, R, ring_slot(i0 + e + 1, uint32_t(rot), rota, rotb, sb, sb2, P.kmask), uint32_t(p));
               ring_stx<LIST>(P.log_term + tb, o, Lt);
               ring_stx<LIST>(P.log_value + tb, o, v);
@@ -1272,10 +1297,16 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     DIAG_REASON(if (bail && !(df & (2048u | 4096u | 8192u | 16384u))) df |= 32768u;);   // reason: anything later
     DIAG_REASON(if (!bail) df &= ~(2048u | 4096u | 8192u | 16384u););
     if (bail) df &= ~0x7FF80000u;   // the class bits 19-30 count taken ticks only
+    if (bail) vxf = 0u;
 #pragma unroll 1
     for (int k = 0; k < 32; ++k) {
       const uint64_t b = __ballot((df >> k) & 1u);
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[32 + k], (unsigned long long)__popcll(b));
+    }
+#pragma unroll 1
+    for (int k = 0; k < 2; ++k) {   // (the VX classes: lean-range slots 28, 29)
+      const uint64_t b = __ballot((vxf >> k) & 1u);
+      if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[28 + k], (unsigned long long)__popcll(b));
     }
   }
 #endif
@@ -1602,7 +1633,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     // made every later load of the lane wait for it: vmcnt counts stores)
     held = (lflags & 1) && at(P.glst, g) != 0;
     const int c = meta & 0xF;
-    const bool skip = held || (meta & M_DEFER) || ((meta >> 4) & 0xF);   // carried / pending catch-up / frozen group
+    const bool skip = held || (meta & M_DEFER) || ((meta >> 4) & 7);   // carried / pending catch-up / frozen group
     take = !skip && (meta & M_SSYNC) && c < R && g != P.dbg_pass;   // (test knob: pass one group on)
     pass = !skip && !take;
     df |= (!skip && g == P.dbg_pass) ? 1u << 24 : 0u;
@@ -1693,10 +1724,14 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         hbw = true;
         const int wph = (L + rot) & int(P.kmask);
         if (take && n && wph != ph) w_slot = wph;
-        wmask = ((1u << R) - 1u) & ~(1u << xs);
-        x_slot = take ? (L + k + rot) & int(P.kmask) : -1;
+        // VX (M_VX): xs's entries are virtual and its column mirrors the
+        // primary's: whole rows, nothing of its own to write
+        const bool vx = (meta & M_VX) != 0;
+        wmask = vx ? (1u << R) - 1u : ((1u << R) - 1u) & ~(1u << xs);
+        x_slot = (take && !vx) ? (L + k + rot) & int(P.kmask) : -1;
         x_r = xs;
-        df |= take ? ((w_slot < 0 ? 256u : 512u) | (1u << 25) | (x_slot == ph ? 1u << 26 : 0u)) : 0u;
+        df |= take ? ((w_slot < 0 ? 256u : 512u) | (1u << 25) | (x_slot == ph ? 1u << 26 : 0u) | (vx ? 1u << 27 : 0u))
+                   : 0u;
       } else {
         // (the followers' CommitIndex min(LeaderCommit, last new entry) is the
         // leader's only while that is at most L+n: a leader's CommitIndex above
@@ -1776,7 +1811,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         committed = cl2 - s.cl;
         w_term = s.term;
         w_vb = vb;
-        if (RAFT && !CRC && sxs) x_vb = rng_k(key, uint32_t(x_r), ST_VALUE, uint64_t(T.tick));
+        if (RAFT && !CRC && sxs && x_slot >= 0) x_vb = rng_k(key, uint32_t(x_r), ST_VALUE, uint64_t(T.tick));
       } else {
         pass = true;
         w_slot = -1;
@@ -1873,9 +1908,9 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
 #endif
     df |= (g < P.G) ? 1024u : 0u;
     df |= pass ? 1u << 23 : 0u;
-    if (!take) df &= ~0x6780000u;   // the class bits 19-22, 25, 26 count taken ticks only
+    if (!take) df &= ~0xE780000u;   // the class bits 19-22, 25-27 count taken ticks only
 #pragma unroll 1
-    for (int k = 0; k < 27; ++k) {
+    for (int k = 0; k < 28; ++k) {
       const uint64_t b = __ballot((df >> k) & 1u);
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
     }
@@ -1922,133 +1957,6 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   }
 }
 
-// Steady tick (the steady-state list skip, engine.cpp; one tick per launch):
-// every live group is proven compressed (SSYNC), in the global ring phase and
-// takeable, and no isolation or corruption is configured, so the tick of
-// every group is the lean kernel's normal class — client append of n entries
-// (main.go:327-329), one accepted AppendEntries per follower (341-372 ->
-// 121-156), the responses (375-378), the commit rule (381-391), one heartbeat
-// time for every follower — and nothing else needs a branch. Each lane runs
-// GPL groups (GPL consecutive 64-group tiles per wave) with all their loads
-// issued in one round trip, so a wave keeps GPL times the lean kernel's bytes
-// in flight. Per group it reads gmeta 2 B + gss 16 B + grot 2 B and writes
-// gss 16 B, hb 4 B and 12 n R B of entries as whole ring rows: the lean
-// kernel's bytes. A group that is not takeable (which the skip's proof
-// excludes) is passed to the list, which the end-of-call check turns into
-// RAFT_EINTERNAL.
-template <int R, int SEM, int GPL>
-__global__ __launch_bounds__(256) void tick_steady_kernel(DevPlanes P, Trace T, unsigned long long* stats,
-                                                          uint32_t* list, uint32_t* count, uint32_t gofs,
-                                                          uint32_t ng) {
-  constexpr bool RAFT = SEM == SEM_RAFT;
-  const int lane = int(threadIdx.x & 63u);
-  const uint32_t wv = blockIdx.x * 4u + (threadIdx.x >> 6);          // this wave of the launch
-  const uint32_t g0 = gofs + wv * 64u * GPL;                          // its first group (a tile boundary)
-  const uint32_t gend = gofs + ng;
-  const int n = int(T.client_entries());
-  const int ph = int(T.entries_before(T.tick) & P.kmask);
-  int meta[GPL], rot[GPL];
-  SsRec s[GPL];
-#pragma unroll
-  for (int q = 0; q < GPL; ++q) {   // every load of the lane in one round trip
-    const uint32_t g = g0 + uint32_t(q * 64 + lane);
-    meta[q] = 0xFFFF; rot[q] = 0; s[q] = SsRec{0, 0, 0, 0};
-    if (g < gend) { meta[q] = at(P.gmeta, g); s[q] = P.gss[g]; rot[q] = at(P.grot, g); }
-  }
-  int k_src[R];
-#pragma unroll
-  for (int k = 0; k < R; ++k) k_src[k] = (k * 64 + lane) / R;
-  int committed = 0, taken = 0, passed = 0;
-#pragma unroll
-  for (int q = 0; q < GPL; ++q) {
-    const uint32_t g = g0 + uint32_t(q * 64 + lane);
-    const bool valid = g < gend;
-    const int mt = meta[q], c = mt & 0xF;
-    const bool skip = !valid || (mt & M_DEFER) || ((mt >> 4) & 0xF);
-    const SsRec x = s[q];
-    const int L = x.last;
-    // (as the fused kernel: SSYNC, no LXS / SXS / HWX, in phase, within range)
-    const bool take = !skip && (mt & M_SSYNC) && c < R && !uses_glx(mt) && !(RAFT && (mt & M_HWX)) &&
-                      g != P.dbg_pass && L > 0 && int64_t(L) + n <= I32MAX && n < int(P.K) && x.cl <= L + n &&
-                      (n == 0 || ((L + rot[q]) & int(P.kmask)) == ph);
-    const bool pass = !skip && !take;
-    int nl = L, cl2 = x.cl, cf2 = x.cf;
-    if (take) {
-      nl = L + n;
-      if (RAFT ? nl > x.cl : (2 * (R - 1) > R && nl > x.cl)) cl2 = nl;
-      cf2 = x.cl > x.cf ? x.cl : x.cf;
-      committed += cl2 - x.cl;
-      ++taken;
-    }
-    if (n && __ballot(take)) {   // this tick's entries as whole ring rows of this tile
-      const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g0 + uint32_t(q * 64)), P.KP, R);
-      int32_t* const rt = P.log_term + tb;
-      int64_t* const rv = P.log_value + tb;
-      const uint64_t vb = take ? rng_k(group_key(T.seed, P.gbase + g), uint32_t(c), ST_VALUE, uint64_t(T.tick)) : 0ull;
-      int k_term[R];
-      bool k_on[R];
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        k_term[k] = __shfl(x.term, k_src[k]);
-        k_on[k] = __shfl(take ? 1 : 0, k_src[k]) != 0;
-      }
-      for (int e = 0; e < n; ++e) {
-        const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
-        const uint32_t row = uint32_t((ph + e) & int(P.kmask)) * 64u * R;
-        const int vlo = int(uint32_t(uint64_t(v))), vhi = int(uint32_t(uint64_t(v) >> 32));
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-          const int lo = __shfl(vlo, k_src[k]), hi = __shfl(vhi, k_src[k]);
-          if (k_on[k]) {
-            const uint32_t o = row + uint32_t(k * 64 + lane);
-            ring_st(rt, o, k_term[k]);
-            ring_st(rv, o, int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo)));
-          }
-        }
-      }
-    }
-    if (take) {
-      if (P.rec_nt) {   // (DevPlanes::rec_nt)
-        typedef int32_t i4 __attribute__((ext_vector_type(4)));
-        if (nl != L || cl2 != x.cl || cf2 != x.cf)
-          __builtin_nontemporal_store(i4{nl, x.term, cl2, cf2}, reinterpret_cast<i4*>(&P.gss[g]));
-        __builtin_nontemporal_store(int32_t(T.now), &P.hb[g]);   // timer.Reset(d) of every follower
-      } else {
-        if (nl != L || cl2 != x.cl || cf2 != x.cf) P.gss[g] = SsRec{nl, x.term, cl2, cf2};
-        at(P.hb, g) = T.now;   // timer.Reset(d) of every follower
-      }
-    }
-    if (pass) {   // (the skip's proof violated: the id only, one atomic per lane; see tick_fused_kernel)
-      const uint32_t k = shard_home(g);
-      list[k * P.scap + atomicAdd(&count[k * SHARD_STRIDE], 1u)] = g;
-      ++passed;
-    }
-  }
-  if (P.dbg) {   // diagnostics (lean kernel counters): lanes, compressed ticks taken, passed on
-    const long long tk = wave_sum(taken), ps = wave_sum(passed);
-    if (lane == 0) {
-      uint32_t nv = 0;
-#pragma unroll
-      for (int q = 0; q < GPL; ++q) nv += (g0 + uint32_t(q * 64) < gend) ? min(gend - (g0 + uint32_t(q * 64)), 64u) : 0u;
-      atomicAdd(&P.dbg[10], (unsigned long long)nv);
-      if (tk) atomicAdd(&P.dbg[18], (unsigned long long)tk);
-      if (ps) atomicAdd(&P.dbg[23], (unsigned long long)ps);
-    }
-  }
-  if (stats) {
-    const int t = taken;
-    if constexpr (RAFT) {
-      const int v[5] = {committed, t * (R - 1), 0, t, 0};
-      const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
-      block_stats<5>(v, idx, stats);
-    } else {
-      const int v[4] = {committed, t * (R - 1), 0, t};
-      const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
-      block_stats<4>(v, idx, stats);
-    }
-  }
-}
-
 // Fused steady ticks (the steady-state list skip, engine.cpp): every live
 // group is proven compressed and takeable and no isolation or corruption is
 // configured, so the lean kernel's normal class is the whole tick of every
@@ -2076,7 +1984,7 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
     c = meta & 0xF;
-    const bool skip = (meta & M_DEFER) || ((meta >> 4) & 0xF);
+    const bool skip = (meta & M_DEFER) || ((meta >> 4) & 7);
     live = !skip && (meta & M_SSYNC) && c < R && !uses_glx(meta) && !(RAFT && (meta & M_HWX)) &&
            g != P.dbg_pass;
     pass = !skip && !live;
@@ -2291,25 +2199,6 @@ hipError_t launch_tick_lean(int R, int sem, const DevPlanes& P, const Trace& T, 
   }
   if (crc) { RAFT_LEAN(true); } else { RAFT_LEAN(false); }
 #undef RAFT_LEAN
-  return hipGetLastError();
-}
-hipError_t launch_tick_steady(int R, int sem, int gpl, const DevPlanes& P, const Trace& T, unsigned long long* stats,
-                              uint32_t* list, uint32_t* count, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop,
-                              uint64_t g0, uint64_t ng) {
-  if (!ng) return hipSuccess;
-  const dim3 grid(unsigned((ng + 256u * uint64_t(gpl) - 1) / (256u * uint64_t(gpl))));
-#define RAFT_STEADY(GPL_)                                                                                       \
-  if (sem == SEM_RAFT) {                                                                                         \
-    RAFT_DISPATCH_R(R, hipExtLaunchKernelGGL((tick_steady_kernel<RR, SEM_RAFT, GPL_>), grid, dim3(256), 0, s,   \
-                                             ev_start, ev_stop, 0, P, T, stats, list, count, uint32_t(g0),       \
-                                             uint32_t(ng)))                                                      \
-  } else {                                                                                                       \
-    RAFT_DISPATCH_R(R, hipExtLaunchKernelGGL((tick_steady_kernel<RR, SEM_REF, GPL_>), grid, dim3(256), 0, s,    \
-                                             ev_start, ev_stop, 0, P, T, stats, list, count, uint32_t(g0),       \
-                                             uint32_t(ng)))                                                      \
-  }
-  if (gpl == 2) { RAFT_STEADY(2); } else { RAFT_STEADY(1); }
-#undef RAFT_STEADY
   return hipGetLastError();
 }
 hipError_t launch_tick_list(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,

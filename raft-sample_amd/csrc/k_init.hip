@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
   uint64_t h = 0;
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
-    const int primary = meta & 0xF, fault = (meta >> 4) & 0xF;
+    const int primary = meta & 0xF, fault = (meta >> 4) & 7;
     const bool msync = (meta & M_MSYNC) && primary < R;
     const bool ssync = (meta & M_SSYNC) && primary < R;   // compressed state: the gss record
     const SsRec ss = ssync ? P.gss[g] : SsRec{0, 0, 0, 0};
@@ -322,7 +322,7 @@ hipError_t launch_digest(int R, const DevPlanes& P, int raft, uint64_t* per_grou
 template <int R>
 __global__ __launch_bounds__(256) void stream_probe_kernel(const uint16_t* a, SsRec* b, const uint16_t* c, int32_t* d,
                                                            int32_t* rt, int64_t* rv, uint32_t n, uint32_t slot,
-                                                           uint32_t kslots) {
+                                                           uint32_t kslots, uint32_t mode) {
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
   SsRec s{0, 0, 0, 0};
   uint32_t x = 0;
@@ -339,19 +339,45 @@ __global__ __launch_bounds__(256) void stream_probe_kernel(const uint16_t* a, Ss
   for (int k = 0; k < R; ++k) {
     const int src = (k * 64 + lane) / R;
     const int t = __shfl(v32, src), lo = __shfl(vlo, src), hi = __shfl(vhi, src);
-    __builtin_nontemporal_store(t, &rt[tb + uint64_t(k * 64 + lane)]);
-    __builtin_nontemporal_store(int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo)), &rv[tb + uint64_t(k * 64 + lane)]);
+    const int64_t val = int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
+    if (mode & 1u) {   // (mode bit 0: plain ring stores)
+      rt[tb + uint64_t(k * 64 + lane)] = t;
+      rv[tb + uint64_t(k * 64 + lane)] = val;
+    } else {
+      __builtin_nontemporal_store(t, &rt[tb + uint64_t(k * 64 + lane)]);
+      __builtin_nontemporal_store(val, &rv[tb + uint64_t(k * 64 + lane)]);
+    }
   }
   if (g < n) {
-    b[g] = SsRec{s.last + 1, s.term, s.cl + 1, s.cf + 1};
-    d[g] = s.term + int32_t(slot);
+    if (mode & 2u) {   // (mode bit 1: non-temporal record / heartbeat stores)
+      typedef int32_t i4 __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(i4{s.last + 1, s.term, s.cl + 1, s.cf + 1}, reinterpret_cast<i4*>(&b[g]));
+      __builtin_nontemporal_store(int32_t(s.term + int32_t(slot)), &d[g]);
+    } else {
+      b[g] = SsRec{s.last + 1, s.term, s.cl + 1, s.cf + 1};
+      d[g] = s.term + int32_t(slot);
+    }
   }
 }
 
+// VX (raft_device.hpp M_VX): every group's virtual suffix into the ring (the
+// engine runs this before host reads of the state and handler batches)
+template <int R>
+__global__ __launch_bounds__(256) void vx_flush_kernel(DevPlanes P, uint64_t Qb, uint32_t E, uint32_t period,
+                                                       uint64_t seed) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  if (g < P.G) vx_materialize<R>(P, g, Qb, E, period, seed);
+}
+hipError_t launch_vx_flush(int R, const DevPlanes& P, uint64_t Qb, uint32_t E, uint32_t period, uint64_t seed,
+                           hipStream_t s) {
+  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(vx_flush_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P, Qb, E, period, seed));
+  return hipGetLastError();
+}
+
 hipError_t launch_stream_probe(int R, const uint16_t* a, SsRec* b, const uint16_t* c, int32_t* d, int32_t* rt,
-                               int64_t* rv, uint32_t n, uint32_t slot, uint32_t kslots, hipStream_t s) {
+                               int64_t* rv, uint32_t n, uint32_t slot, uint32_t kslots, hipStream_t s, uint32_t mode) {
   RAFT_DISPATCH_R(R, hipLaunchKernelGGL(stream_probe_kernel<RR>, grid_for(n), dim3(256), 0, s, a, b, c, d, rt, rv, n,
-                                        slot, kslots));
+                                        slot, kslots, mode));
   return hipGetLastError();
 }
 

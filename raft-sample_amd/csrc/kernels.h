@@ -72,11 +72,7 @@ hipError_t launch_tick_fused(int R, int sem, const DevPlanes& P, const Trace& T,
 hipError_t launch_tick_lean(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* list,
                             uint32_t* count, int lflags, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop,
                             uint64_t g0 = 0, uint64_t ng = ~0ull, uint32_t* zero_count = nullptr);
-// Steady tick (list skipped, no payload CRC): tick_steady_kernel, gpl groups
-// per lane (1 or 2), over groups [g0, g0 + ng) (g0 a multiple of 64)
-hipError_t launch_tick_steady(int R, int sem, int gpl, const DevPlanes& P, const Trace& T, unsigned long long* stats,
-                              uint32_t* list, uint32_t* count, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop,
-                              uint64_t g0, uint64_t ng);
+
 hipError_t launch_tick_list(int R, int sem, const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                             int32_t* work_tick, uint32_t* work_count, uint32_t* list, uint32_t* count,
                             uint32_t* next_count, const ListNext* next, hipStream_t s, hipEvent_t ev_start,
@@ -127,7 +123,10 @@ hipError_t launch_window_tail(const DevPlanes& P, const uint32_t* work, uint32_t
 hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s,
                                const CallCheck* chk = nullptr);
 hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s);
+hipError_t launch_vx_flush(int R, const DevPlanes& P, uint64_t Qb, uint32_t E, uint32_t period, uint64_t seed,
+                           hipStream_t s);
 hipError_t launch_stream_probe(int R, const uint16_t* a, SsRec* b, const uint16_t* c, int32_t* d, int32_t* rt,
-                               int64_t* rv, uint32_t n, uint32_t slot, uint32_t kslots, hipStream_t s);
+                               int64_t* rv, uint32_t n, uint32_t slot, uint32_t kslots, hipStream_t s,
+                               uint32_t mode = 0);
 
 }  // namespace raftstep

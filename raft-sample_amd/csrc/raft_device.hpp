@@ -33,7 +33,23 @@ enum : int {
   S_FAULTS = 6, S_LEADER_GROUPS = 7, NSTAT = 8
 };
 constexpr int NO_PRIMARY = 0xF;
-// gmeta flag bits (above primary:4 | fault:4)
+// gmeta flag bits (above primary:4 | fault:3; fault codes are 0..5)
+// VX (RAFT, with LXS, ONESTALE or SXS; round 5): the group's one cut-off
+// leader xr — the LXS primary, or the ONESTALE / SXS stale leader — holds a
+// VIRTUAL suffix: its entries xlo+1 .. last[xr] are not in its ring column
+// but are its own client appends, one batch per client tick up to the last
+// client tick before the tick being run (a leader appends at every client
+// tick, main.go:327-329, a cut-off one too), so entry xlo+j is regenerated
+// from the trace RNG (vx_entry). xlo is the followers' LastApplied (LXS: the
+// gss record) or the primary's NextIndex for xr minus one (ONESTALE / SXS).
+// Its column there holds the primary's entries instead (every write of the
+// primary's entries includes it), so the stale leader's return — truncation
+// at xlo and the primary's entries appended — needs no ring copy. Only the
+// fast paths that keep both properties take a VX group (k_fast.hip); every
+// other reader first writes the suffix into the column and drops the flag
+// (vx_materialize: the general kernel at load, the engine before host reads
+// and handler batches).
+constexpr int M_VX = 1 << 7;
 constexpr int M_DEFER = 1 << 8;   // on the worklist with ticks pending; the fast kernel leaves it alone
 constexpr int M_MSYNC = 1 << 9;   // primary's MatchIndex[p] == LastApplied[p] for every peer; lmatch is stale
 constexpr int M_STEADY = 1 << 10; // exactly one leader (the primary), every other replica a follower
@@ -144,6 +160,10 @@ struct DevPlanes {
   // anyway (engine.cpp: 40 B x Gp above it; round 5, C2 at 2^24: +2%);
   // below that, plain stores keep them resident (C2 at 2^20: nt 3% slower)
   uint32_t rec_nt;
+  // VX (see M_VX) enabled: RAFT, leader isolation, no payload CRC
+  // (RAFTSTEP_VX=0 turns it off); the fast paths then give a group entering
+  // LXS a virtual suffix
+  uint32_t vx;
   uint32_t diag;       // timing-only diagnostics (RAFTSTEP_DIAG_LEAN; results are wrong when set): 1 = drifted
                        // lanes of the lean kernel skip their ring writes, 2 = they write the wave's common row
                        // (list kernel: 32 = staging alone, 64 = no tick, 128 = no ring writes / copies)
@@ -333,15 +353,29 @@ __device__ __forceinline__ uint32_t udiv_magic(uint32_t x, uint32_t m, uint32_t 
 }
 
 // ------------------------------------------------------------------ RNG --
-__device__ __forceinline__ uint64_t sm64(uint64_t x) {
+__host__ __device__ __forceinline__ uint64_t sm64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ULL;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
   return x ^ (x >> 31);
 }
-__device__ __forceinline__ uint64_t group_key(uint64_t seed, uint64_t gid) { return sm64(seed ^ sm64(gid)); }
-__device__ __forceinline__ uint64_t rng_k(uint64_t key, uint32_t r, uint32_t stream, uint64_t tick) {
+__host__ __device__ __forceinline__ uint64_t group_key(uint64_t seed, uint64_t gid) { return sm64(seed ^ sm64(gid)); }
+__host__ __device__ __forceinline__ uint64_t rng_k(uint64_t key, uint32_t r, uint32_t stream, uint64_t tick) {
   return sm64(sm64(key ^ ((uint64_t(stream) << 32) | r)) ^ tick);
+}
+
+// VX (see M_VX): the value of a leader's client append that is the global
+// client entry q (entry q mod E of client tick (q / E) * period; E entries
+// per client tick), as the tick's client append draws it: value stream
+// rng_k(key, r, ST_VALUE, tick), entry e = sm64(stream ^ e) >> 1 (rand.Int(),
+// main.go:92). kv = sm64(key ^ (ST_VALUE << 32 | r)), the stream's key part.
+__host__ __device__ __forceinline__ uint64_t vx_stream_key(uint64_t key, uint32_t r) {
+  return sm64(key ^ ((uint64_t(ST_VALUE) << 32) | r));
+}
+__host__ __device__ __forceinline__ int64_t vx_value(uint64_t kv, uint64_t q, uint32_t E, uint32_t period) {
+  const uint64_t qt = E == 1u ? q : q / E;
+  const uint64_t qe = E == 1u ? 0u : q - qt * E;
+  return int64_t(sm64(sm64(kv ^ (qt * period)) ^ qe) >> 1);
 }
 
 // Out-of-line RNG for the general kernels' unrolled per-replica code (the
@@ -444,6 +478,48 @@ struct AEReq {          // AppendEntriesRequest (main.go:289-296), LeaderId impl
 };
 struct AEResp { int term, match, ok; };  // AppendEntriesResponse (main.go:298-302)
 
+// VX (see M_VX): writes group g's virtual suffix into its cut-off leader's
+// ring column and drops the flag — the form's state as of the start of a tick
+// whose client entries before it number Qb (entries_before(that tick)), so
+// the suffix's last entry is the global client entry Qb - 1. Every reader
+// other than the VX-aware fast paths runs this first. (RAFT only; never with
+// payload CRC.)
+template <int R>
+__device__ __forceinline__ void vx_materialize(const DevPlanes& P, uint32_t g, uint64_t Qb, uint32_t E, uint32_t period,
+                                               uint64_t seed) {
+  const int meta = at(P.gmeta, g);
+  if (!(meta & M_VX)) return;
+  const int c = meta & 0xF;
+  int xr = c, xlo = 0, xtop = 0, xterm = 0;
+  if (meta & (M_LXS | M_SSYNC)) {   // LXS (the primary k ahead) or SXS (the stale leader xs = glx.dl)
+    const SsRec s = P.gss[g];
+    const LxRec x = P.glx[g];
+    const bool lxs = (meta & M_LXS) != 0;
+    xr = lxs ? c : x.dl;
+    xlo = lxs ? s.last : at(P.lnext, rix<R>(g, xr)) - 1;
+    xtop = s.last + x.k;
+    xterm = lxs ? s.term : s.term - 1;
+  } else {                          // ONESTALE, explicit rows: the other leader
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (r != c && (at(P.rs, rix<R>(g, r)) & 3) == ROLE_L) xr = r;
+    xlo = at(P.lnext, rix<R>(g, xr)) - 1;
+    xtop = at(P.last, rix<R>(g, xr));
+    xterm = at(P.term, rix<R>(g, xr));
+  }
+  const uint64_t tb = ring_tile(g, P.KP, R);
+  const uint32_t rot = at(P.grot, g), rota = at(P.grota, g), rotb = at(P.grotb, g);
+  const int sb = at(P.gsb, g), sb2 = at(P.gsb2, g);
+  const uint64_t kv = vx_stream_key(group_key(seed, P.gbase + g), uint32_t(xr));
+  const int lo = max(xlo, xtop - int(P.K));   // (older entries are out of every reader's window)
+  for (int idx = lo + 1; idx <= xtop; ++idx) {
+    const uint32_t o = ring_in_tile(g, R, ring_slot(idx, rot, rota, rotb, sb, sb2, P.kmask), uint32_t(xr));
+    at(P.log_term + tb, o) = xterm;
+    at(P.log_value + tb, o) = vx_value(kv, Qb - uint64_t(xtop - idx) - 1u, E, period);
+  }
+  at(P.gmeta, g) = uint16_t(meta & ~M_VX);
+}
+
 // Group context: the R replicas of one group, in registers. SEM selects the
 // handler rules: SEM_REF = main.go bit for bit, SEM_RAFT = the EXT
 // Raft-paper mode (same tick model and layout, see the r_* methods).
@@ -523,7 +599,7 @@ struct Group {
     const int m = at(P.gmeta, g);
     meta0 = m;
     primary = m & 0xF;
-    fault = (m >> 4) & 0xF;
+    fault = (m >> 4) & 7;
     hbt = HB_NONE;
     rot = rot0 = at(P.grot, g);
     rota = rota0 = at(P.grota, g);

@@ -119,7 +119,7 @@ struct Seg {
     const int m = at(P.gmeta, g);
     meta0 = m;
     primary = m & 0xF;
-    fault = (m >> 4) & 0xF;
+    fault = (m >> 4) & 7;
     rot = at(P.grot, g);
     rota = at(P.grota, g);
     sbd = at(P.gsb, g);

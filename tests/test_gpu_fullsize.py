@@ -139,14 +139,20 @@ def test_c2_as_benchmarked_full_size_slices():
 MIN_TAKEN = 1000
 
 
-def test_class_coverage_c4_config_full_oracle():
+@pytest.mark.parametrize("vx", ["1", "0"], ids=["virtual_suffix", "stored_suffix"])
+def test_class_coverage_c4_config_full_oracle(monkeypatch, vx):
     """C4's configuration (R=7, K=128, leader isolation, RAFT, seed
     0x5EED0004) on 2^16 groups against ONE oracle over every group — stats
     and per-group digests after every call, the whole canonical state at
     three points — with the tick-class counters on: every fast-path class of
     the lean and list kernels is taken >= 1000 times in this oracle-compared
     run (elections, first rounds, stale leaders, returns with truncation,
-    LXS, HWX, three-segment switches, window starts, quiet leaderless ticks)."""
+    LXS, HWX, three-segment switches, window starts, quiet leaderless ticks).
+    With virtual suffixes (M_VX, the default) the cut-off leaders' entries are
+    regenerated, their returns copy nothing and no switch moves them (the
+    digests after every call materialise the suffixes, so both forms run);
+    RAFTSTEP_VX=0 stores them, copies them back and moves them."""
+    monkeypatch.setenv("RAFTSTEP_VX", vx)
     _, kw = workload_kwargs("C4", groups=1 << 16)
     e = Engine(**kw)
     o = oracle.Oracle(**kw)
@@ -172,7 +178,9 @@ def test_class_coverage_c4_config_full_oracle():
     need = ["lean_ssync", "lean_lxs", "lean_lxs_whole_row", "lean_switch", "lean_three_seg", "lean_hwx",
             "list_quiet", "list_isolated_leader", "list_election", "list_first_round", "list_return",
             "list_return_trunc", "list_stale", "list_hwx", "list_window_start", "list_switch", "lean_sxs",
-            "lean_sxs_stale_in_row", "list_sxs_entered", "list_sxs_materialised", "list_stale_moved"]
+            "list_sxs_entered", "list_sxs_materialised"]
+    need += ["lean_sxs_vx", "list_return_vx", "list_lxs_vx"] if vx == "1" else \
+        ["lean_sxs_stale_in_row", "list_stale_moved"]
     low = {k: cls[k] for k in need if cls[k] < MIN_TAKEN}
     assert not low, f"classes taken fewer than {MIN_TAKEN} times: {low}\nall: {cls}"
 
