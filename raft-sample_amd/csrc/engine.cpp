@@ -159,6 +159,11 @@ struct raft_engine {
   // before vx_tick (-1: unknown, a call failed mid-way: the engine is poisoned)
   bool vx_live = false;
   int64_t vx_tick = 0;
+  // the current run of consecutive raft_tick calls (Trace::contig_q): it
+  // starts at contig_from and continues at run_next; a call at another tick,
+  // a handler batch or a state replacement starts a new one
+  bool run_valid = false, run_done = false;   // (run_done: the last call issued everything)
+  int64_t contig_from = 0, run_next = 0;
   int force_general = 0;        // debug: route every group through the general kernel
   int lane_general = 0;         // RAFTSTEP_GENERAL=lane: one-lane-per-group general kernel (A/B) instead of the segment one
   uint32_t slow_every = 8;      // run the general kernel every this many ticks (and at the end of a call)
@@ -281,6 +286,9 @@ Trace make_trace(const raft_engine* e, int64_t tick) {
   T.secs = e->cfg.tick_seconds;
   T.period = e->cfg.client_period;
   T.entries = e->cfg.entries_per_tick;
+  const int64_t cf = e->contig_from;
+  T.contig_q = (T.period && cf > 0) ? uint64_t((cf + int64_t(T.period) - 1) / int64_t(T.period)) * T.entries : 0u;
+  if (!e->run_valid) T.contig_q = ~uint64_t(0);   // (no run: nothing regenerable)
   return T;
 }
 
@@ -358,6 +366,7 @@ int settle_check(raft_engine* e) {
 void state_replacing(raft_engine* e) {
   e->steady_origin = e->steady_ok = false;
   e->vx_live = false;   // (the state is being replaced: no suffix survives)
+  e->run_valid = false;
 }
 // ... and only once the new state's launches / copies have gone through
 // successfully drops any poison and a still-pending end-of-call check (both
@@ -1134,6 +1143,12 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     e->vx_live = true;
     e->vx_tick = -1;
   }
+  if (!e->run_valid || !e->run_done || first_tick != e->run_next) {   // a new run of consecutive calls
+    e->contig_from = first_tick;
+    e->run_valid = true;
+  }
+  e->run_next = first_tick + int64_t(nticks);
+  e->run_done = false;
   const Trace T0 = make_trace(e, first_tick);
   int64_t win_first = first_tick;   // first tick of the current general-kernel window
   // steady-state list skip (see raft_engine): entries per tick at most E, so
@@ -1402,6 +1417,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (split && prof_b) HIPCHK(hipEventRecord(prof_b, e->stream));   // the span ends with both halves
   e->hist_dirty = 0;   // every reduce of the call is issued
   if (e->P.vx) e->vx_tick = first_tick + int64_t(nticks);
+  e->run_done = true;
   if (e->comm && e->comm_side) {   // the engine stream (readback, next call) waits for the side-stream sums
     HIPCHK(hipEventRecord(e->comm_ev[1], e->comm_stream));
     HIPCHK(hipStreamWaitEvent(e->stream, e->comm_ev[1], 0));
@@ -1551,6 +1567,7 @@ int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_re
   if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
   if (int rc = vx_flush(e)) return rc;
+  e->run_valid = false;   // host mutation: entries from here on are not the trace's
   e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &reqs[0].group, sizeof(raft_ae_req), n)) return rc;
@@ -1605,6 +1622,7 @@ int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_re
   if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
   if (int rc = vx_flush(e)) return rc;
+  e->run_valid = false;   // host mutation: entries from here on are not the trace's
   e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &reqs[0].group, sizeof(raft_vote_req), n)) return rc;
@@ -1637,6 +1655,7 @@ int raft_group_ops_batch(raft_engine* e, int64_t now_tick, const raft_group_op* 
   if (!e || (n && (!ops_in || !out))) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
   if (int rc = vx_flush(e)) return rc;
+  e->run_valid = false;   // host mutation: entries from here on are not the trace's
   e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
   if (int rc = check_distinct(e, &ops_in[0].group, sizeof(raft_group_op), n)) return rc;

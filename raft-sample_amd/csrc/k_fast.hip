@@ -776,6 +776,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       // sr's entry L0+1 is from its ring or the one its own client append adds this tick
       // (VX: sr's entries above L0 = xlo are virtual, of its own term)
       bail |= (L0 + 1 <= Ll ? tc1 : Lt) == ((L0 + 1 <= ls && !(meta & M_VX)) ? ts1 : sel(term, sr));
+      // (the catch-up regenerates the primary's entries L0+1..Ll: they must
+      // all be from the current run of consecutive calls, T.contig_q)
+      if (!(meta & M_VX)) bail |= T.entries_before(T.tick) - uint64_t(Ll - L0) < T.contig_q;
       if (!bail) {
         df |= (1u << 21) | (ls > L0 ? 1u << 22 : 0u);   // class: stale leader's return (its log truncated at L0)
         // the primary's entries after L0 (at most K): copied below by the whole wave
@@ -1038,8 +1041,13 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             const int xtop = stale ? sel(last, xi) + n : 0;   // the stale leader's length after this tick
             const int sbo = GW.sb();
             const uint32_t rota = GW.rota();
+            // (a stale leader's entries above Ll are moved by regenerating them:
+            // only when they are all from the current run of calls, T.contig_q;
+            // else no switch — placement only, the entries stay where they are)
             const bool ok = ring_switch_ok(d, uint32_t(rot), rota, sbo, GW.sb2(), lo, P.K, P.kmask) &&
-                            xtop - Ll <= int(P.K);
+                            xtop - Ll <= int(P.K) &&
+                            !(stale && xtop > Ll && !(meta & M_VX) &&
+                              T.entries_before(T.tick + 1) - uint64_t(xtop - Ll) < T.contig_q);
             df |= hi > Ll ? 64u : 0u;
             df |= ok ? 0u : 128u;
             if (hi <= Ll && ok) {

@@ -320,6 +320,11 @@ struct Trace {          // per-launch trace parameters (virtual clock + RNG)
   uint32_t iso_leader;  // EXT: a window isolates the lowest-id leader at its first tick
   int32_t secs;         // tick_seconds
   uint32_t period, entries;  // client event every `period` ticks, `entries` each
+  // global client entries before the first tick of the current run of
+  // consecutive raft_tick calls (no gap, no host mutation in between):
+  // entries appended from there on are regenerable from the trace RNG
+  // (k_fast.hip entry jobs), older ones are not
+  uint64_t contig_q;
   __device__ __forceinline__ Trace at_tick(int64_t t) const {
     Trace x = *this;
     x.tick = t;
