@@ -97,7 +97,7 @@ def algorithmic_bytes(R, E, crc=False):
     return 25 + 37 * (R - 1) + 12 * E * R + (4 * E * R if crc else 0)
 
 
-def lean_bytes(R, E, crc=False, segmented=False, fuse=1):
+def lean_bytes(R, E, crc=False, segmented=False, fuse=1, glx=False):
     """Algorithmic bytes per group-step of tick_lean_kernel (the dominant
     kernel of the two-pass tick, k_fast.hip) in this engine's layout: a group
     in the compressed steady state (SSYNC) holds term / LastApplied / the
@@ -107,10 +107,13 @@ def lean_bytes(R, E, crc=False, segmented=False, fuse=1):
     segment boundary 4 B when the ring has 2K physical slots) and writes the
     record 16 B + hb 4 B + this tick's entries on all R replicas, 12 E R B
     (+4 E R with a CRC32C stamp). C2: 100 B; C4 shape (R=7, 2K slots): 128 B;
-    C5: 5160 B. With `fuse` ticks per launch (tick_fused_kernel, the `fused`
-    block only) the record / meta / rotation / heartbeat bytes are moved once
-    per launch: 40 / fuse + 12 E R."""
-    return (20 + (4 if segmented else 0) + 20) / fuse + 12 * E * R + (4 * E * R if crc else 0)
+    C5: 5160 B. Under RAFT leader-isolation churn (`glx`) it also reads every
+    group's 8-B glx word with the others (LXS / SXS state and HWX's mark, one
+    round trip for every lane: k_fast.hip RAFTSTEP_LEAN_HOIST_LX): C4 136 B.
+    With `fuse` ticks per launch (tick_fused_kernel, the `fused` block only)
+    the record / meta / rotation / heartbeat bytes are moved once per launch:
+    40 / fuse + 12 E R."""
+    return (20 + (4 if segmented else 0) + (8 if glx else 0) + 20) / fuse + 12 * E * R + (4 * E * R if crc else 0)
 
 
 # SURVEY.md §8(d) workloads runnable by this bench (per GPU)
@@ -393,7 +396,8 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     # priced at the call's mean ticks per launch: K = 20 at 16 is 16 + 4)
     fused = tpl > 1 and not churn and not crc and two_pass
     mean_tpl = steps / -(-steps // tpl) if fused else 1
-    B = lean_bytes(R, E, crc, segmented="iso" in wl and wl["iso"][0] > 0, fuse=mean_tpl) if two_pass else \
+    iso = "iso" in wl and wl["iso"][0] > 0
+    B = lean_bytes(R, E, crc, segmented=iso, fuse=mean_tpl, glx=iso and wl.get("semantics", 0) == 1) if two_pass else \
         algorithmic_bytes(R, E, crc)
     kname = ("tick_fused_kernel" if fused else "tick_lean_kernel") if two_pass else "tick_fast_kernel"
     avg_kernel_s = kernel_ms / 1e3 / max(kernel_ticks, 1)   # per tick

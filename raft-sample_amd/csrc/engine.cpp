@@ -586,14 +586,17 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.hb), Gp * 4);
   A(reinterpret_cast<void**>(&e->P.xmatch), R * R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.gmeta), Gp * 2);
-  A(reinterpret_cast<void**>(&e->P.giso), Gp);
+  A(reinterpret_cast<void**>(&e->P.gseg), Gp * sizeof(GSeg));   // (giso / grota / grotb / gsb2: views, below)
   A(reinterpret_cast<void**>(&e->P.gss), Gp * sizeof(SsRec));
   A(reinterpret_cast<void**>(&e->P.glx), Gp * sizeof(LxRec));
   A(reinterpret_cast<void**>(&e->P.grot), Gp * 2);
-  A(reinterpret_cast<void**>(&e->P.grota), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.gsb), Gp * 4);
-  A(reinterpret_cast<void**>(&e->P.grotb), Gp * 2);
-  A(reinterpret_cast<void**>(&e->P.gsb2), Gp * 4);
+  if (rc == RAFT_OK) {
+    e->P.giso = Strided<uint8_t, 16>{&e->P.gseg->iso};
+    e->P.grota = Strided<uint16_t, 16>{&e->P.gseg->rota};
+    e->P.grotb = Strided<uint16_t, 16>{&e->P.gseg->rotb};
+    e->P.gsb2 = Strided<int32_t, 16>{&e->P.gseg->sb2};
+  }
   // sharded group lists (raft_device.hpp): NSHARD shards of scap entries
   const uint64_t scap = ((Gp / 256 + NSHARD - 1) / NSHARD) * 256;
   for (int q = 0; q < NWORK; ++q) {
@@ -679,15 +682,12 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetAsync(e->P.xmatch, 0, R * R * Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(e->P.gmeta), uint16_t(NO_PRIMARY), Gp,
                                            e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.giso, 0, Gp, e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->P.gseg, 0, Gp * sizeof(GSeg), e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.glst, 0, Gp, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gss, 0, Gp * sizeof(SsRec), e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.glx, 0, Gp * sizeof(LxRec), e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.grot, 0, Gp * 2, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.grota, 0, Gp * 2, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gsb, 0, Gp * 4, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.grotb, 0, Gp * 2, e->stream) : z;
-  z = z == hipSuccess ? hipMemsetAsync(e->P.gsb2, 0, Gp * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->wcount, 0, WCOUNT_WORDS * 4, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->dctr, 0, 64, e->stream) : z;
   z = z == hipSuccess ? hipHostMalloc(reinterpret_cast<void**>(&e->hdone), 64, hipHostMallocCoherent) : z;
@@ -802,7 +802,9 @@ int store_range(raft_engine* e, uint64_t g0, uint64_t n, raft_state_view* v) {
   };
   if (!rc) rc = rows2d(xm, e->P.xmatch);
   if (!rc) rc = d2h(e, meta, e->P.gmeta + g0, n);
-  if (!rc && v->iso_victim) rc = d2h(e, giso, e->P.giso + g0, n);
+  std::vector<GSeg> cold;   // the packed cold words (GSeg), split below
+  if (!rc && (v->iso_victim || v->log_term || v->log_value || v->log_crc)) rc = d2h(e, cold, e->P.gseg + g0, n);
+
   if (!rc && raft) rc = rows2d(xn, e->P.xnext);
   const bool logs = v->log_term || v->log_value || v->log_crc;
   std::vector<int32_t> ltm;
@@ -810,10 +812,8 @@ int store_range(raft_engine* e, uint64_t g0, uint64_t n, raft_state_view* v) {
   const uint64_t t0 = g0 >> 6, nt = ((g0 + n - 1) >> 6) - t0 + 1;   // ring tiles [t0, t0+nt)
   const uint64_t tile = KP * 64 * R;
   if (!rc && logs) rc = d2h(e, rot, e->P.grot + g0, n);
-  if (!rc && logs) rc = d2h(e, rota, e->P.grota + g0, n);
   if (!rc && logs) rc = d2h(e, sb, e->P.gsb + g0, n);
-  if (!rc && logs) rc = d2h(e, rotb, e->P.grotb + g0, n);
-  if (!rc && logs) rc = d2h(e, sb2, e->P.gsb2 + g0, n);
+
   std::vector<SsRec> gss;
   if (!rc) rc = d2h(e, gss, e->P.gss + g0, n);
   std::vector<LxRec> glx;
@@ -824,6 +824,18 @@ int store_range(raft_engine* e, uint64_t g0, uint64_t n, raft_state_view* v) {
   if (!rc && crcs) rc = d2h(e, lcrc, e->P.log_crc + t0 * tile, nt * tile);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(e->stream));
+  if (!cold.empty()) {   // (the packed cold words, copied above, split after the copy completed)
+    giso.resize(n);
+    rota.resize(n);
+    rotb.resize(n);
+    sb2.resize(n);
+    for (uint64_t g = 0; g < n; ++g) {
+      giso[g] = cold[g].iso;
+      rota[g] = cold[g].rota;
+      rotb[g] = cold[g].rotb;
+      sb2[g] = cold[g].sb2;
+    }
+  }
   rec_rows(blk, PL_TERM, R, n, term);
   rec_rows(blk, PL_LAST, R, n, last);
   rec_rows(blk, PL_COMMIT, R, n, commit);
@@ -1040,14 +1052,16 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.hb, hb);
   if (!rc) rc = h2d(e, e->P.xmatch, xm);
   if (!rc) rc = h2d(e, e->P.gmeta, meta);
-  if (!rc) rc = h2d(e, e->P.giso, giso);
-  const std::vector<uint16_t> rot(Gp, 0);   // loaded rings: rotation 0, one segment
+  std::vector<GSeg> cold(Gp);   // loaded rings: rotation 0, one segment; the isolation victims
+  for (uint64_t g = 0; g < Gp; ++g) {
+    cold[g] = GSeg{};
+    cold[g].iso = giso[g];
+  }
+  if (!rc) rc = h2d(e, e->P.gseg, cold);
+  const std::vector<uint16_t> rot(Gp, 0);
   const std::vector<int32_t> sb0(Gp, 0);
   if (!rc) rc = h2d(e, e->P.grot, rot);
-  if (!rc) rc = h2d(e, e->P.grota, rot);
   if (!rc) rc = h2d(e, e->P.gsb, sb0);
-  if (!rc) rc = h2d(e, e->P.grotb, rot);
-  if (!rc) rc = h2d(e, e->P.gsb2, sb0);
   if (!rc && raft) rc = h2d(e, e->P.xnext, xn);
   if (!rc && e->cfg.payload_crc) rc = h2d(e, e->P.log_crc, lcrc);
   if (!rc) rc = h2d(e, e->P.log_term, lt);
@@ -1849,16 +1863,18 @@ int raft_debug_group_words(raft_engine* e, uint64_t group, int32_t* out, uint32_
   SsRec ss{};
   LxRec lx{};
   HIPCHK(hipMemcpyAsync(&meta, e->P.gmeta + group, 2, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipMemcpyAsync(&iso, e->P.giso + group, 1, hipMemcpyDeviceToHost, e->stream));
+  GSeg cw{};
+  HIPCHK(hipMemcpyAsync(&cw, e->P.gseg + group, sizeof cw, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipMemcpyAsync(&hb, e->P.hb + group, 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipMemcpyAsync(&ss, e->P.gss + group, sizeof ss, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipMemcpyAsync(&lx, e->P.glx + group, sizeof lx, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipMemcpyAsync(&rot, e->P.grot + group, 2, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipMemcpyAsync(&rota, e->P.grota + group, 2, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipMemcpyAsync(&sb, e->P.gsb + group, 4, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipMemcpyAsync(&rotb, e->P.grotb + group, 2, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipMemcpyAsync(&sb2, e->P.gsb2 + group, 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  iso = cw.iso;
+  rota = cw.rota;
+  rotb = cw.rotb;
+  sb2 = cw.sb2;
   const int32_t w[RAFT_DEBUG_GROUP_WORDS] = {meta, iso, hb, ss.last, ss.term, ss.cl, ss.cf, lx.k, lx.dl, rot, rota, sb,
                                              rotb, sb2};
   for (uint32_t i = 0; i < n && i < RAFT_DEBUG_GROUP_WORDS; ++i) out[i] = w[i];

@@ -183,16 +183,19 @@ struct RowAcc {
 };
 template <bool LDS>
 struct WordAcc {
-  // global: the plane bases and g; LDS: the lane's slots (g unused)
+  // global: the plane bases and g; LDS: the lane's slots (g unused). The
+  // packed cold words (GSeg) are strided views in global memory.
+  template <typename T>
+  using Cold = std::conditional_t<LDS, T*, Strided<T, 16>>;
   uint16_t* meta_;
   uint16_t* rot_;
-  uint16_t* rota_;
-  uint8_t* iso_;
+  Cold<uint16_t> rota_;
+  Cold<uint8_t> iso_;
   int32_t* hb_;
   int32_t* sb_;
   SsRec* ss_;
-  uint16_t* rotb_;
-  int32_t* sb2_;
+  Cold<uint16_t> rotb_;
+  Cold<int32_t> sb2_;
   LxRec* lx_;
   uint32_t g;
   __device__ __forceinline__ uint16_t& meta() const { if constexpr (LDS) return *meta_; else return raftstep::at(meta_, g); }
@@ -966,6 +969,15 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       // RAFT: MSYNC also makes NextIndex (= match+1) and the high-water marks (= last) implicit
       int nm = sync ? (meta | M_MSYNC) : (meta & ~M_MSYNC);
       nm = (sync && hwx) ? (nm | M_HWX) : (nm & ~M_HWX);
+      if (RAFT && sync && hwx) {
+        // HWX: the highest high-water mark, for the lean kernel, in glx (unused
+        // by an HWX group, which is never LXS / SXS): it reads 8 B with the
+        // group's other words instead of the R-wide hwm row after them
+        int mx = RW.at(PL_HWM, 0);
+#pragma unroll
+        for (int r = 1; r < R; ++r) mx = max(mx, int(RW.at(PL_HWM, r)));
+        GW.lx() = LxRec{mx, 0};
+      }
       nm &= ~M_LXS;   // (a fresh record when compressed: every log at Ll+n)
       nm = keep_ss ? (nm | M_SSYNC) : (nm & ~M_SSYNC);
       if (x_fire) nm = (nm & ~M_STEADY) | M_ONECAND;
@@ -1469,8 +1481,9 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       m0 = uint16_t(mr); r0 = uint16_t(mr >> 16); ss0 = list_ss(lst, cap)[slot];
       sb0 = P.KP > P.K ? list_sb(lst, cap)[slot] : at(P.gsb, g);
       hb0 = at(P.hb, g);
-      ra0 = at(P.grota, g); rb0 = at(P.grotb, g); sc0 = at(P.gsb2, g);
-      if (T.iso_p) gi0 = at(P.giso, g);
+      const GSeg cw = P.gseg[g];   // the cold words, one 16-B load (GSeg)
+      ra0 = cw.rota; rb0 = cw.rotb; sc0 = cw.sb2;
+      if (T.iso_p) gi0 = cw.iso;
       if (uses_glx(m0)) lx0 = P.glx[g];
     }
     smeta[t] = m0; sgrot[t] = r0; sgiso[t] = gi0; shb[t] = hb0; sgss[t] = ss0; sglx[t] = lx0;
@@ -1573,13 +1586,16 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
 // Per group it reads gmeta 2 B + gss 16 B + grot 2 B and writes gss 16 B,
 // hb 4 B and the entries (12·n·R B, +4·n·R with CRC32C) as whole ring rows
 // (a drifted group: its own R-contiguous segment, or a ring segment switch).
-// A/B hooks (round 5, interleaved A/Bs in profiles/r05/ab/): LEAN_HOIST_LX=1
-// reads glx / giso for every lane with gmeta instead of after it for the lanes
-// that use them (C4: neutral, 9 B more per group); hoisting HWX's
-// high-water-mark row the same way was 35% slower (C4's per-group words then
-// no longer stay in the Infinity Cache)
+// A/B hooks (round 5, interleaved A/Bs in profiles/r05/ab/): LEAN_HOIST_LX=1 (default)
+// reads glx (and giso while a window is active) for every lane with gmeta
+// instead of after it for the lanes that use them; with HWX's highest mark
+// kept in glx too (fast_group) every lane of a C4 tick then needs one round
+// trip: C4 2.62 -> 2.71e10 (r5ab9.txt; alone, without the HWX mark in glx,
+// it was neutral: 85% of waves still waited for an HWX row). Hoisting HWX's
+// 28-B high-water-mark row instead was 35% slower (C4's per-group words then
+// no longer stay in the Infinity Cache).
 #ifndef RAFTSTEP_LEAN_HOIST_LX
-#define RAFTSTEP_LEAN_HOIST_LX 0
+#define RAFTSTEP_LEAN_HOIST_LX 1
 #endif
 template <int R, bool CRC, int SEM>
 __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, unsigned long long* stats, uint32_t* list,
@@ -1650,7 +1666,9 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       const LxRec gx = (RAFT && uses_glx(meta)) ? (hl ? gx_h : P.glx[g]) : LxRec{0, 0};
       uint32_t gi = (RAFT && T.iso_p && act && uses_glx(meta)) ? (hl ? gi_h : uint32_t(at(P.giso, g))) : 0u;
       int hwmx = 0;   // RAFT HWX: the highest high-water mark (the hwm plane)
-      if (RAFT && (meta & M_HWX)) {
+      if (RAFT && (meta & M_HWX) && hl) {
+        hwmx = gx_h.k;   // (its copy in glx, kept by the list kernel while HWX holds)
+      } else if (RAFT && (meta & M_HWX)) {
         int hw[R];
         load_row_p<R>(&at(P.hwm, rix<R>(g, 0)), hw);
         hwmx = hw[0];

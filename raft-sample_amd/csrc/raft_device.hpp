@@ -113,6 +113,28 @@ constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to c
 
 // Device layout. Per-replica scalar planes are [Gp][R] (rix below); the
 // log rings are wave tiles [Gp/64][KP][64][R] (see ring_tile below).
+// The cold per-group words — the rotations and boundary of the older ring
+// segments and the leader-isolation victims — packed into one 16-B record per
+// group (round 5): every reader that needs one of them (the list kernel's
+// staging, the general kernel, the digest) needs them all, and a scattered
+// group then costs one line for the four instead of four. The lean kernel's
+// per-group words (gmeta, gss, grot, gsb, hb, glx) stay separate planes.
+struct __attribute__((aligned(16))) GSeg {
+  uint16_t rota, rotb;   // rotation of the previous / older segment
+  int32_t sb2;           // first index of the previous segment (0: none older)
+  uint8_t iso;           // EXT leader-isolation victims (nibble per epoch parity: 8 | replica)
+  uint8_t pad[7];
+};
+// A plane of T with a byte stride S (a field of an array of records): the
+// accessors index it like a plain plane (at(), operator[]).
+template <typename T, uint32_t S>
+struct Strided {
+  T* p;
+  __host__ __device__ __forceinline__ T& operator[](uint32_t i) const {
+    return *reinterpret_cast<T*>(reinterpret_cast<char*>(p) + size_t(i) * S);
+  }
+};
+
 struct DevPlanes {
   int32_t* term;       // Node.Term                 (main.go:19)
   int32_t* last;       // Node.LastApplied=len(Log) (main.go:25)
@@ -127,14 +149,15 @@ struct DevPlanes {
   int32_t* xnext;      // RAFT mode: [R][R][Gp] NextIndex rows of further leaders
   int32_t* hwm;        // RAFT mode: [Gp][R] highest LastApplied ever (== last in REF)
   uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
-  uint8_t* giso;       // [Gp] EXT leader-isolation victims, nibble per epoch parity: 8 | replica (0 = none)
+  GSeg* gseg;          // [Gp] the packed cold words (GSeg); giso / grota / grotb / gsb2 are views of its fields
+  Strided<uint8_t, 16> giso;    // EXT leader-isolation victims, nibble per epoch parity: 8 | replica (0 = none)
   SsRec* gss;          // [Gp] the compressed state of an SSYNC group
   LxRec* glx;          // [Gp] LXS: the cut-off leader's extra entries and the earliest follower deadline
   uint16_t* grot;      // ring rotation of the current segment: entry idx >= gsb sits at slot (idx-1+grot) mod KP
-  uint16_t* grota;     // rotation of the previous segment (entries idx < gsb)
+  Strided<uint16_t, 16> grota;  // rotation of the previous segment (entries idx < gsb)
   int32_t* gsb;        // first index of the current segment (0: one segment)
-  uint16_t* grotb;     // rotation of the segment before the previous one (entries idx < gsb2)
-  int32_t* gsb2;       // first index of the previous segment (0: none older)
+  Strided<uint16_t, 16> grotb;  // rotation of the segment before the previous one (entries idx < gsb2)
+  Strided<int32_t, 16> gsb2;    // first index of the previous segment (0: none older)
   int32_t* lterm;      // [Gp][R] Log[len-1].Term: cached term of each replica's last entry
   int32_t* log_term;   // Log.Term  ring, tiles [Gp/64][KP][64][R] (ring_tile / ring_in_tile)
   int64_t* log_value;  // Log.Value ring
@@ -308,6 +331,10 @@ template <typename T>
 __device__ __forceinline__ T& at(T* base, uint32_t idx) {
   using B = std::conditional_t<std::is_const_v<T>, const char, char>;
   return *reinterpret_cast<T*>(reinterpret_cast<B*>(base) + uint32_t(idx * uint32_t(sizeof(T))));
+}
+template <typename T, uint32_t S>
+__device__ __forceinline__ T& at(Strided<T, S> base, uint32_t idx) {   // (32-bit byte offset, as above)
+  return *reinterpret_cast<T*>(reinterpret_cast<char*>(base.p) + uint32_t(idx * S));
 }
 
 struct Trace {          // per-launch trace parameters (virtual clock + RNG)

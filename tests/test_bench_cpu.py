@@ -52,10 +52,11 @@ def test_live_group_steps_small_case():
     assert bench.live_group_steps(10, 2, [1, 0, 2]) == 8 + 7 + 7
 
 
-@pytest.mark.parametrize("R,E,crc,seg,fuse,want", [(5, 1, 0, False, 1, 100), (7, 1, 0, True, 1, 128),
-                                                    (5, 64, 1, False, 1, 5160), (5, 1, 0, False, 10, 64)])
-def test_byte_accounting(R, E, crc, seg, fuse, want):
-    assert bench.lean_bytes(R, E, crc, segmented=seg, fuse=fuse) == want
+@pytest.mark.parametrize("R,E,crc,seg,fuse,glx,want", [(5, 1, 0, False, 1, False, 100), (7, 1, 0, True, 1, False, 128),
+                                                        (7, 1, 0, True, 1, True, 136), (5, 64, 1, False, 1, False, 5160),
+                                                        (5, 1, 0, False, 10, False, 64)])
+def test_byte_accounting(R, E, crc, seg, fuse, glx, want):
+    assert bench.lean_bytes(R, E, crc, segmented=seg, fuse=fuse, glx=glx) == want
 
 
 def test_survey_bytes():
