@@ -139,8 +139,9 @@ struct raft_engine {
   // RAFTSTEP_OVERLAP_GENERAL=0 runs it in line (not with the pipeline); d >= 1
   // overlaps it with the next d ticks (it catches its groups up through tick
   // t+d, the engine stream joins it before tick t+d+1). Exact for every d
-  // (tests/test_gpu_pipeline.py).
-  int overlap_general = 2;
+  // (tests/test_gpu_pipeline.py). Default 3 since round 5 (C4 +3%, C4R +5%,
+  // C4REF +6% over depth 2 in interleaved A/Bs, profiles/r05/ab/r5ab12).
+  int overlap_general = 3;
   hipStream_t gen_stream = nullptr;
   hipEvent_t gen_ev[2] = {nullptr, nullptr};   // engine -> gen_stream, gen_stream -> engine
   bool gen_pending = false;     // a general kernel is running on gen_stream

@@ -41,7 +41,8 @@ def _kw(sem):
                           ("1", "2", "8", True, "1"), ("1", "2", "3", True, "1"), ("1", "3", "8", True, "1"),
                           ("1", "2", "1", True, "1"), ("0", "2", "3", True, "1"), ("1", "2", "8", False, "1"),
                           ("1", "2", "8", True, "0"), ("1", "1", "3", True, "0"), ("1", "2", "1", True, "0"),
-                          ("1", "2", "3", False, "0")])
+                          ("1", "2", "3", False, "0"), ("1", "3", "3", True, "1"), ("1", "3", "1", True, "0"),
+                          ("1", "3", "8", False, "1"), ("0", "3", "3", True, "1")])
 def test_pipelined_tick_matches_oracle(monkeypatch, sem, pipeline, overlap, slow_every, stats, pingpong):
     monkeypatch.setenv("RAFTSTEP_PIPELINE", pipeline)
     monkeypatch.setenv("RAFTSTEP_PINGPONG", pingpong)
