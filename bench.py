@@ -97,7 +97,7 @@ def algorithmic_bytes(R, E, crc=False):
     return 25 + 37 * (R - 1) + 12 * E * R + (4 * E * R if crc else 0)
 
 
-def lean_bytes(R, E, crc=False, segmented=False, fuse=1, glx=False):
+def lean_bytes(R, E, crc=False, segmented=False, fuse=1, glx=False, shared=False):
     """Algorithmic bytes per group-step of tick_lean_kernel (the dominant
     kernel of the two-pass tick, k_fast.hip) in this engine's layout: a group
     in the compressed steady state (SSYNC) holds term / LastApplied / the
@@ -112,8 +112,13 @@ def lean_bytes(R, E, crc=False, segmented=False, fuse=1, glx=False):
     round trip for every lane: k_fast.hip RAFTSTEP_LEAN_HOIST_LX): C4 136 B.
     With `fuse` ticks per launch (tick_fused_kernel, the `fused` block only)
     the record / meta / rotation / heartbeat bytes are moved once per launch:
-    40 / fuse + 12 E R."""
-    return (20 + (4 if segmented else 0) + (8 if glx else 0) + 20) / fuse + 12 * E * R + (4 * E * R if crc else 0)
+    40 / fuse + 12 E R. With shared entries (`shared`, raft_engine_features:
+    an in-step group's entries stored once, raft_device.hpp ROT_SH) the
+    entries are written once instead of R times: 12 E (+4 E) — C2 52 B, C5
+    1064 B."""
+    copies = 1 if shared else R
+    return (20 + (4 if segmented else 0) + (8 if glx else 0) + 20) / fuse + 12 * E * copies + \
+        (4 * E * copies if crc else 0)
 
 
 # SURVEY.md §8(d) workloads runnable by this bench (per GPU)
@@ -299,6 +304,7 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     churn = wl.get("init") == "new"
     base = ctx.rank * G
     eng = Engine(device=ctx.local, ticks_per_launch=tpl, **engine_kwargs(wl, R, G, base, K, E, crc))
+    shared = eng.features()["shared_entries"]
     if ctx.comm:
         eng.comm_init(world, ctx.rank, rdist.exchange_comm_id(dist, ctx.rank, Engine.comm_unique_id))
     fi = STAT_NAMES.index("faults")
@@ -397,7 +403,8 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     fused = tpl > 1 and not churn and not crc and two_pass
     mean_tpl = steps / -(-steps // tpl) if fused else 1
     iso = "iso" in wl and wl["iso"][0] > 0
-    B = lean_bytes(R, E, crc, segmented=iso, fuse=mean_tpl, glx=iso and wl.get("semantics", 0) == 1) if two_pass else \
+    B = lean_bytes(R, E, crc, segmented=iso, fuse=mean_tpl, glx=iso and wl.get("semantics", 0) == 1,
+                   shared=shared) if two_pass else \
         algorithmic_bytes(R, E, crc)
     kname = ("tick_fused_kernel" if fused else "tick_lean_kernel") if two_pass else "tick_fast_kernel"
     avg_kernel_s = kernel_ms / 1e3 / max(kernel_ticks, 1)   # per tick
@@ -424,7 +431,9 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
                 if fused else
                 ("tick_lean_kernel, one tick per launch, compressed steady state (bench.py lean_bytes), every "
                  "group counted as taken by the lean pass; steady lines: the tick's launches (two halves of the "
-                 "groups on two streams) timed as one span per call") if two_pass else
+                 "groups on two streams) timed as one span per call" +
+                 ("; shared entries (each entry stored once for the R replicas that hold it alike)"
+                  if shared else "")) if two_pass else
                 "SURVEY.md §8(d) B(R,E), per-replica SoA"),
             "units_per_launch": units * (mean_tpl if fused else 1),
             "avg_kernel_us": avg_kernel_s * 1e6 * (mean_tpl if fused else 1),
@@ -445,6 +454,7 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
         "entries_per_tick": E, "ring_depth": K, "payload_crc32c": bool(crc), "seed": hex(wl["seed"]),
         "semantics": "RAFT (EXT, Raft paper)" if wl.get("semantics") else "REF (main.go)",
         "ticks_per_launch": tpl,
+        "storage_forms": eng.features(),
         "timing": {"repeats": reps, "median_s": elapsed, "repeat_ms_per_step": [t * 1e3 / steps for t in times]},
         "roofline": roof,
         "stats": dict(zip(STAT_NAMES, [int(x) for x in stats])),
@@ -484,11 +494,13 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
         # shape at the same size (raft_stream_probe: fresh buffers, no Raft
         # state): the practical roofline of this kernel on this box
         from raftstep import stream_probe
-        pus, pby = stream_probe(ctx.local, R, G, 10)
+        # (shared entries: the probe's ring row is one copy wide, R=1: 52 B)
+        pus, pby = stream_probe(ctx.local, 1 if shared else R, G, 10)
         roof["stream_probe"] = {"GBs": pby / pus / 1e3, "us_per_pass": pus, "bytes_per_pass": pby,
-                                "what": "raft_stream_probe: per element 20 B read in one round trip, 40 + 12R B "
-                                        "(100 B at R=5) moved, record / heartbeat / whole-ring-row stores, on "
-                                        "fresh buffers of the line's group count"}
+                                "what": "raft_stream_probe: per element 20 B read in one round trip, 40 + 12c B "
+                                        "moved (c = %d ring copies: %d B), record / heartbeat / whole-ring-row "
+                                        "stores, on fresh buffers of the line's group count"
+                                        % (1 if shared else R, 40 + 12 * (1 if shared else R))}
         roof["frac_of_stream_probe"] = achieved / (pby / pus / 1e3)
     if do_cpu:
         cb = cpu_baseline(wl, R, E, K, crc, *cpu, leader=leader, check=(digests, tick))

@@ -156,6 +156,15 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out);
 int raft_engine_destroy(raft_engine* e);
 const char* raft_last_error(void);              /* thread-local message of the last failure */
 int raft_engine_info(const raft_engine* e, raft_config* cfg_out, uint64_t* device_bytes);
+/* Storage forms this engine uses (bit set = on; results are identical either
+ * way): RAFT_FEATURE_SHARED_ENTRIES — the steady kernels store the entries
+ * every replica of an in-step group holds alike once (shared ring, copied
+ * back into the replica rings before any other reader); RAFT_FEATURE_
+ * VIRTUAL_SUFFIXES — a cut-off leader's own entries are regenerated instead
+ * of stored (RAFT leader isolation). */
+#define RAFT_FEATURE_SHARED_ENTRIES 1u
+#define RAFT_FEATURE_VIRTUAL_SUFFIXES 2u
+int raft_engine_features(const raft_engine* e, uint32_t* flags);
 
 /* NewNode x R for every group (main.go:59-76) followed by FollowerRun entry
  * (timer drawn, main.go:113-115) at virtual tick `tick0`. */
@@ -348,6 +357,8 @@ enum raft_diag_counter {
   RAFT_DIAG_LEAN_SXS_VX = 27,         /* SXS ticks whose stale leader holds a virtual suffix (whole rows) */
   RAFT_DIAG_LIST_RETURN_VX = 28,      /* stale leaders' returns with a virtual suffix (no entry copy) */
   RAFT_DIAG_LIST_LXS_VX = 29,         /* LXS entered with a virtual suffix */
+  RAFT_DIAG_LEAN_SH = 30,             /* steady ticks whose entries went to the shared ring (SH) */
+  RAFT_DIAG_LIST_SH_COPIED = 31,      /* groups in shared form whose entries the list kernel copied back */
   RAFT_DIAG_LEAN_SWITCH = 5,          /* ring segment switches */
   /* full fast-path body (list kernel / one-pass kernel): 32 + bit */
   RAFT_DIAG_LIST_LANES = 42,          /* groups looked at */

@@ -160,6 +160,10 @@ struct raft_engine {
   // before vx_tick (-1: unknown, a call failed mid-way: the engine is poisoned)
   bool vx_live = false;
   int64_t vx_tick = 0;
+  // SH (raft_device.hpp ROT_SH): groups may hold shared entries (P.sh and a
+  // lean / fused kernel has run since the last sh_flush)
+  bool sh_live = false;
+  int64_t sh_next = 0;          // the tick after the last call that may have left them
   // the current run of consecutive raft_tick calls (Trace::contig_q): it
   // starts at contig_from and continues at run_next; a call at another tick,
   // a handler batch or a state replacement starts a new one
@@ -367,6 +371,7 @@ int settle_check(raft_engine* e) {
 void state_replacing(raft_engine* e) {
   e->steady_origin = e->steady_ok = false;
   e->vx_live = false;   // (the state is being replaced: no suffix survives)
+  e->sh_live = false;   // (nor a shared entry: every rotation is rewritten)
   e->run_valid = false;
 }
 // ... and only once the new state's launches / copies have gone through
@@ -397,6 +402,21 @@ int vx_flush(raft_engine* e) {
   HIPCHK(launch_vx_flush(e->R, e->P, Qb, uint32_t(E), uint32_t(per), e->cfg.seed, e->stream));
   e->vx_live = false;
   return RAFT_OK;
+}
+
+// SH: every group's shared entries into its replica rings, before the host
+// reads or changes the rings (host views, handler batches). Exact at any time
+// (nothing is regenerated); the digest reads the shared ring itself.
+int sh_flush(raft_engine* e) {
+  if (!e->sh_live) return RAFT_OK;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  HIPCHK(launch_sh_flush(e->R, e->P, e->stream));
+  e->sh_live = false;
+  return RAFT_OK;
+}
+int ring_flush(raft_engine* e) {
+  if (int rc = vx_flush(e)) return rc;
+  return sh_flush(e);
 }
 
 hipEvent_t next_event(raft_engine* e) {
@@ -597,6 +617,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
     e->P.grota = Strided<uint16_t, 16>{&e->P.gseg->rota};
     e->P.grotb = Strided<uint16_t, 16>{&e->P.gseg->rotb};
     e->P.gsb2 = Strided<int32_t, 16>{&e->P.gseg->sb2};
+    e->P.gshf = Strided<int32_t, 16>{&e->P.gseg->shf};
   }
   // sharded group lists (raft_device.hpp): NSHARD shards of scap entries
   const uint64_t scap = ((Gp / 256 + NSHARD - 1) / NSHARD) * 256;
@@ -613,6 +634,16 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.log_term), R * K * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.log_value), R * K * Gp * 8);
   if (c.payload_crc) A(reinterpret_cast<void**>(&e->P.log_crc), R * K * Gp * 4);
+  // shared entries (raft_device.hpp ROT_SH): without EXT isolation churn (under
+  // it groups leave the steady form too often for the copy-back to pay), with
+  // slots below the rotation's flag bit; RAFTSTEP_SH=0 turns them off
+  e->P.sh = (c.isolate_per_65536 == 0 && K < ROT_SH) ? 1u : 0u;
+  if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 0) e->P.sh = 0;
+  if (e->P.sh) {
+    A(reinterpret_cast<void**>(&e->P.sh_term), K * Gp * 4);
+    A(reinterpret_cast<void**>(&e->P.sh_value), K * Gp * 8);
+    if (c.payload_crc) A(reinterpret_cast<void**>(&e->P.sh_crc), K * Gp * 4);
+  }
   if (raft) A(reinterpret_cast<void**>(&e->P.xnext), R * R * Gp * 4);
   uint32_t* d_tab = nullptr;
   A(reinterpret_cast<void**>(&d_tab), 8 * 256 * 4);
@@ -748,6 +779,12 @@ int raft_engine_info(const raft_engine* e, raft_config* cfg_out, uint64_t* devic
   if (!e) return fail(RAFT_EINVAL, "null engine");
   if (cfg_out) *cfg_out = e->cfg;
   if (device_bytes) *device_bytes = e->device_bytes;
+  return RAFT_OK;
+}
+
+int raft_engine_features(const raft_engine* e, uint32_t* flags) {
+  if (!e || !flags) return fail(RAFT_EINVAL, "null argument");
+  *flags = (e->P.sh ? RAFT_FEATURE_SHARED_ENTRIES : 0u) | (e->P.vx ? RAFT_FEATURE_VIRTUAL_SUFFIXES : 0u);
   return RAFT_OK;
 }
 
@@ -932,7 +969,7 @@ extern "C" {
 int raft_store_state(raft_engine* e, raft_state_view* v) {
   if (!e || !v) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
-  if (int rc = vx_flush(e)) return rc;
+  if (int rc = ring_flush(e)) return rc;
   return store_range(e, 0, e->cfg.groups, v);
 }
 
@@ -942,7 +979,7 @@ int raft_store_state_range(raft_engine* e, uint64_t first_group, uint64_t n_grou
     return fail(RAFT_ERANGE, "groups [%llu, +%llu) outside the engine's %llu", (unsigned long long)first_group,
                 (unsigned long long)n_groups, (unsigned long long)e->cfg.groups);
   if (int rc = settle_check(e)) return rc;
-  if (int rc = vx_flush(e)) return rc;
+  if (int rc = ring_flush(e)) return rc;
   return store_range(e, first_group, n_groups, v);
 }
 
@@ -1157,6 +1194,16 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (e->P.vx) {   // (unknown until the call has issued all its launches)
     e->vx_live = true;
     e->vx_tick = -1;
+  }
+  // shared entries across a tick gap: copied back first (a group in shared
+  // form out of the global ring phase would go to the list kernel, which a
+  // list-skipping call does not run; a drifted group without them is the lean
+  // kernel's own-segment case)
+  if (e->sh_live && first_tick != e->sh_next)
+    if (int rc = sh_flush(e)) return rc;
+  if (e->P.sh) {   // (any lean / fused launch may leave shared entries)
+    e->sh_live = true;
+    e->sh_next = first_tick + int64_t(nticks);
   }
   if (!e->run_valid || !e->run_done || first_tick != e->run_next) {   // a new run of consecutive calls
     e->contig_from = first_tick;
@@ -1581,7 +1628,7 @@ int raft_append_entries_batch(raft_engine* e, int64_t now_tick, const raft_ae_re
                               const raft_log_entry* entries, size_t n_entries_total, raft_ae_resp* out) {
   if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
-  if (int rc = vx_flush(e)) return rc;
+  if (int rc = ring_flush(e)) return rc;
   e->run_valid = false;   // host mutation: entries from here on are not the trace's
   e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
@@ -1636,7 +1683,7 @@ int raft_request_vote_batch(raft_engine* e, int64_t now_tick, const raft_vote_re
                             raft_vote_resp* out) {
   if (!e || (n && (!reqs || !out))) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
-  if (int rc = vx_flush(e)) return rc;
+  if (int rc = ring_flush(e)) return rc;
   e->run_valid = false;   // host mutation: entries from here on are not the trace's
   e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
@@ -1669,7 +1716,7 @@ int raft_group_ops_batch(raft_engine* e, int64_t now_tick, const raft_group_op* 
                          raft_op_result* out) {
   if (!e || (n && (!ops_in || !out))) return fail(RAFT_EINVAL, "null argument");
   if (int rc = settle_check(e)) return rc;
-  if (int rc = vx_flush(e)) return rc;
+  if (int rc = ring_flush(e)) return rc;
   e->run_valid = false;   // host mutation: entries from here on are not the trace's
   e->steady_origin = e->steady_ok = false;   // host mutation (the list skip needs a fresh proof)
   if (n == 0) return RAFT_OK;
@@ -1856,7 +1903,7 @@ int raft_diag_read(raft_engine* e, uint64_t* counters, uint32_t n) {
 int raft_debug_group_words(raft_engine* e, uint64_t group, int32_t* out, uint32_t n) {
   if (!e || (n && !out)) return fail(RAFT_EINVAL, "null argument");
   if (group >= e->cfg.groups) return fail(RAFT_EINVAL, "group out of range");
-  if (int rc = vx_flush(e)) return rc;
+  if (int rc = ring_flush(e)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   uint16_t meta = 0, rot = 0, rota = 0, rotb = 0;
   uint8_t iso = 0;

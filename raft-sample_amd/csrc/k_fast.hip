@@ -1397,6 +1397,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
   __shared__ uint32_t tab[CRC ? 2048 : 1];
   stage_crc_tab<CRC>(P, tab);
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  if (g < P.G) sh_materialize<R>(P, g);   // (ROT_SH: a group the lean kernel left in shared form)
   fast_group<R, CRC, SEM, false>(P, T, stats, work, work_tick, work_count, force_slow, g, tab,
                                      rows_global<R>(P, g), words_global(P, g));
 }
@@ -1485,8 +1486,15 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       ra0 = cw.rota; rb0 = cw.rotb; sc0 = cw.sb2;
       if (T.iso_p) gi0 = cw.iso;
       if (uses_glx(m0)) lx0 = P.glx[g];
+      // a group the lean kernel left in shared form (ROT_SH): its shared
+      // entries back into the R columns first (the bit is cleared in the
+      // staged rotation and written back with it)
+      if (r0 & ROT_SH) {
+        sh_copy_back<R>(P, g, ss0.last, cw.shf, r0, ra0, rb0, sb0, sc0);
+        if (P.dbg) atomicAdd(&P.dbg[31], 1ull);
+      }
     }
-    smeta[t] = m0; sgrot[t] = r0; sgiso[t] = gi0; shb[t] = hb0; sgss[t] = ss0; sglx[t] = lx0;
+    smeta[t] = m0; sgrot[t] = uint16_t(r0 & ~ROT_SH); sgiso[t] = gi0; shb[t] = hb0; sgss[t] = ss0; sglx[t] = lx0;
     sgrota[t] = ra0; sgrotb[t] = rb0; sgsb[t] = sb0; sgsb2[t] = sc0;
     __syncthreads();
     {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
@@ -1626,6 +1634,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   uint32_t act = 0, starting = 0, im = 0;
   if (T.iso_p) im = iso_windows<R>(key, T, &act, &starting);
   bool held = false;
+  bool shw = false;             // SH: this tick's entries go to the shared ring (ROT_SH)
   uint32_t p_mr = 0;            // a passed group's words as read here, for its list entry
   int32_t p_sb = 0;
   SsRec p_ss{0, 0, 0, 0};
@@ -1658,7 +1667,11 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     held = (lflags & 1) && at(P.glst, g) != 0;
     const int c = meta & 0xF;
     const bool skip = held || (meta & M_DEFER) || ((meta >> 4) & 7);   // carried / pending catch-up / frozen group
-    take = !skip && (meta & M_SSYNC) && c < R && g != P.dbg_pass;   // (test knob: pass one group on)
+    // (a group in shared form is in the plain normal class: anything else,
+    // which only the list / general kernels could have set, goes to the list)
+    const bool shm = (uint32_t(rot) & ROT_SH) != 0u;
+    take = !skip && (meta & M_SSYNC) && c < R && g != P.dbg_pass &&   // (test knob: pass one group on)
+           !(shm && (uses_glx(meta) || (RAFT && (meta & M_HWX))));
     pass = !skip && !take;
     df |= (!skip && g == P.dbg_pass) ? 1u << 24 : 0u;
     df |= skip ? 1u : 0u;
@@ -1793,6 +1806,10 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
           if (sw) sw_d = int(d);
           else w_slot = wph;
         }
+        // SH: a group in step at the global phase writes one shared copy; one
+        // already in shared form that would not (a drift after a tick gap) is
+        // the list kernel's (which copies its shared entries back first)
+        if (shm && (sw_d || w_slot >= 0)) take = false;
         if constexpr (CRC) {   // EXT: every follower verifies the stamp of each entry it received
           if (take && n) {
             uint32_t cm = 0;   // followers whose message is corrupted this tick: the list kernel (rejection)
@@ -1806,6 +1823,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
             if (cm) take &= crc_reject_mask(tab, crc_term_state(tab, s.term), vb, n, cm) == 0u;
           }
         }
+        shw = P.sh && take && n > 0 && w_slot < 0 && !sw_d && !(RAFT && (meta & M_HWX));   // (in phase only)
         nl = L + n;
         if (RAFT ? nl > s.cl : (2 * (R - 1) > R && nl > s.cl)) cl2 = nl;
         cf2 = s.cl > s.cf ? s.cl : s.cf;
@@ -1826,6 +1844,10 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
           if (hbw) at(P.hb, g) = T.now;                   // timer.Reset(d) of every follower
         }
         if (RAFT && lxs) P.glx[g] = LxRec{gx.k + n, gx.dl};   // (SXS: unchanged, both logs grow by n)
+        if (shw && !shm) {   // SH from this tick's first entry on
+          at(P.grot, g) = uint16_t(uint32_t(rot) | ROT_SH);
+          at(P.gshf, g) = L + 1;
+        }
         if (hwx_clear) at(P.gmeta, g) = uint16_t(meta & ~M_HWX);
         if (sw_d) {   // the new segment starts at this tick's first entry
           if (sw_rota >= 0) at(P.grotb, g) = uint16_t(sw_rota);   // (else the older segments are dead)
@@ -1842,6 +1864,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         pass = true;
         w_slot = -1;
         x_slot = -1;
+        shw = false;
       }
     }
   }
@@ -1851,6 +1874,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   // column carries its own entry (term T-1, its value stream) — in the common
   // row when it is in the global phase (xrow), else at its own slot (wx).
   bool wr = take && n && w_slot < 0;
+  const bool wsh = wr && shw;   // SH: the shared ring's row instead (ROT_SH)
+  wr = wr && !shw;
   bool wd = take && n && w_slot >= 0;
   const bool xrow = RAFT && !CRC && take && n && x_slot == ph;
   bool wx = RAFT && !CRC && take && n && x_slot >= 0 && !xrow;
@@ -1862,12 +1887,16 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     if (P.diag & 4u) holes = false;
     if (P.diag & 8u) wx = false;
   }
-  if (__ballot(wr || wd || xrow || wx)) {
+  if (__ballot(wr || wd || xrow || wx || wsh)) {
     const int lane = threadIdx.x & 63;
-    const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g), P.KP, R);
+    const uint32_t g0 = __builtin_amdgcn_readfirstlane(g);
+    const uint64_t tb = ring_tile(g0, P.KP, R);
     int32_t* const rt = P.log_term + tb;
     int64_t* const rv = P.log_value + tb;
     uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
+    const bool anyrow = __ballot(wr || xrow || !holes) != 0ull;   // (wave-uniform: a whole-row lane in the wave)
+    const bool anysh = __ballot(wsh) != 0ull;
+    const uint64_t shb = anysh ? sh_tile(g0, P.KP) : 0u;
     uint32_t cs = 0;
     if constexpr (CRC) cs = crc_term_state(tab, w_term);
     const bool anyx = RAFT && !CRC && __ballot(xrow) != 0ull;   // (wave-uniform)
@@ -1890,8 +1919,15 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       int64_t xv = 0;
       if (RAFT && !CRC && x_slot >= 0) xv = int64_t(sm64(x_vb ^ uint64_t(uint32_t(e))) >> 1);
       const int xlo = int(uint32_t(uint64_t(xv))), xhi = int(uint32_t(uint64_t(xv) >> 32));
+      if (wsh) {   // SH: one copy, 64 consecutive groups' entries per wave row
+        const uint32_t so = uint32_t((ph + e) & int(P.kmask)) * 64u + uint32_t(lane);
+        ring_st(P.sh_term + shb, so, w_term);
+        ring_st(P.sh_value + shb, so, v);
+        if constexpr (CRC) ring_st(P.sh_crc + shb, so, stamp);
+      }
 #pragma unroll
       for (int k = 0; k < R; ++k) {
+        if (!anyrow) break;
         const int lo = __shfl(vlo, k_src[k]), hi = __shfl(vhi, k_src[k]);
         uint32_t sk = 0;
         if constexpr (CRC) sk = uint32_t(__shfl(int(stamp), k_src[k]));
@@ -1940,6 +1976,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       const uint64_t b = __ballot((df >> k) & 1u);
       if ((threadIdx.x & 63) == 0 && b) atomicAdd(&P.dbg[k], (unsigned long long)__popcll(b));
     }
+    const uint64_t bsh = __ballot(wsh);   // SH: ticks written to the shared ring
+    if ((threadIdx.x & 63) == 0 && bsh) atomicAdd(&P.dbg[30], (unsigned long long)__popcll(bsh));
   }
   if (held) at(P.glst, g) = uint8_t(0);   // (the mark read above)
   // the rest go to the list kernel: block-local prefix, one atomic per block
@@ -2006,6 +2044,7 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
   const uint64_t key = group_key(T.seed, P.gbase + g);
   bool live = false, pass = false;
   int c = 0, rot = 0, L = 0, term = 0, cl = 0, cf = 0, done = 0;
+  int sh_from = -1;   // SH: the first entry this launch wrote, for a group entering shared form
   SsRec s0{0, 0, 0, 0};
   if (g < P.G) {
     const int meta = at(P.gmeta, g);
@@ -2021,10 +2060,12 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
     }
   }
   const int lane = threadIdx.x & 63;
-  const uint64_t tb = ring_tile(__builtin_amdgcn_readfirstlane(g), P.KP, R);
+  const uint32_t g0 = __builtin_amdgcn_readfirstlane(g);
+  const uint64_t tb = ring_tile(g0, P.KP, R);
   int32_t* const rt = P.log_term + tb;
   int64_t* const rv = P.log_value + tb;
   uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
+  const uint64_t shb = P.sh ? sh_tile(g0, P.KP) : 0u;   // SH: every live group writes the shared ring (ROT_SH)
   int k_src[R];
 #pragma unroll
   for (int k = 0; k < R; ++k) k_src[k] = (k * 64 + lane) / R;
@@ -2039,6 +2080,7 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
     int committed = 0;
     if (take) {
       const int nl = L + n;
+      if (P.sh && n && sh_from < 0 && !(uint32_t(rot) & ROT_SH)) sh_from = L + 1;
       const int cl2 = (RAFT ? nl > cl : (2 * (R - 1) > R && nl > cl)) ? nl : cl;
       cf = cl > cf ? cl : cf;
       committed = cl2 - cl;
@@ -2061,6 +2103,15 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
         const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
         uint32_t stamp = 0;
         if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+        if (P.sh) {   // (wave-uniform)
+          if (take) {
+            const uint32_t so = uint32_t((ph + e) & int(P.kmask)) * 64u + uint32_t(lane);
+            ring_st(P.sh_term + shb, so, term);
+            ring_st(P.sh_value + shb, so, v);
+            if constexpr (CRC) ring_st(P.sh_crc + shb, so, stamp);
+          }
+          continue;
+        }
         const uint32_t row = uint32_t((ph + e) & int(P.kmask)) * 64u * R;
         const int vlo = int(uint32_t(uint64_t(v))), vhi = int(uint32_t(uint64_t(v) >> 32));
 #pragma unroll
@@ -2095,6 +2146,10 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
   if (done) {   // the record and every follower's timer as of the last tick taken
     if (L != s0.last || cl != s0.cl || cf != s0.cf) P.gss[g] = SsRec{L, term, cl, cf};
     at(P.hb, g) = T.at_tick(T.tick + done - 1).now;
+  }
+  if (sh_from >= 0) {   // SH from that entry on
+    at(P.grot, g) = uint16_t(uint32_t(rot) | ROT_SH);
+    at(P.gshf, g) = sh_from;
   }
   if (P.dbg) {   // diagnostics (lean kernel counters): lanes x ticks, compressed ticks taken, passed on
     const uint64_t b0 = __ballot(g < P.G), b1 = __ballot(pass);

@@ -125,12 +125,30 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
       const uint64_t rb = ring_tile(g, P.KP, R);
       const uint32_t rot = at(P.grot, g), rota = at(P.grota, g), rotb = at(P.grotb, g);
       const int sb = at(P.gsb, g), sb2 = at(P.gsb2, g);
+      // SH (ROT_SH): entries from shf on are read from the shared ring (the
+      // digest of the materialised state, without materialising it)
+      const int shf = (P.sh && (rot & ROT_SH)) ? at(P.gshf, g) : 2147483647;
+      const uint64_t shb = sh_tile(g, P.KP);
 #pragma unroll 1
       for (int idx = hwm > int(P.K) ? hwm - int(P.K) + 1 : 1; idx <= l; ++idx) {
-        const uint32_t o = ring_in_tile(g, R, ring_slot(idx, rot, rota, rotb, sb, sb2, P.kmask), uint32_t(r));
-        h = dg_mix(h, lo32(at(P.log_term + rb, o)) | (lo32(idx) << 32));
-        h = dg_mix(h, uint64_t(at(P.log_value + rb, o)));
-        h = dg_mix(h, P.crc_on ? uint64_t(at(P.log_crc + rb, o)) : 0ull);
+        const uint32_t slot = ring_slot(idx, rot, rota, rotb, sb, sb2, P.kmask);
+        int32_t lt;
+        int64_t lv;
+        uint32_t lc = 0;
+        if (idx >= shf) {
+          const uint32_t so = sh_in_tile(g, slot);
+          lt = at(P.sh_term + shb, so);
+          lv = at(P.sh_value + shb, so);
+          if (P.crc_on) lc = at(P.sh_crc + shb, so);
+        } else {
+          const uint32_t o = ring_in_tile(g, R, slot, uint32_t(r));
+          lt = at(P.log_term + rb, o);
+          lv = at(P.log_value + rb, o);
+          if (P.crc_on) lc = at(P.log_crc + rb, o);
+        }
+        h = dg_mix(h, lo32(lt) | (lo32(idx) << 32));
+        h = dg_mix(h, uint64_t(lv));
+        h = dg_mix(h, P.crc_on ? uint64_t(lc) : 0ull);
       }
     }
     h = dg_mix(h, uint64_t(fault));
@@ -371,6 +389,16 @@ __global__ __launch_bounds__(256) void vx_flush_kernel(DevPlanes P, uint64_t Qb,
 hipError_t launch_vx_flush(int R, const DevPlanes& P, uint64_t Qb, uint32_t E, uint32_t period, uint64_t seed,
                            hipStream_t s) {
   RAFT_DISPATCH_R(R, hipLaunchKernelGGL(vx_flush_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P, Qb, E, period, seed));
+  return hipGetLastError();
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void sh_flush_kernel(DevPlanes P) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  if (g < P.G) sh_materialize<R>(P, g);
+}
+hipError_t launch_sh_flush(int R, const DevPlanes& P, hipStream_t s) {
+  RAFT_DISPATCH_R(R, hipLaunchKernelGGL(sh_flush_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P));
   return hipGetLastError();
 }
 

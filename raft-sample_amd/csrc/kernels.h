@@ -125,6 +125,8 @@ hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out
 hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s);
 hipError_t launch_vx_flush(int R, const DevPlanes& P, uint64_t Qb, uint32_t E, uint32_t period, uint64_t seed,
                            hipStream_t s);
+// SH (raft_device.hpp ROT_SH): every group's shared entries into its replica rings
+hipError_t launch_sh_flush(int R, const DevPlanes& P, hipStream_t s);
 hipError_t launch_stream_probe(int R, const uint16_t* a, SsRec* b, const uint16_t* c, int32_t* d, int32_t* rt,
                                int64_t* rv, uint32_t n, uint32_t slot, uint32_t kslots, hipStream_t s,
                                uint32_t mode = 0);

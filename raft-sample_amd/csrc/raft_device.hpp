@@ -123,7 +123,8 @@ struct __attribute__((aligned(16))) GSeg {
   uint16_t rota, rotb;   // rotation of the previous / older segment
   int32_t sb2;           // first index of the previous segment (0: none older)
   uint8_t iso;           // EXT leader-isolation victims (nibble per epoch parity: 8 | replica)
-  uint8_t pad[7];
+  uint8_t pad[3];
+  int32_t shf;           // SH (ROT_SH): the first index whose entries live in the shared ring
 };
 // A plane of T with a byte stride S (a field of an array of records): the
 // accessors index it like a plain plane (at(), operator[]).
@@ -162,6 +163,13 @@ struct DevPlanes {
   int32_t* log_term;   // Log.Term  ring, tiles [Gp/64][KP][64][R] (ring_tile / ring_in_tile)
   int64_t* log_value;  // Log.Value ring
   uint32_t* log_crc;   // EXT: CRC32C stamp ring (payload_crc only)
+  // SH (ROT_SH): one shared copy of the entries every replica of an SSYNC
+  // group holds alike, tiles [Gp/64][KP][64] (sh_tile / sh_in_tile), the
+  // same slots as the replica rings; null when P.sh is off
+  int32_t* sh_term;
+  int64_t* sh_value;
+  uint32_t* sh_crc;
+  Strided<int32_t, 16> gshf;    // GSeg::shf
   const uint32_t* crc_tab;  // 8 x 256 slice-by-8 CRC32C tables
   uint32_t crc_on;     // payload_crc
   uint32_t corrupt_p;  // EXT corruption probability / 65536
@@ -187,6 +195,9 @@ struct DevPlanes {
   // (RAFTSTEP_VX=0 turns it off); the fast paths then give a group entering
   // LXS a virtual suffix
   uint32_t vx;
+  // SH (ROT_SH) enabled: steady groups' entries go to the shared ring (no
+  // EXT isolation configured, KP < 2^15; RAFTSTEP_SH=0 turns it off)
+  uint32_t sh;
   uint32_t diag;       // timing-only diagnostics (RAFTSTEP_DIAG_LEAN; results are wrong when set): 1 = drifted
                        // lanes of the lean kernel skip their ring writes, 2 = they write the wave's common row
                        // (list kernel: 32 = staging alone, 64 = no tick, 128 = no ring writes / copies)
@@ -296,6 +307,24 @@ __device__ __forceinline__ uint64_t ring_tile(uint32_t g, uint32_t K, uint32_t R
 __device__ __forceinline__ uint32_t ring_in_tile(uint32_t g, uint32_t R, uint32_t slot, uint32_t r) {
   return (slot * 64u + (g & 63u)) * R + r;
 }
+
+// SH — shared entries of a group in step (round 5). While an SSYNC group is
+// taken by the lean kernel's normal class every tick, all R logs receive the
+// same entries (the leader's client append and the AppendEntries every
+// follower accepts, main.go:121-156, 327-372), so the lean kernel stores one
+// copy of each in the shared ring (12 B per entry instead of 12·R, +4 / +4·R
+// with CRC32C) and marks the group: bit 15 of grot (ROT_SH; slot arithmetic
+// masks rotations with kmask < 2^15, so the bit never moves a slot) and, on
+// entry, GSeg::shf = the first shared index. Entries idx >= shf of every log
+// then live in the shared ring at the replica rings' slot, and the replica
+// rings' slots there are stale. Every other reader or writer of the group's
+// rings first copies the live shared entries back into the R columns and
+// clears the bit (sh_materialize: the list, one-pass and general kernels when
+// they load a group; the engine's flush before host reads, digests and
+// handler batches). Nothing is regenerated: a flush at any time is exact.
+constexpr uint32_t ROT_SH = 0x8000u;
+__device__ __forceinline__ uint64_t sh_tile(uint32_t g, uint32_t KP) { return uint64_t(g >> 6) * (KP * 64u); }
+__device__ __forceinline__ uint32_t sh_in_tile(uint32_t g, uint32_t slot) { return slot * 64u + (g & 63u); }
 
 // Addressing: every access is a wave-uniform base (SGPRs: the plane, or a
 // ring tile) plus a 32-bit per-lane byte offset, so the compiler emits
@@ -550,6 +579,40 @@ __device__ __forceinline__ void vx_materialize(const DevPlanes& P, uint32_t g, u
     at(P.log_value + tb, o) = vx_value(kv, Qb - uint64_t(xtop - idx) - 1u, E, period);
   }
   at(P.gmeta, g) = uint16_t(meta & ~M_VX);
+}
+
+// SH (see ROT_SH): the live shared entries [max(shf, L-K+1), L] of group g
+// (every log of length L: SSYNC, normal class) into all R replica columns.
+// The caller clears ROT_SH in grot (or in its staged copy).
+template <int R>
+__device__ __forceinline__ void sh_copy_back(const DevPlanes& P, uint32_t g, int L, int shf, uint32_t rot, uint32_t rota,
+                                             uint32_t rotb, int sb, int sb2) {
+  const uint64_t tb = ring_tile(g, P.KP, R), sb_t = sh_tile(g, P.KP);
+  const int lo = max(shf, L - int(P.K) + 1);
+  for (int idx = lo; idx <= L; ++idx) {
+    const uint32_t slot = ring_slot(idx, rot, rota, rotb, sb, sb2, P.kmask);
+    const uint32_t so = sh_in_tile(g, slot), o = ring_in_tile(g, R, slot, 0u);
+    const int32_t t = at(P.sh_term + sb_t, so);
+    const int64_t v = at(P.sh_value + sb_t, so);
+    const uint32_t c = P.crc_on ? at(P.sh_crc + sb_t, so) : 0u;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      at(P.log_term + tb, o + uint32_t(r)) = t;
+      at(P.log_value + tb, o + uint32_t(r)) = v;
+      if (P.crc_on) at(P.log_crc + tb, o + uint32_t(r)) = c;
+    }
+  }
+}
+// ... reading every word from memory and clearing the bit (general kernels,
+// one-pass kernel, the engine's flush)
+template <int R>
+__device__ __forceinline__ void sh_materialize(const DevPlanes& P, uint32_t g) {
+  if (!P.sh) return;
+  const uint32_t rot = at(P.grot, g);
+  if (!(rot & ROT_SH)) return;
+  const GSeg cw = P.gseg[g];
+  sh_copy_back<R>(P, g, P.gss[g].last, cw.shf, rot, cw.rota, cw.rotb, at(P.gsb, g), cw.sb2);
+  at(P.grot, g) = uint16_t(rot & ~ROT_SH);
 }
 
 // Group context: the R replicas of one group, in registers. SEM selects the

@@ -35,6 +35,7 @@ DIAG = {
     "lean_lxs_whole_row": 21, "lean_hwx": 22, "lean_passed": 23, "lean_forced": 24, "lean_switch": 5,
     "lean_sxs": 25, "lean_sxs_stale_in_row": 26, "list_sxs_materialised": 61, "list_sxs_entered": 62,
     "list_stale_moved": 63, "lean_sxs_vx": 27, "list_return_vx": 28, "list_lxs_vx": 29,
+    "lean_sh": 30, "list_sh_copied": 31,
     "list_lanes": 42, "list_deferred": 33, "list_isolation": 34, "list_switch": 37, "list_quiet": 48,
     "list_isolated_leader": 49, "list_ssync": 50, "list_election": 51, "list_first_round": 52,
     "list_return": 53, "list_return_trunc": 54, "list_stale": 55, "list_hwx": 56, "list_three_seg": 57,
@@ -190,6 +191,7 @@ SIGNATURES = {
     "raft_engine_destroy": (C.c_int, [P]),
     "raft_last_error": (C.c_char_p, []),
     "raft_engine_info": (C.c_int, [P, P, P]),
+    "raft_engine_features": (C.c_int, [P, P]),
     "raft_init_new_nodes": (C.c_int, [P, C.c_int64]),
     "raft_init_steady": (C.c_int, [P, C.c_int32, C.c_int64]),
     "raft_load_state": (C.c_int, [P, P]),
@@ -223,7 +225,8 @@ SIGNATURES = {
 
 # measurement / diagnostics entry points added in round 5: an older build
 # loaded through RAFTSTEP_LIB (A/B runs) may lack them
-OPTIONAL = ("raft_debug_diag_mode", "raft_stream_probe")
+OPTIONAL = ("raft_debug_diag_mode", "raft_stream_probe", "raft_engine_features")
+FEATURE_SHARED_ENTRIES, FEATURE_VIRTUAL_SUFFIXES = 1, 2   # raft_engine_features (include/raftstep.h)
 
 
 def bind(lib):

@@ -95,6 +95,15 @@ class Engine:
         _check(self.lib.raft_engine_info(self.h, None, C.byref(b)))
         return b.value
 
+    def features(self):
+        """Storage forms in use (raft_engine_features): shared_entries,
+        virtual_suffixes. Results are identical either way."""
+        f = C.c_uint32()
+        if hasattr(self.lib, "raft_engine_features"):
+            _check(self.lib.raft_engine_features(self.h, C.byref(f)))
+        return {"shared_entries": bool(f.value & abi.FEATURE_SHARED_ENTRIES),
+                "virtual_suffixes": bool(f.value & abi.FEATURE_VIRTUAL_SUFFIXES)}
+
     # -- state ---------------------------------------------------------
     def init_new_nodes(self, tick0=0):
         _check(self.lib.raft_init_new_nodes(self.h, tick0))
