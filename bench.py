@@ -66,6 +66,8 @@ ENV_KNOBS = {
     "RAFTSTEP_OVERLAP_GENERAL": "exact: 0 = general kernel in line, d = overlapping d ticks (tests/test_gpu_pipeline.py)",
     "RAFTSTEP_SPLIT_STEADY": "exact: 0 = one launch per steady tick instead of two halves on two streams "
                              "(tests/test_gpu_engine_checks.py)",
+    "RAFTSTEP_SH": "exact: 0 = no shared entries (every entry in the R replica rings), 2 = shared entries under "
+                   "isolation churn too (tests/test_gpu_sh.py)",
     "RAFTSTEP_VX": "exact: 0 = no virtual log suffixes (C4's stale leaders' entries stored and copied back at "
                    "their return; tests/test_gpu_fullsize.py, test_gpu_pipeline.py)",
     "RAFTSTEP_DEBUG_WORK": "exact: prints worklist sizes, synchronises (in-line form)",
@@ -304,7 +306,8 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     churn = wl.get("init") == "new"
     base = ctx.rank * G
     eng = Engine(device=ctx.local, ticks_per_launch=tpl, **engine_kwargs(wl, R, G, base, K, E, crc))
-    shared = eng.features()["shared_entries"]
+    feats = eng.features()
+    shared = feats["shared_entries"]
     if ctx.comm:
         eng.comm_init(world, ctx.rank, rdist.exchange_comm_id(dist, ctx.rank, Engine.comm_unique_id))
     fi = STAT_NAMES.index("faults")
@@ -454,7 +457,7 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
         "entries_per_tick": E, "ring_depth": K, "payload_crc32c": bool(crc), "seed": hex(wl["seed"]),
         "semantics": "RAFT (EXT, Raft paper)" if wl.get("semantics") else "REF (main.go)",
         "ticks_per_launch": tpl,
-        "storage_forms": eng.features(),
+        "storage_forms": feats,
         "timing": {"repeats": reps, "median_s": elapsed, "repeat_ms_per_step": [t * 1e3 / steps for t in times]},
         "roofline": roof,
         "stats": dict(zip(STAT_NAMES, [int(x) for x in stats])),

@@ -639,6 +639,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   // slots below the rotation's flag bit; RAFTSTEP_SH=0 turns them off
   e->P.sh = (c.isolate_per_65536 == 0 && K < ROT_SH) ? 1u : 0u;
   if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 0) e->P.sh = 0;
+  if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 2 && K < ROT_SH) e->P.sh = 1;   // (also under churn)
   if (e->P.sh) {
     A(reinterpret_cast<void**>(&e->P.sh_term), K * Gp * 4);
     A(reinterpret_cast<void**>(&e->P.sh_value), K * Gp * 8);
