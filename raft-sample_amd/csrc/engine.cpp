@@ -106,7 +106,7 @@ struct raft_engine {
   DevPlanes P{};
   std::vector<void*> allocs;
   uint64_t device_bytes = 0;
-  // per-tick statistics: atomic targets [cap][STAT_SLOTS][NSTAT] u64 (kept
+  // per-tick statistics: atomic targets [cap][STAT_TICK] u64 (kept
   // zero between calls by the reduce kernel) and the reduced per-tick records
   // [cap][NSTAT] (the 64 B per tick that RCCL sums across GPUs)
   unsigned long long* hist = nullptr;
@@ -163,6 +163,10 @@ struct raft_engine {
   // SH (raft_device.hpp ROT_SH): groups may hold shared entries (P.sh and a
   // lean / fused kernel has run since the last sh_flush)
   bool sh_live = false;
+  // the running call's first tick and whether its ticks run the lean (or
+  // fused) kernel over every group (the base of its statistics)
+  int64_t call_t0 = 0;
+  bool call_lean = false;
   int64_t sh_next = 0;          // the tick after the last call that may have left them
   // the current run of consecutive raft_tick calls (Trace::contig_q): it
   // starts at contig_from and continues at run_next; a call at another tick,
@@ -331,7 +335,7 @@ int ensure_hist(raft_engine* e, uint32_t n) {
   e->hist_cap = 0;
   e->last_stats_n = 0;
   uint32_t cap = std::max<uint32_t>(n, 64);
-  const size_t hb = size_t(cap) * STAT_SLOTS * NSTAT * 8;
+  const size_t hb = size_t(cap) * STAT_TICK * 8;
   const size_t tb = size_t(cap + 2) * NSTAT * 8;   // + the two check records (raft_engine::tstat)
   HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->hist), hb));
   HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->tstat), tb));
@@ -1123,7 +1127,11 @@ static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1, const Ca
                               hipStream_t s = nullptr, bool call_end = false) {
   if (!s) s = e->stream;
   const uint32_t n = w1 - w0 + 1;
-  HIPCHK(launch_stats_reduce(e->hist + size_t(w0) * STAT_SLOTS * NSTAT, e->tstat + size_t(w0) * NSTAT, n, s, chk));
+  // (the lean / fused kernels' statistics are exceptions to a base of every
+  // group taking a normal tick: tick_common.hpp lean_stats)
+  const LeanBase lb{e->call_lean ? e->cfg.groups : 0ull, e->call_t0 + int64_t(w0), e->cfg.entries_per_tick,
+                    e->cfg.client_period, uint32_t(e->R), e->cfg.semantics == RAFT_SEM_RAFT ? 1u : 0u};
+  HIPCHK(launch_stats_reduce(e->hist + size_t(w0) * STAT_TICK, e->tstat + size_t(w0) * NSTAT, n, lb, s, chk));
   if (!e->comm) return RAFT_OK;
   while (e->comm_ev.size() < 2) {
     hipEvent_t x;
@@ -1182,7 +1190,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     // its kernels (on any of the engine's streams) are done, or the next
     // call's stats would include them
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemsetAsync(e->hist, 0, size_t(e->hist_dirty) * STAT_SLOTS * NSTAT * 8, e->stream));
+    HIPCHK(hipMemsetAsync(e->hist, 0, size_t(e->hist_dirty) * STAT_TICK * 8, e->stream));
     e->hist_dirty = 0;
   }
   // (the per-tick records need nticks slots; the check records exist at any capacity)
@@ -1223,6 +1231,8 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   e->n_ticks += nticks;
   if (skip_list) e->n_skip_ticks += nticks;
   const bool two = e->two_pass && !e->force_general;
+  e->call_t0 = first_tick;
+  e->call_lean = two;
   const bool pipe = two && !skip_list && !e->debug_work && e->pipeline;
   const bool pp = pipe && e->pingpong;
   if (e->debug_pipe)
@@ -1267,7 +1277,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   for (uint32_t i = 0; i < nticks; ++i) {
     const int64_t t = first_tick + int64_t(i);
     const Trace T = make_trace(e, t);
-    unsigned long long* st = stats ? e->hist + size_t(i) * STAT_SLOTS * NSTAT : nullptr;
+    unsigned long long* st = stats ? e->hist + size_t(i) * STAT_TICK : nullptr;
     // worklist counter of this window; zeroed by the previous general kernel
     // (or at engine creation), so no per-call memset
     uint32_t* cnt = e->wcount + (e->wpar % NWORK) * SHARD_WORDS;
@@ -1333,7 +1343,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
       ListNext nx{};
       if (carry) {   // tick t+1: its stats record, the worklist of its window
         const int np = int((e->wpar + ((i + 1) % e->slow_every == 0 ? 1u : 0u)) % NWORK);
-        nx = ListNext{stats ? st + size_t(STAT_SLOTS) * NSTAT : nullptr, e->work[np], e->work_tick[np],
+        nx = ListNext{stats ? st + size_t(STAT_TICK) : nullptr, e->work[np], e->work_tick[np],
                       e->wcount + np * SHARD_WORDS};
       }
       // (the call's last list kernel zeroes nothing: list L+2 then still
@@ -1491,7 +1501,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
     // its pinned copy is verified by the next call (settle_check)
     const CallCheck chk{e->wcount, int((e->wpar + NWORK - 1) % NWORK), 1, e->tstat + size_t(e->hist_cap + 1) * NSTAT,
                         int((e->lpar + 2) % 3), nullptr, nullptr, nullptr, 0u};
-    HIPCHK(launch_stats_reduce(nullptr, nullptr, 0, e->stream, &chk));
+    HIPCHK(launch_stats_reduce(nullptr, nullptr, 0, LeanBase{}, e->stream, &chk));
     const size_t off = size_t(e->hist_cap + 1) * NSTAT;
     HIPCHK(hipMemcpyAsync(e->hrb + off, e->tstat + off, NSTAT * 8, hipMemcpyDeviceToHost, e->stream));
     if (!e->chk_ev) HIPCHK(hipEventCreateWithFlags(&e->chk_ev, hipEventDisableTiming));

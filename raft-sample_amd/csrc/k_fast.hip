@@ -2004,21 +2004,12 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     list_ss(list, cap)[off] = p_ss;
     if (lflags & 2) at(P.glst, g) = uint8_t(1);   // the list kernel carries it through the next tick too
   }
-  if (stats) {
-    const int t = take ? 1 : 0;
-    if constexpr (RAFT) {
-      // (an LXS tick: every AppendEntries of the cut-off leader dropped; an SXS
-      // tick: the one to the stale leader and every one it sends)
-      const int v[5] = {committed, (take && !lxs) ? (sxs ? R - 2 : R - 1) : 0,
-                        (take && lxs) ? R - 1 : ((take && sxs) ? R : 0), t, 0};
-      const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
-      block_stats<5>(v, idx, stats);
-    } else {
-      const int v[4] = {committed, t * (R - 1), 0, t};
-      const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
-      block_stats<4>(v, idx, stats);
-    }
-  }
+  // (packed, tick_common.hpp lean_stats: a normal tick R-1 accepted
+  // AppendEntries; an LXS tick every AppendEntries of the cut-off leader
+  // dropped; an SXS tick the one to the stale leader and every one it sends)
+  if (stats)
+    lean_stats<RAFT>(g < P.G, committed - lean_base_committed(RAFT, R, uint32_t(n)), take && !lxs && !sxs,
+                     take && lxs, take && sxs, stats);
 }
 
 // Fused steady ticks (the steady-state list skip, engine.cpp): every live
@@ -2128,20 +2119,9 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
         }
       }
     }
-    if (stats) {   // tick j's record
-      unsigned long long* st = stats + size_t(j) * STAT_SLOTS * NSTAT;
-      const int t1 = take ? 1 : 0;
-      if constexpr (RAFT) {
-        const int v[5] = {committed, t1 * (R - 1), 0, t1, 0};
-        const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
-        block_stats<5>(v, idx, st);
-      } else {
-        const int v[4] = {committed, t1 * (R - 1), 0, t1};
-        const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
-        block_stats<4>(v, idx, st);
-      }
-      __syncthreads();   // (block_stats' LDS words are reused by the next tick)
-    }
+    if (stats)   // tick j's record (exceptions: normal ticks only)
+      lean_stats<RAFT>(g < P.G, committed - lean_base_committed(RAFT, R, uint32_t(n)), take, false, false,
+                       stats + size_t(j) * STAT_TICK);
   }
   if (done) {   // the record and every follower's timer as of the last tick taken
     if (L != s0.last || cl != s0.cl || cf != s0.cf) P.gss[g] = SsRec{L, term, cl, cf};

@@ -254,19 +254,46 @@ hipError_t launch_window_tail(const DevPlanes& P, const uint32_t* work, uint32_t
 }
 
 __global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hist, unsigned long long* out,
-                                                          uint32_t nticks, CallCheck chk) {
+                                                          uint32_t nticks, LeanBase lb, CallCheck chk) {
   static_assert(STAT_SLOTS == 64, "one lane per slot");
   if (blockIdx.x == nticks) {
     call_check_block(chk);
     host_mirror_done(chk);
     return;
   }
-  unsigned long long* h = hist + size_t(blockIdx.x) * STAT_SLOTS * NSTAT + threadIdx.x * NSTAT;
+  unsigned long long* h = hist + size_t(blockIdx.x) * STAT_TICK + threadIdx.x * NSTAT;
   unsigned long long v[NSTAT];
 #pragma unroll
   for (int s = 0; s < NSTAT; ++s) {
     v[s] = h[s];
     h[s] = 0ull;
+  }
+  // the lean / fused kernels' exception sums (tick_common.hpp lean_stats):
+  // this lane's STAT_PKS / 64 slots
+  unsigned long long dc = 0, nn = 0, nl = 0, ns = 0;
+#pragma unroll 4
+  for (int j = 0; j < STAT_PKS / 64; ++j) {
+    unsigned long long* pk = hist + size_t(blockIdx.x) * STAT_TICK + STAT_PK + (threadIdx.x + 64u * j) * 8;
+    const unsigned long long w0 = pk[0], w1 = pk[1], w2 = pk[2];
+    if (w0 | w1 | w2) {
+      pk[0] = 0ull;
+      pk[1] = 0ull;
+      pk[2] = 0ull;
+    }
+    dc += w0;   // (two's complement: the sum of signed differences)
+    nn += w1 & 0xFFFFFFFFull;
+    nl += w1 >> 32;
+    ns += w2;
+  }
+  {   // the base (lane 0, once per tick): every live group a normal tick with the tick's base commits;
+      // the differences wrap in unsigned arithmetic and the tick's totals are exact
+    const int64_t t = lb.t0 + int64_t(blockIdx.x);
+    const uint32_t n = (lb.period && t % int64_t(lb.period) == 0) ? lb.E : 0u;
+    const unsigned long long R = lb.R, base = threadIdx.x == 0 ? lb.G : 0ull;
+    v[S_COMMITTED] += base * (unsigned long long)lean_base_committed(int(lb.raft), int(lb.R), n) + dc;
+    v[S_AE_OK] += (base - nn) * (R - 1u) + (R >= 2u ? ns * (R - 2u) : 0ull);
+    v[S_AE_FAIL] += nl * (R - 1u) + ns * R;
+    v[S_LEADER_GROUPS] += base - nn + nl + ns;
   }
 #pragma unroll
   for (int s = 0; s < NSTAT; ++s)
@@ -281,11 +308,11 @@ __global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hi
   }
   host_mirror_done(chk);
 }
-hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s,
-                               const CallCheck* chk) {
+hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, const LeanBase& lb,
+                               hipStream_t s, const CallCheck* chk) {
   const uint32_t blocks = nticks + (chk ? 1u : 0u);
   if (!blocks) return hipSuccess;
-  hipLaunchKernelGGL(stats_reduce_kernel, dim3(blocks), dim3(64), 0, s, hist, out, chk ? nticks : 0xFFFFFFFFu,
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3(blocks), dim3(64), 0, s, hist, out, chk ? nticks : 0xFFFFFFFFu, lb,
                      chk ? *chk : CallCheck{});
   return hipGetLastError();
 }

@@ -120,8 +120,17 @@ struct CallCheck {
 // Clears DEFER of the groups on worklist `parity` (work), records their
 // number and zeroes that worklist's counters (k_init.hip window_tail_kernel).
 hipError_t launch_window_tail(const DevPlanes& P, const uint32_t* work, uint32_t* wcount, int parity, hipStream_t s);
-hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, hipStream_t s,
-                               const CallCheck* chk = nullptr);
+// The base the lean / fused kernels' exception statistics are relative to
+// (tick_common.hpp lean_stats): every tick of a two-pass call, G live groups
+// each taking a normal tick.
+struct LeanBase {
+  uint64_t G;          // groups (0: no lean kernel ran, no base)
+  int64_t t0;          // tick of the reduce's first record
+  uint32_t E, period;  // client entries per client tick, ticks per client tick
+  uint32_t R, raft;
+};
+hipError_t launch_stats_reduce(unsigned long long* hist, unsigned long long* out, uint32_t nticks, const LeanBase& lb,
+                               hipStream_t s, const CallCheck* chk = nullptr);
 hipError_t launch_init_steady(int R, const DevPlanes& P, const Trace& T, int32_t leader, hipStream_t s);
 hipError_t launch_vx_flush(int R, const DevPlanes& P, uint64_t Qb, uint32_t E, uint32_t period, uint64_t seed,
                            hipStream_t s);

@@ -110,6 +110,12 @@ __device__ __host__ __forceinline__ bool msync_peer(int meta, const LxRec& x, in
 constexpr int HB_NONE = -2147483647 - 1;
 constexpr int I32MAX = 2147483647;
 constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to cut atomic contention
+// Per tick the statistics area holds the STAT_SLOTS x NSTAT counters, then
+// STAT_PKS 64-B slots of the lean / fused kernels' exception sums (lean_stats
+// in tick_common.hpp; the reduce kernel adds them to the base it computes).
+constexpr int STAT_PKS = 1024;
+constexpr int STAT_PK = STAT_SLOTS * NSTAT;                  // offset of the exception slots in a tick's area
+constexpr int STAT_TICK = STAT_SLOTS * NSTAT + STAT_PKS * 8;   // words per tick
 
 // Device layout. Per-replica scalar planes are [Gp][R] (rix below); the
 // log rings are wave tiles [Gp/64][KP][64][R] (see ring_tile below).

@@ -202,6 +202,39 @@ __device__ __forceinline__ void block_stats(const int (&v)[N], const int (&idx)[
   }
 }
 
+// The lean / fused kernels' statistics of one tick, as exceptions (round 5).
+// The reduce kernel adds, for every tick of a two-pass call, the statistics
+// of every live group taking a normal tick with `lean_base_committed` entries
+// committed (k_init.hip stats_reduce_kernel: R-1 accepted AppendEntries and
+// one leader group each); a lane reports only how it differs from that — a
+// committed count other than the base, a tick that is not normal (passed on,
+// skipped, held by the list kernel), an LXS or an SXS tick (k_fast.hip: an
+// LXS tick has R-1 AppendEntries dropped, an SXS tick R-2 accepted and R
+// dropped). A wave whose lanes are all the base does nothing; one that is not
+// adds its sums to one of STAT_PKS slots (64-B lines: committed difference,
+// not-normal | LXS << 32, SXS). Measured (round 5, tools/stats_cost.py): the
+// per-block sums with a barrier cost the C2-shape kernel 8% per tick with
+// statistics, atomics or not; in steady state this costs one ballot.
+__host__ __device__ __forceinline__ int lean_base_committed(int sem_raft, int R, uint32_t n) {
+  return (sem_raft || 2 * (R - 1) > R) ? int(n) : 0;   // (k_fast.hip: the commit rule of a normal tick)
+}
+template <bool RAFT>
+__device__ __forceinline__ void lean_stats(bool live, int dcommitted, bool normal, bool lxs, bool sxs,
+                                           unsigned long long* stats) {
+  if (!__ballot(live && (dcommitted != 0 || !normal))) return;   // (wave-uniform)
+  const long long c = wave_sum(live ? dcommitted : 0);
+  const unsigned long long nn = __popcll(__ballot(live && !normal));
+  const unsigned long long nl = RAFT ? __popcll(__ballot(live && lxs)) : 0ull;
+  const unsigned long long ns = RAFT ? __popcll(__ballot(live && sxs)) : 0ull;
+  if ((threadIdx.x & 63) == 0) {
+    const uint32_t slot = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % STAT_PKS;
+    unsigned long long* pk = stats + STAT_PK + slot * 8;
+    if (c) atomicAdd(&pk[0], (unsigned long long)c);
+    if (nn | nl) atomicAdd(&pk[1], nn | (nl << 32));
+    if (ns) atomicAdd(&pk[2], ns);
+  }
+}
+
 template <int R, typename F>
 __device__ __forceinline__ void with_replica(int x, F&& f) {
   static_for<R>([&](auto PI) {
