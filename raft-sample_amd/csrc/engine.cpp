@@ -1232,7 +1232,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (skip_list) e->n_skip_ticks += nticks;
   const bool two = e->two_pass && !e->force_general;
   e->call_t0 = first_tick;
-  e->call_lean = two;
+  e->call_lean = two && T0.iso_p == 0;   // (under isolation churn the lean kernel counts absolutely)
   const bool pipe = two && !skip_list && !e->debug_work && e->pipeline;
   const bool pp = pipe && e->pingpong;
   if (e->debug_pipe)

@@ -2007,9 +2007,24 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   // (packed, tick_common.hpp lean_stats: a normal tick R-1 accepted
   // AppendEntries; an LXS tick every AppendEntries of the cut-off leader
   // dropped; an SXS tick the one to the stale leader and every one it sends)
-  if (stats)
+  if (stats && !T.iso_p) {
     lean_stats<RAFT>(g < P.G, committed - lean_base_committed(RAFT, R, uint32_t(n)), take && !lxs && !sxs,
                      take && lxs, take && sxs, stats);
+  } else if (stats) {   // (isolation churn: absolute per-block counters, no base — engine.cpp call_lean)
+    const int t = take ? 1 : 0;
+    if constexpr (RAFT) {
+      // (an LXS tick: every AppendEntries of the cut-off leader dropped; an SXS
+      // tick: the one to the stale leader and every one it sends)
+      const int v[5] = {committed, (take && !lxs) ? (sxs ? R - 2 : R - 1) : 0,
+                        (take && lxs) ? R - 1 : ((take && sxs) ? R : 0), t, 0};
+      const int idx[5] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS, S_BUMPS};
+      block_stats<5>(v, idx, stats);
+    } else {
+      const int v[4] = {committed, t * (R - 1), 0, t};
+      const int idx[4] = {S_COMMITTED, S_AE_OK, S_AE_FAIL, S_LEADER_GROUPS};
+      block_stats<4>(v, idx, stats);
+    }
+  }
 }
 
 // Fused steady ticks (the steady-state list skip, engine.cpp): every live

@@ -274,16 +274,15 @@ __global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hi
 #pragma unroll 4
   for (int j = 0; j < STAT_PKS / 64; ++j) {
     unsigned long long* pk = hist + size_t(blockIdx.x) * STAT_TICK + STAT_PK + (threadIdx.x + 64u * j) * 8;
-    const unsigned long long w0 = pk[0], w1 = pk[1], w2 = pk[2];
-    if (w0 | w1 | w2) {
+    const unsigned long long w0 = pk[0], w1 = pk[1];
+    if (w0 | w1) {
       pk[0] = 0ull;
       pk[1] = 0ull;
-      pk[2] = 0ull;
     }
     dc += w0;   // (two's complement: the sum of signed differences)
-    nn += w1 & 0xFFFFFFFFull;
-    nl += w1 >> 32;
-    ns += w2;
+    nn += w1 & 0x1FFFFFull;
+    nl += (w1 >> 21) & 0x1FFFFFull;
+    ns += w1 >> 42;
   }
   {   // the base (lane 0, once per tick): every live group a normal tick with the tick's base commits;
       // the differences wrap in unsigned arithmetic and the tick's totals are exact

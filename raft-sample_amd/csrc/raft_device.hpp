@@ -113,7 +113,7 @@ constexpr int STAT_SLOTS = 64;   // per-tick stats are spread over 64 slots to c
 // Per tick the statistics area holds the STAT_SLOTS x NSTAT counters, then
 // STAT_PKS 64-B slots of the lean / fused kernels' exception sums (lean_stats
 // in tick_common.hpp; the reduce kernel adds them to the base it computes).
-constexpr int STAT_PKS = 1024;
+constexpr int STAT_PKS = 256;
 constexpr int STAT_PK = STAT_SLOTS * NSTAT;                  // offset of the exception slots in a tick's area
 constexpr int STAT_TICK = STAT_SLOTS * NSTAT + STAT_PKS * 8;   // words per tick
 

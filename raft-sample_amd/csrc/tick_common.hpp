@@ -212,9 +212,12 @@ __device__ __forceinline__ void block_stats(const int (&v)[N], const int (&idx)[
 // LXS tick has R-1 AppendEntries dropped, an SXS tick R-2 accepted and R
 // dropped). A wave whose lanes are all the base does nothing; one that is not
 // adds its sums to one of STAT_PKS slots (64-B lines: committed difference,
-// not-normal | LXS << 32, SXS). Measured (round 5, tools/stats_cost.py): the
+// not-normal | LXS << 21 | SXS << 42). Measured (round 5, tools/stats_cost.py): the
 // per-block sums with a barrier cost the C2-shape kernel 8% per tick with
-// statistics, atomics or not; in steady state this costs one ballot.
+// statistics, atomics or not; in steady state this costs one ballot. Under
+// isolation churn (most waves hold an exception) the lean kernel keeps the
+// per-block absolute counters (block_stats; 2% faster on C4) and the call
+// has no base (engine.cpp call_lean).
 __host__ __device__ __forceinline__ int lean_base_committed(int sem_raft, int R, uint32_t n) {
   return (sem_raft || 2 * (R - 1) > R) ? int(n) : 0;   // (k_fast.hip: the commit rule of a normal tick)
 }
@@ -222,16 +225,17 @@ template <bool RAFT>
 __device__ __forceinline__ void lean_stats(bool live, int dcommitted, bool normal, bool lxs, bool sxs,
                                            unsigned long long* stats) {
   if (!__ballot(live && (dcommitted != 0 || !normal))) return;   // (wave-uniform)
-  const long long c = wave_sum(live ? dcommitted : 0);
-  const unsigned long long nn = __popcll(__ballot(live && !normal));
-  const unsigned long long nl = RAFT ? __popcll(__ballot(live && lxs)) : 0ull;
-  const unsigned long long ns = RAFT ? __popcll(__ballot(live && sxs)) : 0ull;
-  if ((threadIdx.x & 63) == 0) {
-    const uint32_t slot = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % STAT_PKS;
-    unsigned long long* pk = stats + STAT_PK + slot * 8;
-    if (c) atomicAdd(&pk[0], (unsigned long long)c);
-    if (nn | nl) atomicAdd(&pk[1], nn | (nl << 32));
-    if (ns) atomicAdd(&pk[2], ns);
+  const unsigned long long c = (unsigned long long)wave_sum(live ? dcommitted : 0);
+  // not-normal | LXS << 21 | SXS << 42 (per slot and tick at most 64 * ceil(G / 64 / STAT_PKS) lanes each,
+  // < 2^21: engine.cpp limits G to Gp * recw * 4 < 2^32, i.e. G < 2^27)
+  const unsigned long long k = (unsigned long long)__popcll(__ballot(live && !normal)) |
+                               (RAFT ? ((unsigned long long)__popcll(__ballot(live && lxs)) << 21) |
+                                           ((unsigned long long)__popcll(__ballot(live && sxs)) << 42)
+                                     : 0ull);
+  if ((threadIdx.x & 63u) == 0) {
+    unsigned long long* pk = stats + STAT_PK + ((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % STAT_PKS) * 8;
+    if (c) atomicAdd(&pk[0], c);
+    if (k) atomicAdd(&pk[1], k);
   }
 }
 
