@@ -270,9 +270,10 @@ __global__ __launch_bounds__(64) void stats_reduce_kernel(unsigned long long* hi
   }
   // the lean / fused kernels' exception sums (tick_common.hpp lean_stats):
   // this lane's STAT_PKS / 64 slots
+  // (none without a base: the lean kernel then counts absolutely)
   unsigned long long dc = 0, nn = 0, nl = 0, ns = 0;
 #pragma unroll 4
-  for (int j = 0; j < STAT_PKS / 64; ++j) {
+  for (int j = 0; j < (lb.G ? STAT_PKS / 64 : 0); ++j) {
     unsigned long long* pk = hist + size_t(blockIdx.x) * STAT_TICK + STAT_PK + (threadIdx.x + 64u * j) * 8;
     const unsigned long long w0 = pk[0], w1 = pk[1];
     if (w0 | w1) {
