@@ -67,7 +67,7 @@ ENV_KNOBS = {
     "RAFTSTEP_SPLIT_STEADY": "exact: 0 = one launch per steady tick instead of two halves on two streams "
                              "(tests/test_gpu_engine_checks.py)",
     "RAFTSTEP_SH": "exact: 0 = no shared entries (every entry in the R replica rings), 2 = shared entries under "
-                   "isolation churn too (tests/test_gpu_sh.py)",
+                   "isolation churn too (A/B only: 4x slower on C4; tests/test_gpu_sh.py)",
     "RAFTSTEP_VX": "exact: 0 = no virtual log suffixes (C4's stale leaders' entries stored and copied back at "
                    "their return; tests/test_gpu_fullsize.py, test_gpu_pipeline.py)",
     "RAFTSTEP_DEBUG_WORK": "exact: prints worklist sizes, synchronises (in-line form)",

@@ -151,3 +151,29 @@ def test_corrupted_copies_leave_the_shared_form(monkeypatch):
     assert cls["list_sh_copied"] > 0 and cls["lean_sh"] > 0, cls
     _digests(e, o, f"after tick {t - 1}")
     H.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")
+
+
+def test_forced_on_under_isolation_churn(monkeypatch):
+    """RAFTSTEP_SH=2 (the A/B knob: shared entries under C4's leader-isolation
+    churn too, with virtual suffixes and ring segment switches): every group
+    leaves and re-enters the shared form through the list kernel's copy-back;
+    statistics of every call, then digests and the whole state, equal the
+    oracle's."""
+    import bench
+    monkeypatch.setenv("RAFTSTEP_SH", "2")
+    wl = bench.WORKLOADS["C4"]
+    kw = bench.engine_kwargs(wl, 7, 1 << 13, 0, wl["ring_depth"], 1, 0)
+    kw["isolate_per_65536"] = 4 * wl["iso"][0]
+    e, o = Engine(**kw), oracle.Oracle(**kw)
+    assert e.features()["shared_entries"]
+    e.diag_enable()
+    e.init_new_nodes(0)
+    o.init_new_nodes(0)
+    t = 0
+    for k in (48, 20, 20, 20, 13, 30):
+        assert list(e.tick(t, k)) == list(o.tick(t, k, threads=16)), f"stats of ticks [{t}, {t + k})"
+        t += k
+    cls = e.diag_read()
+    assert cls["list_sh_copied"] > 100 and cls["lean_sh"] > 0, cls
+    _digests(e, o, f"after tick {t - 1}")
+    H.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")
