@@ -116,11 +116,12 @@ def lean_bytes(R, E, crc=False, segmented=False, fuse=1, glx=False, shared=False
     the record / meta / rotation / heartbeat bytes are moved once per launch:
     40 / fuse + 12 E R. With shared entries (`shared`, raft_engine_features:
     an in-step group's entries stored once, raft_device.hpp ROT_SH) the
-    entries are written once instead of R times: 12 E (+4 E) — C2 52 B, C5
-    1064 B."""
+    entries are written once instead of R times, 12 E (+4 E), and the
+    heartbeat time is implied (DevPlanes::sh_hb: no hb store) — C2 48 B, C5
+    1060 B."""
     copies = 1 if shared else R
-    return (20 + (4 if segmented else 0) + (8 if glx else 0) + 20) / fuse + 12 * E * copies + \
-        (4 * E * copies if crc else 0)
+    words = 20 + (4 if segmented else 0) + (8 if glx else 0) + 16 + (0 if shared else 4)
+    return words / fuse + 12 * E * copies + (4 * E * copies if crc else 0)
 
 
 # SURVEY.md §8(d) workloads runnable by this bench (per GPU)
@@ -497,7 +498,8 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
         # shape at the same size (raft_stream_probe: fresh buffers, no Raft
         # state): the practical roofline of this kernel on this box
         from raftstep import stream_probe
-        # (shared entries: the probe's ring row is one copy wide, R=1: 52 B)
+        # (shared entries: the probe's ring row is one copy wide, R=1: 52 B;
+        # its heartbeat store stays, so it moves 4 B more than the kernel)
         pus, pby = stream_probe(ctx.local, 1 if shared else R, G, 10)
         roof["stream_probe"] = {"GBs": pby / pus / 1e3, "us_per_pass": pus, "bytes_per_pass": pby,
                                 "what": "raft_stream_probe: per element 20 B read in one round trip, 40 + 12c B "

@@ -168,6 +168,7 @@ struct raft_engine {
   int64_t call_t0 = 0;
   bool call_lean = false;
   int64_t sh_next = 0;          // the tick after the last call that may have left them
+  bool sh_done = true;          // that call issued all its launches (else the implied heartbeat time is unknown)
   // the current run of consecutive raft_tick calls (Trace::contig_q): it
   // starts at contig_from and continues at run_next; a call at another tick,
   // a handler batch or a state replacement starts a new one
@@ -411,8 +412,21 @@ int vx_flush(raft_engine* e) {
 // SH: every group's shared entries into its replica rings, before the host
 // reads or changes the rings (host views, handler batches). Exact at any time
 // (nothing is regenerated); the digest reads the shared ring itself.
+// The heartbeat time every group in shared form holds implicitly (now of the
+// last tick run, DevPlanes::sh_hb); unknown after a call that failed mid-way.
+int sh_heartbeat(raft_engine* e) {
+  if (!e->sh_done) {
+    e->poisoned = true;
+    e->steady_ok = false;
+    e->poison_msg = "a failed raft_tick call left shared entries' heartbeat times undefined (state must be replaced)";
+    return fail(RAFT_EINTERNAL, "%s", e->poison_msg.c_str());
+  }
+  e->P.sh_hb = make_trace(e, e->sh_next - 1).now;
+  return RAFT_OK;
+}
 int sh_flush(raft_engine* e) {
   if (!e->sh_live) return RAFT_OK;
+  if (int rc = sh_heartbeat(e)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   HIPCHK(launch_sh_flush(e->R, e->P, e->stream));
   e->sh_live = false;
@@ -1213,6 +1227,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (e->P.sh) {   // (any lean / fused launch may leave shared entries)
     e->sh_live = true;
     e->sh_next = first_tick + int64_t(nticks);
+    e->sh_done = false;   // (until the call has issued all its launches)
   }
   if (!e->run_valid || !e->run_done || first_tick != e->run_next) {   // a new run of consecutive calls
     e->contig_from = first_tick;
@@ -1490,6 +1505,7 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (split && prof_b) HIPCHK(hipEventRecord(prof_b, e->stream));   // the span ends with both halves
   e->hist_dirty = 0;   // every reduce of the call is issued
   if (e->P.vx) e->vx_tick = first_tick + int64_t(nticks);
+  e->sh_done = true;
   e->run_done = true;
   if (e->comm && e->comm_side) {   // the engine stream (readback, next call) waits for the side-stream sums
     HIPCHK(hipEventRecord(e->comm_ev[1], e->comm_stream));
@@ -2014,6 +2030,8 @@ int raft_state_digest(raft_engine* e, uint64_t* per_group, uint64_t* total) {
   if (!e) return fail(RAFT_EINVAL, "null engine");
   if (int rc = settle_check(e)) return rc;
   if (int rc = vx_flush(e)) return rc;
+  if (e->sh_live)   // (the digest reads shared entries and implied heartbeat times directly)
+    if (int rc = sh_heartbeat(e)) return rc;
   HIPCHK(hipSetDevice(e->cfg.device));
   const uint64_t G = e->cfg.groups;
   uint64_t* d_pg = nullptr;

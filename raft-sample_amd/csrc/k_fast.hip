@@ -1397,7 +1397,7 @@ __global__ __launch_bounds__(256) void tick_fast_kernel(DevPlanes P, Trace T, un
   __shared__ uint32_t tab[CRC ? 2048 : 1];
   stage_crc_tab<CRC>(P, tab);
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-  if (g < P.G) sh_materialize<R>(P, g);   // (ROT_SH: a group the lean kernel left in shared form)
+  if (g < P.G) sh_materialize<R>(P, g, T.at_tick(T.tick - 1).now);   // (ROT_SH: a group the lean kernel left in shared form)
   fast_group<R, CRC, SEM, false>(P, T, stats, work, work_tick, work_count, force_slow, g, tab,
                                      rows_global<R>(P, g), words_global(P, g));
 }
@@ -1494,7 +1494,10 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
         if (P.dbg) atomicAdd(&P.dbg[31], 1ull);
       }
     }
-    smeta[t] = m0; sgrot[t] = uint16_t(r0 & ~ROT_SH); sgiso[t] = gi0; shb[t] = hb0; sgss[t] = ss0; sglx[t] = lx0;
+    // (a group in shared form was taken by the lean kernel at the tick before
+    // this one: its heartbeat time is implied, and written back from here)
+    const int32_t hbs = (r0 & ROT_SH) ? T.at_tick(T.tick - 1).now : hb0;
+    smeta[t] = m0; sgrot[t] = uint16_t(r0 & ~ROT_SH); sgiso[t] = gi0; shb[t] = hbs; sgss[t] = ss0; sglx[t] = lx0;
     sgrota[t] = ra0; sgrotb[t] = rb0; sgsb[t] = sb0; sgsb2[t] = sc0;
     __syncthreads();
     {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
@@ -1834,6 +1837,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
                    : 0u;
       }
       if (take) {
+        // (SH: the heartbeat time of a group in shared form is implied, P.sh_hb)
+        if (shw || shm) hbw = false;
         if (P.rec_nt) {   // (per-group words beyond the Infinity Cache: streamed, DevPlanes::rec_nt)
           typedef int32_t i4 __attribute__((ext_vector_type(4)));
           if (nl != L || cl2 != s.cl || cf2 != s.cf)
@@ -2138,9 +2143,9 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
       lean_stats<RAFT>(g < P.G, committed - lean_base_committed(RAFT, R, uint32_t(n)), take, false, false,
                        stats + size_t(j) * STAT_TICK);
   }
-  if (done) {   // the record and every follower's timer as of the last tick taken
+  if (done) {   // the record and every follower's timer as of the last tick taken (SH: implied)
     if (L != s0.last || cl != s0.cl || cf != s0.cf) P.gss[g] = SsRec{L, term, cl, cf};
-    at(P.hb, g) = T.at_tick(T.tick + done - 1).now;
+    if (!(sh_from >= 0 || (uint32_t(rot) & ROT_SH))) at(P.hb, g) = T.at_tick(T.tick + done - 1).now;
   }
   if (sh_from >= 0) {   // SH from that entry on
     at(P.grot, g) = uint16_t(uint32_t(rot) | ROT_SH);

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
     const bool ssync = (meta & M_SSYNC) && primary < R;   // compressed state: the gss record
     const SsRec ss = ssync ? P.gss[g] : SsRec{0, 0, 0, 0};
     const LxRec lx = (ssync && uses_glx(meta)) ? P.glx[g] : LxRec{0, 0};
-    const int hb = at(P.hb, g);
+    const int hb = (P.sh && (at(P.grot, g) & ROT_SH)) ? P.sh_hb : at(P.hb, g);   // (SH: implied)
     int last[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) last[r] = ssync ? ss_last(ss, r, primary, meta, lx) : at(P.last, rix<R>(g, r));
@@ -422,7 +422,7 @@ hipError_t launch_vx_flush(int R, const DevPlanes& P, uint64_t Qb, uint32_t E, u
 template <int R>
 __global__ __launch_bounds__(256) void sh_flush_kernel(DevPlanes P) {
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-  if (g < P.G) sh_materialize<R>(P, g);
+  if (g < P.G) sh_materialize<R>(P, g, P.sh_hb);
 }
 hipError_t launch_sh_flush(int R, const DevPlanes& P, hipStream_t s) {
   RAFT_DISPATCH_R(R, hipLaunchKernelGGL(sh_flush_kernel<RR>, grid_for(P.G), dim3(256), 0, s, P));

@@ -204,6 +204,12 @@ struct DevPlanes {
   // SH (ROT_SH) enabled: steady groups' entries go to the shared ring (no
   // EXT isolation configured, KP < 2^15; RAFTSTEP_SH=0 turns it off)
   uint32_t sh;
+  // SH: a group in shared form is taken by the lean (or fused) kernel every
+  // tick, so its heartbeat time (hb, every follower's timer reset) is implied:
+  // now of the last tick run. Its hb store is skipped; whoever copies the
+  // group back writes it (the list kernel: now of the tick before its own;
+  // the engine's flush and the digest: sh_hb, now of the last call's last tick)
+  int32_t sh_hb;
   uint32_t diag;       // timing-only diagnostics (RAFTSTEP_DIAG_LEAN; results are wrong when set): 1 = drifted
                        // lanes of the lean kernel skip their ring writes, 2 = they write the wave's common row
                        // (list kernel: 32 = staging alone, 64 = no tick, 128 = no ring writes / copies)
@@ -609,15 +615,16 @@ __device__ __forceinline__ void sh_copy_back(const DevPlanes& P, uint32_t g, int
     }
   }
 }
-// ... reading every word from memory and clearing the bit (general kernels,
-// one-pass kernel, the engine's flush)
+// ... reading every word from memory, writing the implied heartbeat time hb
+// and clearing the bit (general kernels, one-pass kernel, the engine's flush)
 template <int R>
-__device__ __forceinline__ void sh_materialize(const DevPlanes& P, uint32_t g) {
+__device__ __forceinline__ void sh_materialize(const DevPlanes& P, uint32_t g, int32_t hb) {
   if (!P.sh) return;
   const uint32_t rot = at(P.grot, g);
   if (!(rot & ROT_SH)) return;
   const GSeg cw = P.gseg[g];
   sh_copy_back<R>(P, g, P.gss[g].last, cw.shf, rot, cw.rota, cw.rotb, at(P.gsb, g), cw.sb2);
+  at(P.hb, g) = hb;   // (implied while shared: now of the last tick it was taken)
   at(P.grot, g) = uint16_t(rot & ~ROT_SH);
 }
 

@@ -56,9 +56,9 @@ def test_live_group_steps_small_case():
                          [(5, 1, 0, False, 1, False, False, 100), (7, 1, 0, True, 1, False, False, 128),
                           (7, 1, 0, True, 1, True, False, 136), (5, 64, 1, False, 1, False, False, 5160),
                           (5, 1, 0, False, 10, False, False, 64),
-                          # shared entries (C2 / C5 / fused C2): one copy of each entry
-                          (5, 1, 0, False, 1, False, True, 52), (5, 64, 1, False, 1, False, True, 1064),
-                          (5, 1, 0, False, 10, False, True, 16)])
+                          # shared entries (C2 / C5 / fused C2): one copy of each entry, no hb store
+                          (5, 1, 0, False, 1, False, True, 48), (5, 64, 1, False, 1, False, True, 1060),
+                          (5, 1, 0, False, 10, False, True, 15.6)])
 def test_byte_accounting(R, E, crc, seg, fuse, glx, sh, want):
     assert bench.lean_bytes(R, E, crc, segmented=seg, fuse=fuse, glx=glx, shared=sh) == want
 
