@@ -498,14 +498,16 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
         # shape at the same size (raft_stream_probe: fresh buffers, no Raft
         # state): the practical roofline of this kernel on this box
         from raftstep import stream_probe
-        # (shared entries: the probe's ring row is one copy wide, R=1: 52 B;
-        # its heartbeat store stays, so it moves 4 B more than the kernel)
-        pus, pby = stream_probe(ctx.local, 1 if shared else R, G, 10)
+        # (shared entries: the probe's ring row is one copy wide, R=1, and it
+        # skips the heartbeat store as the kernel does: 48 B)
+        pus, pby = stream_probe(ctx.local, 1 if shared else R, G, 10, heartbeat=not shared)
+        pb = (36 if shared else 40) + 12 * (1 if shared else R)
         roof["stream_probe"] = {"GBs": pby / pus / 1e3, "us_per_pass": pus, "bytes_per_pass": pby,
-                                "what": "raft_stream_probe: per element 20 B read in one round trip, 40 + 12c B "
-                                        "moved (c = %d ring copies: %d B), record / heartbeat / whole-ring-row "
-                                        "stores, on fresh buffers of the line's group count"
-                                        % (1 if shared else R, 40 + 12 * (1 if shared else R))}
+                                "what": "raft_stream_probe: per element 20 B read in one round trip, %d B moved "
+                                        "(%d ring copies%s), record%s / whole-ring-row stores, on fresh buffers of "
+                                        "the line's group count"
+                                        % (pb, 1 if shared else R, ", no heartbeat store" if shared else "",
+                                           "" if shared else " / heartbeat")}
         roof["frac_of_stream_probe"] = achieved / (pby / pus / 1e3)
     if do_cpu:
         cb = cpu_baseline(wl, R, E, K, crc, *cpu, leader=leader, check=(digests, tick))

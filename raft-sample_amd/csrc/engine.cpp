@@ -1986,7 +1986,8 @@ int raft_stream_probe(int device, uint32_t replicas, uint64_t elems, uint32_t re
                         hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess))
     rc = fail(RAFT_EHIP, "stream probe: stream / event creation failed");
   float ms = 0.f;
-  // (RAFTSTEP_PROBE_MODE, diagnostics: bit 0 plain ring stores, bit 1 non-temporal record stores)
+  // (RAFTSTEP_PROBE_MODE: bit 0 plain ring stores, bit 1 non-temporal record stores, bit 2 no
+  // heartbeat store — the mix of a group in shared form, which bench.py selects for those lines)
   const uint32_t mode = getenv("RAFTSTEP_PROBE_MODE") ? uint32_t(atoi(getenv("RAFTSTEP_PROBE_MODE"))) : 0u;
   if (rc == RAFT_OK) {
     hipError_t h = launch_stream_probe(int(R), a, b, c, d, rt, rv, uint32_t(n), 1u, uint32_t(KS), s, mode);
@@ -2004,7 +2005,7 @@ int raft_stream_probe(int device, uint32_t replicas, uint64_t elems, uint32_t re
   for (void* p : mem) (void)hipFree(p);
   if (rc != RAFT_OK) return rc;
   *us_per_pass = double(ms) * 1e3 / reps;
-  *bytes_per_pass = double(n) * double(40 + 12 * R);
+  *bytes_per_pass = double(n) * double(((mode & 4u) ? 36 : 40) + 12 * R);   // (bit 2: no heartbeat store)
   return RAFT_OK;
 }
 

@@ -397,10 +397,10 @@ __global__ __launch_bounds__(256) void stream_probe_kernel(const uint16_t* a, Ss
     if (mode & 2u) {   // (mode bit 1: non-temporal record / heartbeat stores)
       typedef int32_t i4 __attribute__((ext_vector_type(4)));
       __builtin_nontemporal_store(i4{s.last + 1, s.term, s.cl + 1, s.cf + 1}, reinterpret_cast<i4*>(&b[g]));
-      __builtin_nontemporal_store(int32_t(s.term + int32_t(slot)), &d[g]);
+      if (!(mode & 4u)) __builtin_nontemporal_store(int32_t(s.term + int32_t(slot)), &d[g]);
     } else {
       b[g] = SsRec{s.last + 1, s.term, s.cl + 1, s.cf + 1};
-      d[g] = s.term + int32_t(slot);
+      if (!(mode & 4u)) d[g] = s.term + int32_t(slot);   // (bit 2: no heartbeat store, as in shared form)
     }
   }
 }

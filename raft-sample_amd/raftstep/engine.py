@@ -38,12 +38,22 @@ def _check(rc):
         raise RaftError(rc, load_library().raft_last_error().decode(errors="replace"))
 
 
-def stream_probe(device=0, replicas=5, elems=1 << 24, reps=10):
+def stream_probe(device=0, replicas=5, elems=1 << 24, reps=10, heartbeat=True):
     """The steady lean kernel's byte mix on fresh buffers (raft_stream_probe):
-    (us per pass, bytes per pass)."""
+    (us per pass, bytes per pass). heartbeat=False: without the heartbeat
+    store (a group in shared form; RAFTSTEP_PROBE_MODE bit 2)."""
     lib = load_library()
     us, by = C.c_double(), C.c_double()
-    _check(lib.raft_stream_probe(int(device), int(replicas), int(elems), int(reps), C.byref(us), C.byref(by)))
+    old = os.environ.get("RAFTSTEP_PROBE_MODE")
+    if not heartbeat:
+        os.environ["RAFTSTEP_PROBE_MODE"] = str(int(old or 0) | 4)
+    try:
+        _check(lib.raft_stream_probe(int(device), int(replicas), int(elems), int(reps), C.byref(us), C.byref(by)))
+    finally:
+        if old is None:
+            os.environ.pop("RAFTSTEP_PROBE_MODE", None)
+        else:
+            os.environ["RAFTSTEP_PROBE_MODE"] = old
     return us.value, by.value
 
 

@@ -227,5 +227,7 @@ def test_stream_probe_reports_its_bytes():
     assert by == (1 << 20) * 100 and 0 < us < 1e5
     us7, by7 = stream_probe(0, 7, 1000, 2)
     assert by7 == 1024 * 124 and us7 > 0
+    us1, by1 = stream_probe(0, 1, 1 << 20, 3, heartbeat=False)   # (the shared-form mix: 36 + 12 B)
+    assert by1 == (1 << 20) * 48 and 0 < us1 < 1e5
     with pytest.raises(RaftError):
         stream_probe(0, 9, 1 << 20, 1)
