@@ -99,7 +99,7 @@ def algorithmic_bytes(R, E, crc=False):
     return 25 + 37 * (R - 1) + 12 * E * R + (4 * E * R if crc else 0)
 
 
-def lean_bytes(R, E, crc=False, segmented=False, fuse=1, glx=False, shared=False):
+def lean_bytes(R, E, crc=False, segmented=False, fuse=1, glx=False, shared=False, staged=False):
     """Algorithmic bytes per group-step of tick_lean_kernel (the dominant
     kernel of the two-pass tick, k_fast.hip) in this engine's layout: a group
     in the compressed steady state (SSYNC) holds term / LastApplied / the
@@ -118,10 +118,12 @@ def lean_bytes(R, E, crc=False, segmented=False, fuse=1, glx=False, shared=False
     an in-step group's entries stored once, raft_device.hpp ROT_SH) the
     entries are written once instead of R times, 12 E (+4 E), and the
     heartbeat time is implied (DevPlanes::sh_hb: no hb store) — C2 48 B, C5
-    1060 B."""
+    1060 B. With staged client values (`staged`, RAFT_CLIENT_STAGED) it also
+    reads the E values of the group's client request, 8 E B (SURVEY §8(d):
+    "add 8E if client values are staged in HBM"): C2S 56 B, C4S 144 B."""
     copies = 1 if shared else R
     words = 20 + (4 if segmented else 0) + (8 if glx else 0) + 16 + (0 if shared else 4)
-    return words / fuse + 12 * E * copies + (4 * E * copies if crc else 0)
+    return words / fuse + 12 * E * copies + (4 * E * copies if crc else 0) + (8 * E if staged else 0)
 
 
 # SURVEY.md §8(d) workloads runnable by this bench (per GPU)
@@ -158,7 +160,60 @@ WORKLOADS = {
                   iso=(8192, 8, 32, 1), seed=0x5EED0004, allow_faults=True,
                   desc="NewNode start, leader-isolation churn, REF semantics (prefix; groups freeze on their first fault)"),
 }
-EXTRA_DEFAULT = ("C2X", "C4", "C5")
+# Staged client values (raft_config.client_source = RAFT_CLIENT_STAGED,
+# VERDICT r5 #1): the same workloads with every client value supplied by the
+# caller in an HBM buffer (raft_stage_values, [ticks][E][G] int64) instead of
+# the engine's trace RNG -- the drop-in LogReq path (main.go:87-93 ->
+# 327-329). The engine cannot regenerate an entry in this mode (no virtual
+# suffixes, no regenerated catch-up copies: those groups take the general
+# kernel, which reads the leader's ring), and the lean kernel reads 8 B per
+# group-step more. The values are staged before each timed region (inputs
+# resident in HBM); `pcie_inclusive` times staging + ticks.
+for _k in ("C2", "C4", "C5"):
+    WORKLOADS[_k + "S"] = dict(WORKLOADS[_k], staged=True, desc=WORKLOADS[_k]["desc"] + ", client values staged by "
+                               "the caller in HBM (RAFT_CLIENT_STAGED)")
+# C5 with verification on the timed path: every follower's
+# copy is corrupted w.p. 300/65536 per tick, so CRC32C rejections (and the
+# backoff of the rejecting followers) happen inside the timed region
+# (K = 512: a follower that rejected j batches in a row is sent (j+1) x 64
+# entries with prevLogIndex j x 64 + 64 back; REF faults with RING_EVICTED
+# once that leaves the window, i.e. after 7 rejections in a row here, after
+# one with C5's K = 128)
+WORKLOADS["C5V"] = dict(WORKLOADS["C5"], corrupt=300, ring_depth=512,
+                        desc=WORKLOADS["C5"]["desc"] + ", EXT corruption 300/65536 per follower and tick (rejections "
+                                                       "timed)")
+EXTRA_DEFAULT = ("C2X", "C4", "C5", "C2S", "C4S", "C5V")
+
+
+def _sm64_np(x):
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+_KEYS = {}   # staged_values: the per-group keys of the last (seed, base, groups)
+
+
+def staged_values(seed, group_base, groups, first_tick, nticks, E):
+    """The client's values for RAFT_CLIENT_STAGED lines and tests: [nticks][E][G]
+    int64 in [0, 2^63) like rand.Int() (main.go:92), a hash of (seed, global
+    group id, tick, entry) made by the CALLER (numpy, independent of the
+    engine's trace RNG), so that any slice of groups can be re-staged for an
+    oracle slice: a hashed per-group key XOR a hashed (tick, entry) word, one
+    pass per value (staging 2^22 groups x 20 ticks takes well under a second)."""
+    with np.errstate(over="ignore"):
+        ck = (seed, group_base, groups)
+        key = _KEYS.get(ck)
+        if key is None:
+            gid = np.arange(group_base, group_base + groups, dtype=np.uint64)
+            key = _sm64_np(gid ^ np.uint64(seed ^ 0xC11E57A6ED)) >> np.uint64(1)
+            _KEYS.clear()
+            _KEYS[ck] = key
+        q = np.arange(first_tick, first_tick + nticks, dtype=np.uint64)[:, None] * np.uint64(E) + \
+            np.arange(E, dtype=np.uint64)[None, :]
+        q = _sm64_np(q ^ np.uint64(seed)) >> np.uint64(1)
+        return (key[None, None, :] ^ q[:, :, None]).view(np.int64)
 
 
 def cpu_baseline(wl, R, E, K, crc, groups, ticks, leader=0, check=None):
@@ -185,10 +240,17 @@ def cpu_baseline(wl, R, E, K, crc, groups, ticks, leader=0, check=None):
     G = min(G, Geng)
     # a seeded, unaligned offset inside the engine's group range
     off = 0 if G >= Geng else int(np.random.default_rng(wl["seed"]).integers(0, Geng - G + 1))
+    staged = bool(wl.get("staged"))
+
+    def stage(o, t, n):   # RAFT_CLIENT_STAGED: the slice's columns of the line's values (untimed)
+        if staged and n > 0:
+            o.stage_values(t, staged_values(wl["seed"], off, G, t, n, E))
+
     if wl.get("init") == "new":
         G, T = max(1, G // 2), max(1, T // 2)
         o = oracle.Oracle(**engine_kwargs(wl, R, G, off, K, E, crc))
         o.init_new_nodes(0)
+        stage(o, 0, wl["settle"])
         o.tick(0, wl["settle"], threads=threads)
         t_first, start = wl["settle"], "after a NewNode start and %d settle ticks" % wl["settle"]
     else:
@@ -201,6 +263,7 @@ def cpu_baseline(wl, R, E, K, crc, groups, ticks, leader=0, check=None):
     if check is not None:
         dig, t_end = check
         T = max(T, t_end - t_first)
+        stage(o, t, t_end - t)
         t0 = time.perf_counter()
         o.tick(t, t_end - t, threads=threads)
         dt += time.perf_counter() - t0
@@ -214,6 +277,7 @@ def cpu_baseline(wl, R, E, K, crc, groups, ticks, leader=0, check=None):
                                "last call vs the oracle run over the same groups and ticks"}
     rest = t_first + T - t
     if rest > 0:
+        stage(o, t, rest)
         t0 = time.perf_counter()
         o.tick(t, rest, threads=threads)
         dt += time.perf_counter() - t0
@@ -229,7 +293,8 @@ def cpu_baseline(wl, R, E, K, crc, groups, ticks, leader=0, check=None):
 
 def engine_kwargs(wl, R, G, base, K, E, crc):
     kw = dict(replicas=R, groups=G, group_base=base, ring_depth=K, entries_per_tick=E, client_period=1,
-              payload_crc=crc, seed=wl["seed"], semantics=wl.get("semantics", 0))
+              payload_crc=crc, seed=wl["seed"], semantics=wl.get("semantics", 0),
+              client_source=1 if wl.get("staged") else 0, corrupt_per_65536=wl.get("corrupt", 0))
     if "iso" in wl:
         kw.update(isolate_per_65536=wl["iso"][0], isolate_min_ticks=wl["iso"][1], isolate_max_ticks=wl["iso"][2],
                   isolate_leader=wl["iso"][3])
@@ -312,15 +377,23 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     if ctx.comm:
         eng.comm_init(world, ctx.rank, rdist.exchange_comm_id(dist, ctx.rank, Engine.comm_unique_id))
     fi = STAT_NAMES.index("faults")
+    staged = bool(wl.get("staged"))
+
+    def stage(t, n):   # RAFT_CLIENT_STAGED: the caller's values for ticks [t, t+n) into HBM (never timed)
+        if staged and n > 0:
+            eng.stage_values(t, staged_values(wl["seed"], base, G, t, n, E))
+
     untimed = np.zeros(len(STAT_NAMES), np.int64)   # stats of the settle and warm-up ticks
     if churn:   # NewNode start; the first elections happen in untimed settle ticks
         eng.init_new_nodes(0)
+        stage(0, wl["settle"])
         untimed += eng.tick(0, wl["settle"], stats=True)
         tick = wl["settle"]
     else:
         eng.init_steady(leader, 0)
         tick = 1
     if warmup:
+        stage(tick, warmup)
         untimed += eng.tick(tick, warmup, stats=True)
         tick += warmup
 
@@ -336,6 +409,7 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     frozen = int(untimed[fi])
     live_steps = []
     for _ in range(max(1, repeats)):
+        stage(tick, steps)   # (inputs resident in HBM before the timed region)
         ctx.barrier()
         t0 = time.perf_counter()
         s = eng.tick(tick, steps, stats=True)
@@ -356,19 +430,40 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     # untimed passes: the steady-state kernel's own duration (events attached
     # to each of its dispatches), then the list kernel's and its group-steps
     two_pass = os.environ.get("RAFTSTEP_TWO_PASS", "1") != "0"
+    pcie = None
+    if staged:
+        # the same call with the values crossing PCIe inside the timed span
+        # (raft_stage_values from host memory, then the ticks): never `value`
+        vals = staged_values(wl["seed"], base, G, tick, steps, E)
+        ctx.barrier()
+        t0 = time.perf_counter()
+        eng.stage_values(tick, vals)
+        t1 = time.perf_counter()
+        eng.tick(tick, steps, stats=True)
+        ctx.barrier()
+        t2 = time.perf_counter()
+        tick += steps
+        pcie = {"value": G * world * steps / (t2 - t0), "stage_ms": (t1 - t0) * 1e3,
+                "stage_GBs": vals.nbytes / max(t1 - t0, 1e-9) / 1e9, "ms_per_step": (t2 - t0) * 1e3 / steps,
+                "what": "raft_stage_values (host buffer -> HBM, %d MB) + the %d ticks, one call, wall clock"
+                        % (vals.nbytes // 1000000, steps)}
+        del vals
     eng.profile(1)
+    stage(tick, steps)
     eng.tick(tick, steps, stats=False)
     tick += steps
     kernel_ms, kernel_ticks = eng.profile_read()
     list_ms = list_launches = list_steps = 0
     if two_pass and churn:   # the second pass (list kernel over the groups the lean kernel passed on)
         eng.profile(3)
+        stage(tick, steps)
         eng.tick(tick, steps, stats=False)
         tick += steps
         list_ms, list_launches = eng.profile_read()
         eng.profile(0)
         if list_count:   # (separately: the class counters cost time) listed group-steps per launch
             eng.diag_enable(True)
+            stage(tick, steps)
             eng.tick(tick, steps, stats=False)
             tick += steps
             list_steps = eng.diag_read()["list_lanes"]
@@ -398,6 +493,12 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     if churn:
         ok = bool(wl.get("allow_faults") or
                   (faults == 0 and stats[STAT_NAMES.index("leader_groups")] > 0.5 * G * world * steps * reps))
+    elif wl.get("corrupt"):
+        # CRC32C rejections in the timed region: a rejected copy fails that
+        # follower's AppendEntries (the only failures of a steady REF group);
+        # the leader still commits whenever 3 of its 4 peers match
+        ok = bool(faults * 100000 <= G * world and stats[STAT_NAMES.index("ae_fail")] > 0 and
+                  stats[STAT_NAMES.index("committed")] > 0.99 * G * world * steps * E * reps)
     else:
         ok = bool(stats[STAT_NAMES.index("committed")] == G * world * steps * E * reps and faults == 0)
 
@@ -408,8 +509,8 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     mean_tpl = steps / -(-steps // tpl) if fused else 1
     iso = "iso" in wl and wl["iso"][0] > 0
     B = lean_bytes(R, E, crc, segmented=iso, fuse=mean_tpl, glx=iso and wl.get("semantics", 0) == 1,
-                   shared=shared) if two_pass else \
-        algorithmic_bytes(R, E, crc)
+                   shared=shared, staged=staged) if two_pass else \
+        algorithmic_bytes(R, E, crc) + (8 * E if staged else 0)
     kname = ("tick_fused_kernel" if fused else "tick_lean_kernel") if two_pass else "tick_fast_kernel"
     avg_kernel_s = kernel_ms / 1e3 / max(kernel_ticks, 1)   # per tick
     # C4REF: the lean kernel's algorithmic bytes are those of the live groups it
@@ -459,12 +560,25 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
         "semantics": "RAFT (EXT, Raft paper)" if wl.get("semantics") else "REF (main.go)",
         "ticks_per_launch": tpl,
         "storage_forms": feats,
+        "client_values": ("staged by the caller in HBM (RAFT_CLIENT_STAGED, raft_stage_values), never regenerated"
+                          if staged else "trace RNG on the device (RAFT_CLIENT_TRACE)"),
         "timing": {"repeats": reps, "median_s": elapsed, "repeat_ms_per_step": [t * 1e3 / steps for t in times]},
         "roofline": roof,
         "stats": dict(zip(STAT_NAMES, [int(x) for x in stats])),
         "stats_check": ok,
         "rccl": {"nranks": nranks, "stat_allreduces": allreduces},
     }
+    if pcie is not None:
+        line["pcie_inclusive"] = pcie
+    if wl.get("corrupt"):
+        st = line["stats"]
+        line["verification"] = {
+            "corrupt_per_65536": wl["corrupt"], "rejections": st["ae_fail"],
+            "entries_verified": (st["ae_ok"] + st["ae_fail"]) * E,
+            "what": "every follower checks each received entry against the leader's CRC32C stamp (an unaltered "
+                    "copy carries the stamp itself; a corrupted copy -- its last value's bit 0 flipped -- is "
+                    "recomputed and rejected: AppendEntries false, main.go:148-149 append skipped); rejections = "
+                    "AppendEntries answered false in the timed region"}
     if two_pass and churn:
         # the list kernel: the full fast-path body over the groups the lean
         # kernel passed on (elections, first rounds, returns, isolated
@@ -694,6 +808,32 @@ def main():
                 "note": "the headline's 2^20 groups keep their 40 B of per-group words (42 MB) L3-resident between "
                         "ticks, so part of its `achieved` is Infinity-Cache-served; this line's frac is the HBM "
                         "fraction of the same kernel (extra_workloads.C2X)"}
+    # flat copies of the nested numbers a reader of the driver's record needs
+    # (the driver's `parsed` keeps top-level scalars only)
+    r0 = result["roofline"]
+    flat = {"roofline_frac": r0["frac"], "roofline_achieved_GBs": r0["achieved"],
+            "lean_kernel_us_per_tick": r0["avg_kernel_us_per_tick"],
+            "stream_probe_GBs": (r0.get("stream_probe") or {}).get("GBs"),
+            "frac_of_stream_probe": r0.get("frac_of_stream_probe"),
+            "l3_proof_frac": (r0.get("l3_proof") or {}).get("frac"),
+            "l3_proof_GBs": (r0.get("l3_proof") or {}).get("achieved"),
+            "cpu_baseline_value": (result.get("cpu_baseline") or {}).get("value"),
+            "fused_value": (fused or {}).get("value")}
+    for name, x in extras.items():
+        if "value" not in x:
+            continue
+        flat[f"{name}_value"] = x["value"]
+        flat[f"{name}_frac"] = x["roofline"]["frac"]
+        flat[f"{name}_kernel_us"] = x["roofline"]["avg_kernel_us_per_tick"]
+        flat[f"{name}_stats_check"] = x["stats_check"]
+        if "pcie_inclusive" in x:
+            flat[f"{name}_pcie_inclusive_value"] = x["pcie_inclusive"]["value"]
+        if "verification" in x:
+            flat[f"{name}_rejections"] = x["verification"]["rejections"]
+        if "list_kernel" in x:
+            flat[f"{name}_list_kernel_us"] = x["list_kernel"]["avg_us"]
+    result["flat"] = "the *_value / *_frac / ... keys below copy nested numbers to the top level"
+    result.update({k: v for k, v in flat.items() if v is not None})
     result["bench_wall_s"] = time.perf_counter() - t_start
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RAFT_ABI_VERSION 5u
+#define RAFT_ABI_VERSION 6u
 #define RAFT_MAX_REPLICAS 8u
 
 /* Node.State (main.go:51-57). */
@@ -113,8 +113,23 @@ typedef struct raft_config {
                                   many steady ticks run in one launch of the fused kernel (state kept in registers
                                   between them; results identical, not the §8(d) form) */
   uint32_t debug_flags;        /* RAFT_DEBUG_*; 0 in production */
-  uint32_t reserved[3];        /* must be 0 */
+  uint32_t client_source;      /* enum raft_client_source: where the client's values (main.go:92) come from */
+  uint32_t reserved[2];        /* must be 0 */
 } raft_config;
+
+/* raft_config.client_source. The reference's client sends rand.Int() to
+ * every node whose State is Leader (main.go:87-93 -> LogReq -> 327-329).
+ *  RAFT_CLIENT_TRACE  (0): the values come from the seeded trace RNG on the
+ *      device (splitmix64 keyed by seed, group, replica, tick, entry);
+ *  RAFT_CLIENT_STAGED (1): the caller supplies them. Before raft_tick runs
+ *      ticks [t0, t0+n) the caller stages n x E x G int64 values with
+ *      raft_stage_values; every Leader of group g at tick t appends
+ *      values[((t - t0) * E + e) * G + g] as its e-th entry of that tick (one
+ *      client request per group and entry, sent to whichever replicas are
+ *      leaders, like main.go:90-93). The engine never regenerates an entry in
+ *      this mode: entries are read from the staged buffer when appended and
+ *      from the rings afterwards. */
+enum raft_client_source { RAFT_CLIENT_TRACE = 0, RAFT_CLIENT_STAGED = 1 };
 
 /* raft_config.debug_flags */
 #define RAFT_DEBUG_ALLOW_WRONG_RESULTS 1u  /* accept the timing-only environment knob RAFTSTEP_DIAG_LEAN, whose modes
@@ -217,6 +232,15 @@ int raft_checkpoint_load(raft_engine* e, const char* path);
  *      at once by the new candidate's vote round (main.go:171-177, 248-251).
  * `out` (may be NULL) receives the stats summed over the ticks. */
 int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_stats* out);
+/* RAFT_CLIENT_STAGED engines: the client values of ticks [first_tick,
+ * first_tick + nticks), laid out [nticks][E][G] int64 (E = entries_per_tick,
+ * G = groups of this engine, indexed by the local group; the value stream of
+ * main.go:92, one request per group, tick and entry, LogReq at main.go:327-329).
+ * Copied into HBM (the host buffer is only borrowed for the call); replaces
+ * whatever was staged before. raft_tick then accepts calls whose ticks lie
+ * inside the staged range (RAFT_EINVAL otherwise). RAFT_EINVAL on a
+ * RAFT_CLIENT_TRACE engine. */
+int raft_stage_values(raft_engine* e, int64_t first_tick, uint32_t nticks, const int64_t* values);
 /* Per-tick statistics of the last raft_tick call that asked for stats: record
  * t (0 <= t < nticks of that call) holds tick first_tick+t, summed over groups
  * and, with a communicator, over GPUs (the 64-B record the all-reduce carries). */
@@ -359,6 +383,8 @@ enum raft_diag_counter {
   RAFT_DIAG_LIST_LXS_VX = 29,         /* LXS entered with a virtual suffix */
   RAFT_DIAG_LEAN_SH = 30,             /* steady ticks whose entries went to the shared ring (SH) */
   RAFT_DIAG_LIST_SH_COPIED = 31,      /* groups in shared form whose entries the list kernel copied back */
+  RAFT_DIAG_LIST_SH_ENTRIES = 1,      /* ... the shared entries it copied (0 for groups closed ahead of a window) */
+  RAFT_DIAG_LEAN_SH_CLOSED = 2,       /* groups whose shared form closed ahead of an isolation window start */
   RAFT_DIAG_LEAN_SWITCH = 5,          /* ring segment switches */
   /* full fast-path body (list kernel / one-pass kernel): 32 + bit */
   RAFT_DIAG_LIST_LANES = 42,          /* groups looked at */
@@ -409,8 +435,11 @@ int raft_debug_diag_mode(raft_engine* e, uint32_t mode);
  * fresh elements on `device`, no Raft state: one untimed pass, then `reps`
  * back-to-back passes between HIP events. Returns the mean pass time and the
  * bytes per pass (bench.py: the device's sustained rate for that pattern). */
-int raft_stream_probe(int device, uint32_t replicas, uint64_t elems, uint32_t reps, double* us_per_pass,
-                      double* bytes_per_pass);
+#define RAFT_PROBE_PLAIN_RING 1u    /* plain (write-back) ring stores instead of non-temporal ones */
+#define RAFT_PROBE_NT_RECORD 2u     /* non-temporal record / heartbeat stores */
+#define RAFT_PROBE_NO_HEARTBEAT 4u  /* no heartbeat store (a group in shared form): 16 B written + ring */
+int raft_stream_probe(int device, uint32_t replicas, uint64_t elems, uint32_t reps, uint32_t flags,
+                      double* us_per_pass, double* bytes_per_pass);
 
 #ifdef __cplusplus
 }

@@ -39,6 +39,7 @@ def load(path=None):
             "oracle_load_state": (C.c_int, [P, P]),
             "oracle_store_state": (None, [P, P]),
             "oracle_tick": (None, [P, C.c_int64, C.c_uint32, C.c_int, P]),
+            "oracle_stage_values": (C.c_int, [P, C.c_int64, C.c_uint32, P]),
             "oracle_append_entries": (C.c_int, [P, C.c_int64, P, C.c_size_t, P, P]),
             "oracle_request_vote": (C.c_int, [P, C.c_int64, P, C.c_size_t, P]),
             "oracle_group_ops": (C.c_int, [P, C.c_int64, P, C.c_size_t, P]),
@@ -119,7 +120,18 @@ class Oracle:
         v = abi.make_view(st)
         _check(self.lib.oracle_load_state(self.h, C.byref(v)))
 
+    def stage_values(self, first_tick, values):
+        """RAFT_CLIENT_STAGED: values[t][e][g] for ticks first_tick.. (raft_stage_values' layout)."""
+        v = np.ascontiguousarray(values, dtype=np.int64)
+        assert v.ndim == 3 and v.shape[1:] == (self.cfg.entries_per_tick, self.cfg.groups), v.shape
+        _check(self.lib.oracle_stage_values(self.h, int(first_tick), v.shape[0], _ptr(v)))
+        self._staged = (int(first_tick), v.shape[0])
+
     def tick(self, first_tick, nticks=1, stats=True, threads=1):
+        if self.cfg.client_source == abi.CLIENT_STAGED:
+            t0, n = getattr(self, "_staged", (0, 0))
+            if nticks and not (t0 <= first_tick and first_tick + nticks <= t0 + n):
+                raise OracleError(f"ticks [{first_tick}, {first_tick + nticks}) are not staged")
         s = abi.TickStats()
         self.lib.oracle_tick(self.h, first_tick, nticks, threads, C.byref(s))
         return np.array(s.v, dtype=np.int64) if stats else None

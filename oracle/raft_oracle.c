@@ -153,11 +153,18 @@ static uint32_t group_iso_mask(const raft_config* c, uint64_t gid, o_group* G, i
 struct oracle {
   raft_config cfg;
   o_group* g;
+  /* RAFT_CLIENT_STAGED: the caller's client values [cv_n][E][G] for ticks
+   * [cv_t0, cv_t0 + cv_n) (oracle_stage_values; raftstep.h raft_stage_values) */
+  int64_t* cv;
+  int64_t cv_t0;
+  uint32_t cv_n;
 };
 
 typedef struct {                                 /* one handler invocation's context */
   const raft_config* cfg;
   uint64_t gid;
+  const int64_t* cv;                             /* staged values of this group and tick (entry e at cv[e*G]), or NULL */
+  uint64_t cv_stride;
   int64_t tick, now;
   int64_t st[RAFT_NSTATS];
   uint32_t iso;                                  /* EXT: replicas cut off this tick (bit r) */
@@ -596,7 +603,10 @@ static void tick_group(o_ctx* c, o_group* G) {
     for (int r = 0; r < R && !G->fault; ++r) {
       if (G->n[r].role != RAFT_LEADER) continue;
       for (uint32_t e = 0; e < c->cfg->entries_per_tick && !G->fault; ++e)
-        client_append(c, G, r, (int64_t)oracle_client_value(c->cfg->seed, c->gid, (uint32_t)r, (uint64_t)c->tick, e));
+        /* rand.Int() (main.go:92), or the request the caller staged for the group
+         * (RAFT_CLIENT_STAGED: the same value to every leader, main.go:90-93) */
+        client_append(c, G, r, c->cv ? c->cv[(uint64_t)e * c->cv_stride]
+                                     : (int64_t)oracle_client_value(c->cfg->seed, c->gid, (uint32_t)r, (uint64_t)c->tick, e));
     }
   }
   /* 2. rounds, ascending replica id */
@@ -644,6 +654,7 @@ void oracle_destroy(oracle* o) {
   if (!o) return;
   free_logs(o);
   free(o->g);
+  free(o->cv);
   free(o);
 }
 
@@ -652,6 +663,10 @@ static o_ctx make_ctx(const oracle* o, uint64_t g, int64_t tick) {
   memset(&c, 0, sizeof c);
   c.cfg = &o->cfg;
   c.gid = o->cfg.group_base + g;
+  if (o->cfg.client_source == RAFT_CLIENT_STAGED && o->cv && tick >= o->cv_t0 && tick < o->cv_t0 + (int64_t)o->cv_n) {
+    c.cv = o->cv + ((uint64_t)(tick - o->cv_t0) * o->cfg.entries_per_tick) * o->cfg.groups + g;
+    c.cv_stride = o->cfg.groups;
+  }
   c.tick = tick;
   c.now = tick * o->cfg.tick_seconds;
   /* message-level handlers see the windows as they stand (no leader-mode decision) */
@@ -806,7 +821,24 @@ static void* run_job(void* arg) {
   return NULL;
 }
 
+int oracle_stage_values(oracle* o, int64_t first_tick, uint32_t nticks, const int64_t* values) {
+  if (o->cfg.client_source != RAFT_CLIENT_STAGED || (nticks && !values)) return -22;
+  const size_t n = (size_t)nticks * o->cfg.entries_per_tick * o->cfg.groups;
+  free(o->cv);
+  o->cv = n ? (int64_t*)malloc(n * sizeof(int64_t)) : NULL;
+  if (n) memcpy(o->cv, values, n * sizeof(int64_t));
+  o->cv_t0 = first_tick;
+  o->cv_n = nticks;
+  return 0;
+}
+
 void oracle_tick(oracle* o, int64_t first_tick, uint32_t nticks, int nthreads, raft_tick_stats* out) {
+  if (o->cfg.client_source == RAFT_CLIENT_STAGED &&
+      (nticks && (!o->cv || first_tick < o->cv_t0 || first_tick + (int64_t)nticks > o->cv_t0 + (int64_t)o->cv_n))) {
+    fprintf(stderr, "oracle_tick: ticks [%lld, %lld) are not staged\n", (long long)first_tick,
+            (long long)(first_tick + nticks));
+    abort();   /* (test infrastructure: oracle.py checks the range first) */
+  }
   if (nthreads < 1) nthreads = 1;
   if ((uint64_t)nthreads > o->cfg.groups) nthreads = o->cfg.groups ? (int)o->cfg.groups : 1;
   o_job* jobs = (o_job*)calloc((size_t)nthreads, sizeof(o_job));

@@ -36,6 +36,9 @@ void oracle_store_state(const oracle* o, raft_state_view* v);
 /* Runs nticks ticks; groups are split into nthreads contiguous ranges, each
  * run by its own pthread through all ticks (groups are independent). */
 void oracle_tick(oracle* o, int64_t first_tick, uint32_t nticks, int nthreads, raft_tick_stats* out);
+/* RAFT_CLIENT_STAGED: client values of ticks [first_tick, +nticks), [nticks][E][G]
+ * over the oracle's groups (raft_stage_values' layout); 0 or -22. */
+int oracle_stage_values(oracle* o, int64_t first_tick, uint32_t nticks, const int64_t* values);
 int oracle_append_entries(oracle* o, int64_t now_tick, const raft_ae_req* reqs, size_t n,
                           const raft_log_entry* entries, raft_ae_resp* out);
 int oracle_request_vote(oracle* o, int64_t now_tick, const raft_vote_req* reqs, size_t n,

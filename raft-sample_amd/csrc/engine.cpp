@@ -251,6 +251,12 @@ struct raft_engine {
   // handler-batch staging
   void* stage = nullptr;
   size_t stage_cap = 0;
+  // RAFT_CLIENT_STAGED: the caller's client values in HBM, [cv_n][E][G]
+  // int64 for ticks [cv_t0, cv_t0 + cv_n) (raft_stage_values; DevPlanes::cv)
+  int64_t* cvbuf = nullptr;
+  uint64_t cv_cap = 0;          // elements allocated
+  int64_t cv_t0 = 0;
+  uint32_t cv_n = 0;
   // profiling: 0 off, 1 per fast-kernel dispatch (hipExtLaunchKernel events),
   // 2 one event pair around each raft_tick call's launches (no per-launch cost)
   int prof = 0;
@@ -264,6 +270,8 @@ struct raft_engine {
   ncclComm_t comm = nullptr;
   hipStream_t comm_stream = nullptr;
   std::vector<hipEvent_t> comm_ev;
+  std::vector<hipEvent_t> comm_pre;   // markers before each all-reduce since the last completed wait (wait_stream)
+  size_t comm_pre_used = 0;
   int nranks = 1, rank = 0;
   uint64_t allreduces = 0;      // ncclAllReduce calls issued (diagnostics)
   bool comm_side = false;       // a sum on comm_stream the engine stream has not waited for
@@ -299,6 +307,9 @@ Trace make_trace(const raft_engine* e, int64_t tick) {
   const int64_t cf = e->contig_from;
   T.contig_q = (T.period && cf > 0) ? uint64_t((cf + int64_t(T.period) - 1) / int64_t(T.period)) * T.entries : 0u;
   if (!e->run_valid) T.contig_q = ~uint64_t(0);   // (no run: nothing regenerable)
+  // staged client values: no entry is ever regenerated (entry jobs read the
+  // rings instead: the general kernel), whatever the run
+  if (e->cfg.client_source == RAFT_CLIENT_STAGED) T.contig_q = ~uint64_t(0);
   return T;
 }
 
@@ -570,6 +581,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
     return fail(RAFT_EINVAL, "isolation length must satisfy 1 <= min <= max <= 32");
   if (c.ticks_per_launch > 64) return fail(RAFT_EINVAL, "ticks_per_launch must be 0..64 (0 and 1: one tick per launch)");
   if (c.debug_flags & ~RAFT_DEBUG_ALLOW_WRONG_RESULTS) return fail(RAFT_EINVAL, "unknown debug_flags bits");
+  if (c.client_source > RAFT_CLIENT_STAGED) return fail(RAFT_EINVAL, "client_source must be RAFT_CLIENT_TRACE or RAFT_CLIENT_STAGED");
   for (uint32_t w : c.reserved)
     if (w) return fail(RAFT_EINVAL, "reserved config words must be 0");
   // RAFTSTEP_DIAG_LEAN (timing diagnostics of the lean / list kernels) skips
@@ -636,6 +648,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
     e->P.grotb = Strided<uint16_t, 16>{&e->P.gseg->rotb};
     e->P.gsb2 = Strided<int32_t, 16>{&e->P.gseg->sb2};
     e->P.gshf = Strided<int32_t, 16>{&e->P.gseg->shf};
+    e->P.gshn = Strided<uint16_t, 16>{&e->P.gseg->shn};
   }
   // sharded group lists (raft_device.hpp): NSHARD shards of scap entries
   const uint64_t scap = ((Gp / 256 + NSHARD - 1) / NSHARD) * 256;
@@ -655,9 +668,18 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   // shared entries (raft_device.hpp ROT_SH): without EXT isolation churn (under
   // it groups leave the steady form too often for the copy-back to pay), with
   // slots below the rotation's flag bit; RAFTSTEP_SH=0 turns them off
-  e->P.sh = (c.isolate_per_65536 == 0 && K < ROT_SH) ? 1u : 0u;
+  // (round 6: under isolation churn too, closed ahead of every window start,
+  // DevPlanes::sh_look; RAFTSTEP_SH=3 keeps them open under churn — the round-5
+  // form, whose copy-backs at window starts made C4 4x slower: A/B only)
+  e->P.sh = K <= ROT_SHX / 2 ? 1u : 0u;
   if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 0) e->P.sh = 0;
-  if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 2 && K < ROT_SH) e->P.sh = 1;   // (also under churn)
+  e->P.sh_look = 0;
+  if (e->P.sh && c.isolate_per_65536 && c.client_period && c.entries_per_tick) {
+    // client ticks enough for K entries (E per client tick), in ticks, + one period of margin
+    const uint64_t ct = (c.ring_depth + c.entries_per_tick - 1) / c.entries_per_tick;
+    e->P.sh_look = uint32_t(std::min<uint64_t>((ct + 1) * c.client_period, 1u << 20));
+    if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 3) e->P.sh_look = 0;
+  }
   if (e->P.sh) {
     A(reinterpret_cast<void**>(&e->P.sh_term), K * Gp * 4);
     A(reinterpret_cast<void**>(&e->P.sh_value), K * Gp * 8);
@@ -697,6 +719,9 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   // virtual suffixes (M_VX): RAFT leader isolation without payload CRC; RAFTSTEP_VX=0 turns them off
   e->P.vx = (raft && c.isolate_per_65536 && c.isolate_leader && !c.payload_crc) ? 1u : 0u;
   if (const char* vx = getenv("RAFTSTEP_VX"); vx && atoi(vx) == 0) e->P.vx = 0;
+  // a virtual suffix is regenerated from the trace RNG: never with staged client values
+  if (c.client_source == RAFT_CLIENT_STAGED) e->P.vx = 0;
+  e->P.cv = nullptr;   // (raft_stage_values)
   e->P.corrupt_p = c.corrupt_per_65536;
   if (const char* fg = getenv("RAFTSTEP_FORCE_GENERAL")) e->force_general = atoi(fg) != 0;
   if (const char* gk = getenv("RAFTSTEP_GENERAL")) e->lane_general = std::strcmp(gk, "lane") == 0;
@@ -765,6 +790,7 @@ int raft_engine_destroy(raft_engine* e) {
   if (e->comm) (void)ncclCommDestroy(e->comm);
   for (hipEvent_t x : e->ev) (void)hipEventDestroy(x);
   for (hipEvent_t x : e->comm_ev) (void)hipEventDestroy(x);
+  for (hipEvent_t x : e->comm_pre) (void)hipEventDestroy(x);
   if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
   if (e->gen_stream) (void)hipStreamSynchronize(e->gen_stream);
   if (e->list_stream) (void)hipStreamSynchronize(e->list_stream);
@@ -789,6 +815,7 @@ int raft_engine_destroy(raft_engine* e) {
   if (e->chk_ev) (void)hipEventDestroy(e->chk_ev);
   if (e->cstat) (void)hipFree(e->cstat);
   if (e->stage) (void)hipFree(e->stage);
+  if (e->cvbuf) (void)hipFree(e->cvbuf);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return RAFT_OK;
@@ -1129,6 +1156,9 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   return RAFT_OK;
 }
 
+static int wait_stream(raft_engine* e, hipStream_t s = nullptr);
+static int comm_marker(raft_engine* e, hipStream_t s);
+
 // Stats of the window [w0, w1] (indices into this call's ticks) are final
 // once its general kernel has run: reduce them to per-tick records and, with
 // a communicator, sum those across GPUs on the comm stream (ordered by an
@@ -1165,6 +1195,7 @@ static int flush_window_stats(raft_engine* e, uint32_t w0, uint32_t w1, const Ca
     HIPCHK(hipStreamWaitEvent(e->comm_stream, e->comm_ev[0], 0));
     e->comm_side = true;
   }
+  if (int rc = comm_marker(e, cs)) return rc;
   RCCLCHK(ncclAllReduce(e->tstat + size_t(w0) * NSTAT, e->tstat + size_t(w0) * NSTAT, size_t(n) * NSTAT, ncclUint64,
                         ncclSum, e->comm, cs));
   ++e->allreduces;
@@ -1201,12 +1232,27 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
   if (e->hist_dirty) {
     // a failed call's per-tick slots were never reduced (the reduce is what
     // re-zeroes them): zero every slot it may have counted into, after all of
-    // its kernels (on any of the engine's streams) are done, or the next
-    // call's stats would include them
-    HIPCHK(hipDeviceSynchronize());
+    // its kernels are done, or the next call's stats would include them. Only
+    // this engine's streams are joined (not the whole device, which
+    // would wait on other engines too), the comm stream with wait_stream's bound.
+    for (hipStream_t s : {e->gen_stream, e->list_stream, e->half_stream})
+      if (s) HIPCHK(hipStreamSynchronize(s));
+    if (e->comm_stream)
+      if (int rc = wait_stream(e, e->comm_stream)) return rc;
+    if (int rc = wait_stream(e)) return rc;
     HIPCHK(hipMemsetAsync(e->hist, 0, size_t(e->hist_dirty) * STAT_TICK * 8, e->stream));
     e->hist_dirty = 0;
   }
+  // a failed call may have left groups in shared form with an unknown implied
+  // heartbeat time: poison now, whatever tick this call starts at (ADVICE r5;
+  // sh_flush below runs only for a call after a tick gap)
+  if (e->sh_live && !e->sh_done)
+    if (int rc = sh_heartbeat(e)) return rc;
+  if (e->cfg.client_source == RAFT_CLIENT_STAGED && nticks &&
+      (!e->cv_n || first_tick < e->cv_t0 || first_tick + int64_t(nticks) > e->cv_t0 + int64_t(e->cv_n)))
+    return fail(RAFT_EINVAL, "client_source RAFT_CLIENT_STAGED: ticks [%lld, %lld) are not staged (raft_stage_values "
+                "holds [%lld, %lld))", (long long)first_tick, (long long)(first_tick + nticks), (long long)e->cv_t0,
+                (long long)(e->cv_t0 + e->cv_n));
   // (the per-tick records need nticks slots; the check records exist at any capacity)
   if (int rc = ensure_hist(e, stats ? std::max<uint32_t>(nticks, 1) : 1)) return rc;
   if (!nticks) return RAFT_OK;
@@ -1547,31 +1593,69 @@ static int tick_impl(raft_engine* e, int64_t first_tick, uint32_t nticks, bool s
 // RAFTSTEP_COMM_TIMEOUT_S: an all-reduce whose peers never arrive (a rank
 // gone, or ranks issuing different collectives) aborts the communicator and
 // poisons the engine with RAFT_ETIMEDOUT instead of hanging the caller.
-static int wait_stream(raft_engine* e) {
+// The clock times the collectives, not the call's compute: every
+// all-reduce is preceded by a marker event on its stream (comm_pre, recorded
+// by flush_window_stats / raft_comm_allreduce_stats), and the budget runs
+// from the latest marker that has completed — i.e. only while an all-reduce
+// (and the short compute after it) is outstanding, restarting whenever the
+// call makes progress past another marker. Compute before the first marker
+// always finishes and is waited for without a bound. The host sleeps between
+// polls after the first 2 ms.
+static int wait_stream(raft_engine* e, hipStream_t s) {
+  if (!s) s = e->stream;
   if (!e->comm) {
-    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipStreamSynchronize(s));
     return RAFT_OK;
   }
-  const auto t0 = std::chrono::steady_clock::now();
   const double tmo = comm_timeout_s();
+  const auto start = std::chrono::steady_clock::now();
+  auto t0 = start;
+  bool armed = false;            // a marker has completed: an all-reduce may be what is outstanding
+  size_t seen = 0;               // markers known complete (they complete in issue order per stream)
   for (;;) {
-    const hipError_t q = hipStreamQuery(e->stream);
-    if (q == hipSuccess) return RAFT_OK;
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) {
+      e->comm_pre_used = 0;
+      return RAFT_OK;
+    }
     if (q != hipErrorNotReady) return fail(RAFT_EHIP, "hipStreamQuery: %s", hipGetErrorString(q));
-    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (el > tmo) {
+    const auto now = std::chrono::steady_clock::now();
+    bool progress = false;
+    while (seen < e->comm_pre_used && hipEventQuery(e->comm_pre[seen]) == hipSuccess) {
+      ++seen;
+      progress = true;
+    }
+    if (progress) {
+      armed = true;
+      t0 = now;
+    }
+    const double el = std::chrono::duration<double>(now - t0).count();
+    if (armed && el > tmo) {
       (void)ncclCommAbort(e->comm);
       e->comm = nullptr;
+      e->comm_pre_used = 0;
       e->poisoned = true;
       e->poison_msg = "RCCL statistics all-reduce did not complete within " + std::to_string(int(tmo)) +
                       " s (RAFTSTEP_COMM_TIMEOUT_S): communicator aborted";
       return fail(RAFT_ETIMEDOUT, "%s", e->poison_msg.c_str());
     }
-    if (el > 2e-3) std::this_thread::yield();
+    if (std::chrono::duration<double>(now - start).count() > 2e-3)
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
 #if defined(__x86_64__) || defined(__i386__)
     else __builtin_ia32_pause();
 #endif
   }
+}
+
+// A marker on stream s just before an all-reduce is enqueued there (wait_stream).
+static int comm_marker(raft_engine* e, hipStream_t s) {
+  if (e->comm_pre_used == e->comm_pre.size()) {
+    hipEvent_t x;
+    HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+    e->comm_pre.push_back(x);
+  }
+  HIPCHK(hipEventRecord(e->comm_pre[e->comm_pre_used++], s));
+  return RAFT_OK;
 }
 
 // longest host spin on a mirrored call's completion word (raft_tick)
@@ -1628,6 +1712,37 @@ int raft_tick(raft_engine* e, int64_t first_tick, uint32_t nticks, raft_tick_sta
       if (e->steady_origin) e->steady_ok = c[CHK_LISTED] == 0 && c[CHK_DEFERRED] == 0;
     }
   }
+  return RAFT_OK;
+}
+
+int raft_stage_values(raft_engine* e, int64_t first_tick, uint32_t nticks, const int64_t* values) {
+  if (!e || (nticks && !values)) return fail(RAFT_EINVAL, "null argument");
+  if (e->cfg.client_source != RAFT_CLIENT_STAGED)
+    return fail(RAFT_EINVAL, "raft_stage_values needs client_source RAFT_CLIENT_STAGED");
+  if (int rc = check_ticks(e, first_tick, nticks)) return rc;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  // every kernel that may read the previous values has finished once the
+  // engine stream has: each call joins its other streams into it at its end
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const uint64_t n = uint64_t(nticks) * e->cfg.entries_per_tick * e->cfg.groups;
+  if (n > e->cv_cap) {
+    if (e->cvbuf) HIPCHK(hipFree(e->cvbuf));
+    e->cvbuf = nullptr;
+    e->cv_cap = 0;
+    e->cv_n = 0;
+    e->P.cv = nullptr;
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&e->cvbuf), n * 8));
+    e->cv_cap = n;
+  }
+  e->cv_n = 0;   // (until the copy has gone through)
+  e->P.cv = nullptr;
+  if (n) HIPCHK(hipMemcpy(e->cvbuf, values, n * 8, hipMemcpyHostToDevice));
+  e->cv_t0 = first_tick;
+  e->cv_n = nticks;
+  e->P.cv = nticks ? e->cvbuf : nullptr;
+  e->P.cv_t0 = first_tick;
+  e->P.cv_stride = e->cfg.groups;
+  e->P.cv_tstride = uint64_t(e->cfg.entries_per_tick) * e->cfg.groups;
   return RAFT_OK;
 }
 
@@ -1788,10 +1903,14 @@ int raft_comm_init(raft_engine* e, int nranks, int rank, const uint8_t id[128]) 
   // thread so that a missing rank, or ranks disagreeing on nranks or the id,
   // ends in RAFT_ETIMEDOUT with a message instead of a hang (the caller then
   // exits; a helper still blocked in RCCL is abandoned with the process)
+  // (a helper that completes after the caller gave up finds the
+  // job abandoned and aborts the communicator it made, so peers that did
+  // finish their init see its rank leave instead of a rank that never
+  // issues a collective; a retry starts a fresh job)
   struct InitJob {
     std::mutex m;
     std::condition_variable cv;
-    bool done = false;
+    bool done = false, abandoned = false;
     ncclResult_t r = ncclSuccess;
     ncclComm_t comm = nullptr;
   };
@@ -1801,6 +1920,10 @@ int raft_comm_init(raft_engine* e, int nranks, int rank, const uint8_t id[128]) 
     ncclComm_t c = nullptr;
     ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclCommInitRank(&c, nranks, uid, rank) : ncclInvalidUsage;
     std::lock_guard<std::mutex> lk(job->m);
+    if (job->abandoned) {
+      if (c) (void)ncclCommAbort(c);
+      return;
+    }
     job->r = r;
     job->comm = c;
     job->done = true;
@@ -1808,10 +1931,12 @@ int raft_comm_init(raft_engine* e, int nranks, int rank, const uint8_t id[128]) 
   }).detach();
   const double tmo = comm_timeout_s();
   std::unique_lock<std::mutex> lk(job->m);
-  if (!job->cv.wait_for(lk, std::chrono::duration<double>(tmo), [&] { return job->done; }))
+  if (!job->cv.wait_for(lk, std::chrono::duration<double>(tmo), [&] { return job->done; })) {
+    job->abandoned = true;
     return fail(RAFT_ETIMEDOUT, "raft_comm_init: ncclCommInitRank(nranks=%d, rank=%d) did not complete within %.0f s "
                 "(RAFTSTEP_COMM_TIMEOUT_S): a rank is missing, or the ranks disagree on nranks or the unique id",
                 nranks, rank, tmo);
+  }
   if (job->r != ncclSuccess)
     return fail(RAFT_ERCCL, "raft_comm_init: ncclCommInitRank(nranks=%d, rank=%d): %s", nranks, rank,
                 ncclGetErrorString(job->r));
@@ -1849,6 +1974,7 @@ int raft_comm_allreduce_stats(raft_engine* e, raft_tick_stats* stats) {
   std::vector<unsigned long long> h(NSTAT);
   for (int s = 0; s < NSTAT; ++s) h[s] = (unsigned long long)stats->v[s];
   HIPCHK(hipMemcpyAsync(e->cstat, h.data(), NSTAT * 8, hipMemcpyHostToDevice, e->stream));
+  if (int rc = comm_marker(e, e->stream)) return rc;
   RCCLCHK(ncclAllReduce(e->cstat, e->cstat, NSTAT, ncclUint64, ncclSum, e->comm, e->stream));
   HIPCHK(hipMemcpyAsync(h.data(), e->cstat, NSTAT * 8, hipMemcpyDeviceToHost, e->stream));
   if (int rc = wait_stream(e)) return rc;
@@ -1956,8 +2082,8 @@ int raft_debug_group_words(raft_engine* e, uint64_t group, int32_t* out, uint32_
   return RAFT_OK;
 }
 
-int raft_stream_probe(int device, uint32_t replicas, uint64_t elems, uint32_t reps, double* us_per_pass,
-                      double* bytes_per_pass) {
+int raft_stream_probe(int device, uint32_t replicas, uint64_t elems, uint32_t reps, uint32_t flags,
+                      double* us_per_pass, double* bytes_per_pass) {
   if (!us_per_pass || !bytes_per_pass) return fail(RAFT_EINVAL, "null argument");
   if (replicas < 1 || replicas > RAFT_MAX_REPLICAS || elems < 64 || elems > (1ull << 26) || reps < 1)
     return fail(RAFT_EINVAL, "replicas 1..8, elems 64..2^26, reps >= 1");
@@ -1986,9 +2112,12 @@ int raft_stream_probe(int device, uint32_t replicas, uint64_t elems, uint32_t re
                         hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess))
     rc = fail(RAFT_EHIP, "stream probe: stream / event creation failed");
   float ms = 0.f;
-  // (RAFTSTEP_PROBE_MODE: bit 0 plain ring stores, bit 1 non-temporal record stores, bit 2 no
-  // heartbeat store — the mix of a group in shared form, which bench.py selects for those lines)
-  const uint32_t mode = getenv("RAFTSTEP_PROBE_MODE") ? uint32_t(atoi(getenv("RAFTSTEP_PROBE_MODE"))) : 0u;
+  // (flags, raftstep.h RAFT_PROBE_*: bit 0 plain ring stores, bit 1 non-temporal record stores,
+  // bit 2 no heartbeat store — the mix of a group in shared form, which bench.py selects for those
+  // lines; the environment variable RAFTSTEP_PROBE_MODE replaces them, for A/Bs only)
+  if (flags & ~7u) return fail(RAFT_EINVAL, "unknown stream probe flags");
+  const char* pm = getenv("RAFTSTEP_PROBE_MODE");
+  const uint32_t mode = pm ? uint32_t(atoi(pm)) & 7u : flags;
   if (rc == RAFT_OK) {
     hipError_t h = launch_stream_probe(int(R), a, b, c, d, rt, rv, uint32_t(n), 1u, uint32_t(KS), s, mode);
     if (h == hipSuccess) h = hipEventRecord(e0, s);

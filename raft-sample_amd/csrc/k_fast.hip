@@ -586,7 +586,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           wr = 1u << c;                                   // only the leader's log grows
           w_term = Lt;
           w_ph = int((uint32_t(Ll) + uint32_t(GW.rot())) & P.kmask);
-          w_vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+          w_vb = cv_base(P, key, uint32_t(c), T.tick, g);
         }
         if (cm != Lc && !to_lxs) RW.st(PL_COMMIT, c, cm);
         int nm = (meta | M_MSYNC) & ~(M_SSYNC | M_HWX | M_LXS);   // (no truncated log here: hwup == 0)
@@ -693,8 +693,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
               (rng_k(key, uint32_t(p), ST_CORRUPT, uint64_t(T.tick)) & 0xFFFF) < P.corrupt_p)
             cm |= 1u << p;
         // (an unaltered copy carries the leader's stamp: CRCs only for cm)
-        if (cm) crcbad = crc_reject_mask(tab, crc_term_state(tab, Lt), rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick)),
-                                         n, cm);
+        if (cm) crcbad = crc_reject_mask(tab, crc_term_state(tab, Lt), cv_base(P, key, uint32_t(c), T.tick, g),
+                                         cv_stride(P), n, cm);
       }
     }
     uint32_t okm = 0, cch = 0, mch = 0, ltch = 0;
@@ -934,7 +934,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           // the stale leader's own client append (main.go:327-329) at its own log's end
           const int xl = sel(last, xi);
           if (n) {
-            const uint64_t xvb = rng_k(key, uint32_t(xi), ST_VALUE, uint64_t(T.tick));
+            const uint64_t xvb = cv_base(P, key, uint32_t(xi), T.tick, g);
             const uint64_t tb = ring_tile(g, P.KP, R);
             const uint32_t xrot = GW.rot(), xrota = GW.rota(), xrotb = GW.rotb();
             const int xsb = GW.sb(), xsb2 = GW.sb2();
@@ -942,7 +942,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             if constexpr (CRC) cs = crc_term_state(tab, x_term);
             // (VX: its entries are virtual — its column mirrors the primary's)
             for (int e = 0; e < ((meta & M_VX) ? 0 : n); ++e) {
-              const int64_t v = int64_t(sm64(xvb ^ uint64_t(uint32_t(e))) >> 1);
+              const int64_t v = cv_value(xvb, uint32_t(e), cv_stride(P));
               const uint32_t o = ring_in_tile(g, R, ring_slot(xl + 1 + e, xrot, xrota, xrotb, xsb, xsb2, P.kmask), uint32_t(xi));
               ring_stx<LIST>(P.log_term + tb, o, x_term);
               ring_stx<LIST>(P.log_value + tb, o, v);
@@ -1016,7 +1016,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
 #pragma unroll
         for (int p = 0; p < R; ++p)
           if (((okm >> p) & 1u) && last[p] - n != Ll) same = false;
-        const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+        const uint64_t vb = cv_base(P, key, uint32_t(c), T.tick, g);
         // ring rotation: index i at slot (i-1+rot) mod K; an empty group's first
         // entry goes to the global phase (its logs hold nothing to move)
         int rot = GW.rot();
@@ -1096,7 +1096,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           uint32_t cs = 0;
           if constexpr (CRC) cs = crc_term_state(tab, Lt);
           for (int e = 0; e < n; ++e) {
-            const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+            const int64_t v = cv_value(vb, uint32_t(e), cv_stride(P));
             uint32_t stamp = 0;
             if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
             // (VX: the stale leader's column mirrors the primary's entries)
@@ -1209,7 +1209,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       uint32_t cs = 0;
       if constexpr (CRC) cs = crc_term_state(tab, w_term);
       for (int e = 0; e < n; ++e) {
-        const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
+        const int64_t v = cv_value(w_vb, uint32_t(e), cv_stride(P));
         uint32_t stamp = 0;
         if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
         const uint32_t o = ring_in_tile(g, R, uint32_t((w_ph + e) & int(P.kmask)), 0u);
@@ -1273,7 +1273,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           k_on[k] = (uint32_t(__shfl(cwr, src)) >> rr) & 1u;
         }
         for (int e = 0; e < n; ++e) {
-          const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
+          const int64_t v = cv_value(w_vb, uint32_t(e), cv_stride(P));
           uint32_t stamp = 0;
           if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
           const uint32_t row = uint32_t((s0 + e) & int(P.kmask)) * 64u * R;
@@ -1489,15 +1489,19 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       // a group the lean kernel left in shared form (ROT_SH): its shared
       // entries back into the R columns first (the bit is cleared in the
       // staged rotation and written back with it)
+      // (closed, ROT_SHX, ahead of a window start: nothing left to copy)
       if (r0 & ROT_SH) {
-        sh_copy_back<R>(P, g, ss0.last, cw.shf, r0, ra0, rb0, sb0, sc0);
-        if (P.dbg) atomicAdd(&P.dbg[31], 1ull);
+        const int nc = sh_copy_back<R>(P, g, ss0.last, cw.shf, sh_end(r0, cw.shf, cw.shn), r0, ra0, rb0, sb0, sc0);
+        if (P.dbg) {
+          atomicAdd(&P.dbg[31], 1ull);
+          if (nc) atomicAdd(&P.dbg[1], (unsigned long long)nc);
+        }
       }
     }
     // (a group in shared form was taken by the lean kernel at the tick before
     // this one: its heartbeat time is implied, and written back from here)
     const int32_t hbs = (r0 & ROT_SH) ? T.at_tick(T.tick - 1).now : hb0;
-    smeta[t] = m0; sgrot[t] = uint16_t(r0 & ~ROT_SH); sgiso[t] = gi0; shb[t] = hbs; sgss[t] = ss0; sglx[t] = lx0;
+    smeta[t] = m0; sgrot[t] = uint16_t(r0 & ~ROT_SHM); sgiso[t] = gi0; shb[t] = hbs; sgss[t] = ss0; sglx[t] = lx0;
     sgrota[t] = ra0; sgrotb[t] = rb0; sgsb[t] = sb0; sgsb2[t] = sc0;
     __syncthreads();
     {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
@@ -1638,9 +1642,11 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   if (T.iso_p) im = iso_windows<R>(key, T, &act, &starting);
   bool held = false;
   bool shw = false;             // SH: this tick's entries go to the shared ring (ROT_SH)
+  bool shc = false;             // SH: the group's shared form closes this tick (ROT_SHX)
   uint32_t p_mr = 0;            // a passed group's words as read here, for its list entry
   int32_t p_sb = 0;
   SsRec p_ss{0, 0, 0, 0};
+  int64_t cv0 = 0;              // RAFT_CLIENT_STAGED: the group's entry 0 of this tick
   if (g < P.G) {
     // gmeta and, speculatively, the record, the ring rotation and the segment
     // boundary go out together: one round trip instead of two for the groups
@@ -1650,6 +1656,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
     const SsRec s = P.gss[g];
     const int rot = at(P.grot, g);
     const int sb0 = P.KP > P.K ? at(P.gsb, g) : 0;
+    // staged client values: this tick's entry 0 in the same round trip
+    if (P.cv && n) cv0 = __builtin_nontemporal_load(P.cv + uint64_t(T.tick - P.cv_t0) * P.cv_tstride + g);
     p_mr = uint32_t(meta) | (uint32_t(rot) << 16);
     p_sb = sb0;
     p_ss = s;
@@ -1715,7 +1723,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       const int L = s.last;
       // (the value stream of this tick's entries: the primary's, the only
       // appending leader but SXS's stale one, whose stream follows below)
-      const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(T.tick));
+      const uint64_t vb = cv_base(P, key, uint32_t(c), T.tick, g);
       int nl = L, cl2 = s.cl, cf2 = s.cf;   // the record after this tick
       bool hbw = false;                     // every follower's timer reset (hb = now)
       int hwx_clear = 0;                    // RAFT HWX: a truncated log in step (high-water marks in the hwm plane)
@@ -1823,10 +1831,21 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
             // (as fast_group: each follower checks the copy it received; an
             // unaltered copy carries the leader's stamp, so only cm's need a
             // CRC — the stamps themselves are computed once, in the row stores)
-            if (cm) take &= crc_reject_mask(tab, crc_term_state(tab, s.term), vb, n, cm) == 0u;
+            if (cm) take &= crc_reject_mask(tab, crc_term_state(tab, s.term), vb, cv_stride(P), n, cm) == 0u;
           }
         }
         shw = P.sh && take && n > 0 && w_slot < 0 && !sw_d && !(RAFT && (meta & M_HWX));   // (in phase only)
+        // SH under isolation churn (round 6, DevPlanes::sh_look): no shared
+        // entry is written within sh_look ticks of a window start, so at that
+        // start, when the group leaves the lean kernel, its shared entries are
+        // out of every log's window and nothing is copied back. A group in
+        // shared form closes it here (ROT_SHX: [shf, L] stay shared, this
+        // tick's entries and later ones go to the R replica rings)
+        const bool shx = (uint32_t(rot) & ROT_SHX) != 0u;
+        if (shw && (shx || (P.sh_look && window_starts_within(key, T, P.sh_look)))) {
+          shw = false;
+          shc = shm && !shx;
+        }
         nl = L + n;
         if (RAFT ? nl > s.cl : (2 * (R - 1) > R && nl > s.cl)) cl2 = nl;
         cf2 = s.cl > s.cf ? s.cl : s.cf;
@@ -1853,6 +1872,13 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
           at(P.grot, g) = uint16_t(uint32_t(rot) | ROT_SH);
           at(P.gshf, g) = L + 1;
         }
+        if (shc) {   // closed: the live shared entries are [max(shf, L+1-K), L] (a rare dependent read of shf)
+          const int shf1 = max(int(at(P.gshf, g)), L + 1 - int(P.K));
+          at(P.gshf, g) = shf1;
+          at(P.gshn, g) = uint16_t(L + 1 - shf1);
+          at(P.grot, g) = uint16_t(uint32_t(rot) | ROT_SHX);
+          df |= 4u;   // diagnostics: SH closed ahead of a window start
+        }
         if (hwx_clear) at(P.gmeta, g) = uint16_t(meta & ~M_HWX);
         if (sw_d) {   // the new segment starts at this tick's first entry
           if (sw_rota >= 0) at(P.grotb, g) = uint16_t(sw_rota);   // (else the older segments are dead)
@@ -1864,12 +1890,13 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         committed = cl2 - s.cl;
         w_term = s.term;
         w_vb = vb;
-        if (RAFT && !CRC && sxs && x_slot >= 0) x_vb = rng_k(key, uint32_t(x_r), ST_VALUE, uint64_t(T.tick));
+        if (RAFT && !CRC && sxs && x_slot >= 0) x_vb = cv_base(P, key, uint32_t(x_r), T.tick, g);
       } else {
         pass = true;
         w_slot = -1;
         x_slot = -1;
         shw = false;
+        shc = false;
       }
     }
   }
@@ -1915,14 +1942,17 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       k_on[k] = ((uint32_t(__shfl(int(wr ? wmask : 0u), src)) >> rr) & 1u) != 0u || !holes;   // (LXS: the leader's column)
       k_x[k] = anyx && ((uint32_t(__shfl(xrow ? int(1u << x_r) : 0, src)) >> rr) & 1u) != 0u;
     }
+    const uint64_t cvs = cv_stride(P);
     for (int e = 0; e < n; ++e) {
-      const int64_t v = int64_t(sm64(w_vb ^ uint64_t(uint32_t(e))) >> 1);
+      // (staged values: every leader of the group appends the same request,
+      // entry 0 already loaded with the group's words)
+      const int64_t v = (cvs && e == 0) ? cv0 : cv_value(w_vb, uint32_t(e), cvs);
       uint32_t stamp = 0;
       if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
       const uint32_t row = uint32_t((ph + e) & int(P.kmask)) * 64u * R;
       const int vlo = int(uint32_t(uint64_t(v))), vhi = int(uint32_t(uint64_t(v) >> 32));
       int64_t xv = 0;
-      if (RAFT && !CRC && x_slot >= 0) xv = int64_t(sm64(x_vb ^ uint64_t(uint32_t(e))) >> 1);
+      if (RAFT && !CRC && x_slot >= 0) xv = cvs ? v : cv_value(x_vb, uint32_t(e), 0u);
       const int xlo = int(uint32_t(uint64_t(xv))), xhi = int(uint32_t(uint64_t(xv) >> 32));
       if (wsh) {   // SH: one copy, 64 consecutive groups' entries per wave row
         const uint32_t so = uint32_t((ph + e) & int(P.kmask)) * 64u + uint32_t(lane);
@@ -2100,7 +2130,7 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
       done = j + 1;
     }
     if (n && __ballot(take)) {   // this tick's entries as whole ring rows (holes for the other lanes)
-      const uint64_t vb = rng_k(key, uint32_t(c), ST_VALUE, uint64_t(Tj.tick));
+      const uint64_t vb = take ? cv_base(P, key, uint32_t(c), Tj.tick, g) : 0ull;
       uint32_t cs = 0;
       if constexpr (CRC) cs = crc_term_state(tab, term);
       int k_term[R];
@@ -2111,7 +2141,7 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
         k_on[k] = __shfl(take ? 1 : 0, k_src[k]) != 0;
       }
       for (int e = 0; e < n; ++e) {
-        const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);
+        const int64_t v = cv_value(vb, uint32_t(e), cv_stride(P));
         uint32_t stamp = 0;
         if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
         if (P.sh) {   // (wave-uniform)

@@ -129,7 +129,8 @@ struct __attribute__((aligned(16))) GSeg {
   uint16_t rota, rotb;   // rotation of the previous / older segment
   int32_t sb2;           // first index of the previous segment (0: none older)
   uint8_t iso;           // EXT leader-isolation victims (nibble per epoch parity: 8 | replica)
-  uint8_t pad[3];
+  uint8_t pad;
+  uint16_t shn;          // SH closed (ROT_SHX): the shared entries are [shf, shf + shn) (<= K of them)
   int32_t shf;           // SH (ROT_SH): the first index whose entries live in the shared ring
 };
 // A plane of T with a byte stride S (a field of an array of records): the
@@ -176,6 +177,7 @@ struct DevPlanes {
   int64_t* sh_value;
   uint32_t* sh_crc;
   Strided<int32_t, 16> gshf;    // GSeg::shf
+  Strided<uint16_t, 16> gshn;   // GSeg::shn
   const uint32_t* crc_tab;  // 8 x 256 slice-by-8 CRC32C tables
   uint32_t crc_on;     // payload_crc
   uint32_t corrupt_p;  // EXT corruption probability / 65536
@@ -201,15 +203,27 @@ struct DevPlanes {
   // (RAFTSTEP_VX=0 turns it off); the fast paths then give a group entering
   // LXS a virtual suffix
   uint32_t vx;
-  // SH (ROT_SH) enabled: steady groups' entries go to the shared ring (no
-  // EXT isolation configured, KP < 2^15; RAFTSTEP_SH=0 turns it off)
+  // SH (ROT_SH) enabled: steady groups' entries go to the shared ring
+  // (KP < 2^14; RAFTSTEP_SH=0 turns it off)
   uint32_t sh;
+  // SH under EXT isolation churn (round 6): a group stops writing the shared
+  // ring (ROT_SHX) once an isolation window starts within the next sh_look
+  // ticks, enough client ticks for K entries: its shared entries are then out
+  // of every log's window (dead) when the window starts and takes the group
+  // off the lean kernel, so nothing is copied back (0: no isolation)
+  uint32_t sh_look;
   // SH: a group in shared form is taken by the lean (or fused) kernel every
   // tick, so its heartbeat time (hb, every follower's timer reset) is implied:
   // now of the last tick run. Its hb store is skipped; whoever copies the
   // group back writes it (the list kernel: now of the tick before its own;
   // the engine's flush and the digest: sh_hb, now of the last call's last tick)
   int32_t sh_hb;
+  // RAFT_CLIENT_STAGED: the caller's client values (raft_stage_values),
+  // [ticks][E][G] int64 from tick cv_t0 on; null: the trace RNG (cv_base)
+  const int64_t* cv;
+  int64_t cv_t0;
+  uint64_t cv_stride;   // G: between a group's entries e and e+1 of one tick
+  uint64_t cv_tstride;  // E * G: between two ticks
   uint32_t diag;       // timing-only diagnostics (RAFTSTEP_DIAG_LEAN; results are wrong when set): 1 = drifted
                        // lanes of the lean kernel skip their ring writes, 2 = they write the wave's common row
                        // (list kernel: 32 = staging alone, 64 = no tick, 128 = no ring writes / copies)
@@ -335,6 +349,15 @@ __device__ __forceinline__ uint32_t ring_in_tile(uint32_t g, uint32_t R, uint32_
 // they load a group; the engine's flush before host reads, digests and
 // handler batches). Nothing is regenerated: a flush at any time is exact.
 constexpr uint32_t ROT_SH = 0x8000u;
+// SH closed (round 6, with ROT_SH; see DevPlanes::sh_look): the group's
+// entries [shf, shf + shn) stay in the shared ring, later ones are written to
+// the R replica rings again (bit 14 of grot: KP <= 2^13, so no slot moves)
+constexpr uint32_t ROT_SHX = 0x4000u;
+constexpr uint32_t ROT_SHM = ROT_SH | ROT_SHX;
+// one past the last shared index of a group in shared form (open: none)
+__device__ __forceinline__ int sh_end(uint32_t rot, int shf, uint32_t shn) {
+  return (rot & ROT_SHX) ? shf + int(shn) : 2147483647;
+}
 __device__ __forceinline__ uint64_t sh_tile(uint32_t g, uint32_t KP) { return uint64_t(g >> 6) * (KP * 64u); }
 __device__ __forceinline__ uint32_t sh_in_tile(uint32_t g, uint32_t slot) { return slot * 64u + (g & 63u); }
 
@@ -451,13 +474,35 @@ __host__ __device__ __forceinline__ int64_t vx_value(uint64_t kv, uint64_t q, ui
   return int64_t(sm64(sm64(kv ^ (qt * period)) ^ qe) >> 1);
 }
 
+// Client values (rand.Int(), main.go:92 -> LogReq -> 327-329). A tick's
+// client append of E entries by leader r of group g is described by one
+// 64-bit value base vb: with the trace RNG (P.cv null) vb = rng_k(key, r,
+// ST_VALUE, tick) and entry e is sm64(vb ^ e) >> 1; with staged values
+// (raft_config.client_source RAFT_CLIENT_STAGED, P.cv) vb is the address of
+// the group's entry-0 value of that tick in the caller's buffer and entry e is
+// read at vb + e*G (every leader of the group appends the same request). The
+// staged values are read once, when appended (non-temporal: they are not
+// re-read, and must not push the per-group words out of the Infinity Cache).
+__device__ __forceinline__ uint64_t cv_base(const DevPlanes& P, uint64_t key, uint32_t r, int64_t tick, uint32_t g) {
+  if (P.cv) return uint64_t(reinterpret_cast<uintptr_t>(P.cv + uint64_t(tick - P.cv_t0) * P.cv_tstride + g));
+  return rng_k(key, r, ST_VALUE, uint64_t(tick));
+}
+// stride: P.cv_stride when staged, 0 with the trace RNG
+__device__ __forceinline__ int64_t cv_value(uint64_t vb, uint32_t e, uint64_t stride) {
+  // (vb 0: a lane that appends nothing; its value is never used)
+  if (stride) return vb ? __builtin_nontemporal_load(reinterpret_cast<const int64_t*>(uintptr_t(vb)) + uint64_t(e) * stride)
+                        : 0;
+  return int64_t(sm64(vb ^ uint64_t(e)) >> 1);
+}
+__device__ __forceinline__ uint64_t cv_stride(const DevPlanes& P) { return P.cv ? P.cv_stride : 0u; }
+
 // Out-of-line RNG for the general kernels' unrolled per-replica code (the
 // steady-state kernel inlines rng_k/sm64 directly).
 __device__ __attribute__((noinline)) uint64_t rng_k_call(uint64_t key, uint32_t r, uint32_t stream, uint64_t tick) {
   return rng_k(key, r, stream, tick);
 }
-__device__ __attribute__((noinline)) int64_t entry_value(uint64_t vbase, uint32_t e) {   // rand.Int() (main.go:92)
-  return int64_t(sm64(vbase ^ uint64_t(e)) >> 1);
+__device__ __attribute__((noinline)) int64_t entry_value(uint64_t vbase, uint32_t e, uint64_t stride) {   // main.go:92
+  return cv_value(vbase, e, stride);
 }
 
 // Election timer duration min + (rng >> 32) % span (main.go:114, 194). Kept
@@ -496,9 +541,10 @@ __device__ __forceinline__ uint32_t crc_entry(const uint32_t* T, int term, int64
 // `cm` receive an altered copy (EXT corruption: the batch's last value with
 // bit 0 flipped), each checked against the leader's stamp of that entry.
 // Returns the followers whose copy fails (a subset of cm).
-__device__ __forceinline__ uint32_t crc_reject_mask(const uint32_t* T, uint32_t cs, uint64_t vb, int n, uint32_t cm) {
+__device__ __forceinline__ uint32_t crc_reject_mask(const uint32_t* T, uint32_t cs, uint64_t vb, uint64_t stride, int n,
+                                                    uint32_t cm) {
   if (!cm || n <= 0) return 0u;
-  const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(n - 1))) >> 1);
+  const int64_t v = cv_value(vb, uint32_t(n - 1), stride);
   return crc_value_final(T, cs, v ^ 1) != crc_value_final(T, cs, v) ? cm : 0u;
 }
 
@@ -593,15 +639,16 @@ __device__ __forceinline__ void vx_materialize(const DevPlanes& P, uint32_t g, u
   at(P.gmeta, g) = uint16_t(meta & ~M_VX);
 }
 
-// SH (see ROT_SH): the live shared entries [max(shf, L-K+1), L] of group g
-// (every log of length L: SSYNC, normal class) into all R replica columns.
-// The caller clears ROT_SH in grot (or in its staged copy).
+// SH (see ROT_SH): the live shared entries [max(shf, L-K+1), min(she-1, L)]
+// of group g (every log of length L: SSYNC, normal class; she = sh_end) into
+// all R replica columns. The caller clears ROT_SHM in grot (or in its staged
+// copy). Returns the number of entries copied.
 template <int R>
-__device__ __forceinline__ void sh_copy_back(const DevPlanes& P, uint32_t g, int L, int shf, uint32_t rot, uint32_t rota,
-                                             uint32_t rotb, int sb, int sb2) {
+__device__ __forceinline__ int sh_copy_back(const DevPlanes& P, uint32_t g, int L, int shf, int she, uint32_t rot,
+                                            uint32_t rota, uint32_t rotb, int sb, int sb2) {
   const uint64_t tb = ring_tile(g, P.KP, R), sb_t = sh_tile(g, P.KP);
-  const int lo = max(shf, L - int(P.K) + 1);
-  for (int idx = lo; idx <= L; ++idx) {
+  const int lo = max(shf, L - int(P.K) + 1), hi = min(she - 1, L);
+  for (int idx = lo; idx <= hi; ++idx) {
     const uint32_t slot = ring_slot(idx, rot, rota, rotb, sb, sb2, P.kmask);
     const uint32_t so = sh_in_tile(g, slot), o = ring_in_tile(g, R, slot, 0u);
     const int32_t t = at(P.sh_term + sb_t, so);
@@ -614,6 +661,7 @@ __device__ __forceinline__ void sh_copy_back(const DevPlanes& P, uint32_t g, int
       if (P.crc_on) at(P.log_crc + tb, o + uint32_t(r)) = c;
     }
   }
+  return hi >= lo ? hi - lo + 1 : 0;
 }
 // ... reading every word from memory, writing the implied heartbeat time hb
 // and clearing the bit (general kernels, one-pass kernel, the engine's flush)
@@ -623,9 +671,10 @@ __device__ __forceinline__ void sh_materialize(const DevPlanes& P, uint32_t g, i
   const uint32_t rot = at(P.grot, g);
   if (!(rot & ROT_SH)) return;
   const GSeg cw = P.gseg[g];
-  sh_copy_back<R>(P, g, P.gss[g].last, cw.shf, rot, cw.rota, cw.rotb, at(P.gsb, g), cw.sb2);
+  sh_copy_back<R>(P, g, P.gss[g].last, cw.shf, sh_end(rot, cw.shf, cw.shn), rot, cw.rota, cw.rotb, at(P.gsb, g),
+                  cw.sb2);
   at(P.hb, g) = hb;   // (implied while shared: now of the last tick it was taken)
-  at(P.grot, g) = uint16_t(rot & ~ROT_SH);
+  at(P.grot, g) = uint16_t(rot & ~ROT_SHM);
 }
 
 // Group context: the R replicas of one group, in registers. SEM selects the
@@ -1509,12 +1558,13 @@ struct TickSrc {
   int leader, from;
   int cache_leader, cache_from, cache_term;
   uint64_t cache_vbase;
+  uint64_t cv_stride;   // (cv_value: 0 = trace RNG)
   __device__ __forceinline__ void fetch(int j, int& t, int64_t& v, uint32_t& c) const {
     const int idx = from + j;
     c = 0;
     if (leader == cache_leader && idx >= cache_from) {
       t = cache_term;
-      v = entry_value(cache_vbase, uint32_t(idx - cache_from));
+      v = entry_value(cache_vbase, uint32_t(idx - cache_from), cv_stride);
       if (crc_on) c = crc_entry(tab, t, v);   // the leader's stamp of its own fresh entry
     } else {
       const uint64_t tb = ring_tile(g, KP, R);

@@ -305,17 +305,17 @@ struct Seg {
   // entries of its term at [last-ecur+1, last].
   struct Src {
     int leader, from, a_n, a_from, a_term;
-    uint64_t a_vb;
+    uint64_t a_vb;   // value base of c's appends this tick (cv_base)
   };
-  __device__ __forceinline__ Src leader_src(int c, int lt, int ll) const {
-    return Src{c, 1, ecur, ll - ecur + 1, lt, ecur ? rng_k(key, uint32_t(c), ST_VALUE, uint64_t(tick)) : 0ull};
+  __device__ __forceinline__ Src leader_src(const DevPlanes& P, int c, int lt, int ll) const {
+    return Src{c, 1, ecur, ll - ecur + 1, lt, ecur ? cv_base(P, key, uint32_t(c), tick, g) : 0ull};
   }
   __device__ __forceinline__ void fetch(const DevPlanes& P, const Src& s, int j, int& t, int64_t& v, uint32_t& c) const {
     const int idx = s.from + j;
     c = 0;
     if (s.a_n && idx >= s.a_from) {
       t = s.a_term;
-      v = int64_t(sm64(s.a_vb ^ uint64_t(uint32_t(idx - s.a_from))) >> 1);   // entry_value
+      v = cv_value(s.a_vb, uint32_t(idx - s.a_from), cv_stride(P));   // entry_value
       if (P.crc_on) c = crc_entry(P.crc_tab, t, v);
     } else {
       const uint64_t tb = ring_tile(g, P.KP, R);
@@ -376,11 +376,11 @@ struct Seg {
     const uint32_t ov = mask(ld && n_ok < int(E));
     const int first_ov = first_of(ov);
     if (ld && me <= first_ov) {
-      const uint64_t vb = rng_k(key, uint32_t(me), ST_VALUE, uint64_t(tick));
+      const uint64_t vb = cv_base(P, key, uint32_t(me), tick, g);
       const int l = last;
       const int e0 = n_ok > int(P.K) ? n_ok - int(P.K) : 0;
       for (int e = e0; e < n_ok; ++e) {
-        const int64_t v = int64_t(sm64(vb ^ uint64_t(uint32_t(e))) >> 1);   // entry_value
+        const int64_t v = cv_value(vb, uint32_t(e), cv_stride(P));   // entry_value
         ring_term(P, me, l + 1 + e) = term;
         ring_value(P, me, l + 1 + e) = v;
         if (P.crc_on) ring_crc(P, me, l + 1 + e) = crc_entry(P.crc_tab, term, v);
@@ -425,7 +425,7 @@ struct Seg {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // c's ring stores before the peers read them
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const int lt = bc(term, c), ll = bc(last, c), lc = bc(commit, c), lltm = bc(ltm, c);
-    Src src = leader_src(c, lt, ll);
+    Src src = leader_src(P, c, lt, ll);
     const bool peer = act && me != c;
     int m, nx_unused;
     load_rows(P, c, peer, m, nx_unused);
@@ -592,7 +592,7 @@ struct Seg {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const int lt = bc(term, c), ll = bc(last, c), lc = bc(commit, c), lh = bc(hw, c), lltm = bc(ltm, c);
     const int K = int(P.K);
-    Src src = leader_src(c, lt, ll);
+    Src src = leader_src(P, c, lt, ll);
     const bool peer = act && me != c;
     const int pri = primary;   // rows are written back where they were read
     int m, nx;

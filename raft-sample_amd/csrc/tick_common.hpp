@@ -38,6 +38,19 @@ __device__ __forceinline__ uint32_t iso_windows(uint64_t key, const Trace& T, ui
   }
   return mask;
 }
+// Does an isolation window (either mode) start in (T.tick, T.tick + H]?
+// (SH under churn, DevPlanes::sh_look: the epochs of that range, one hash each)
+__device__ __forceinline__ bool window_starts_within(uint64_t key, const Trace& T, uint32_t H) {
+  const uint64_t inner = sm64(key ^ (uint64_t(ST_ISOLATE) << 32));
+  const int64_t t1 = T.tick + int64_t(H);
+  bool any = false;
+  for (int64_t e = (T.tick + 1) >> 5; e <= (t1 >> 5); ++e) {
+    const uint64_t h = sm64(inner ^ uint64_t(e));
+    const int64_t start = e * 32 + int64_t((h >> 24) & 31);
+    any |= (h & 0xFFFF) < T.iso_p && start > T.tick && start <= t1;
+  }
+  return any;
+}
 // Hashed-victim mode: the replicas cut off this tick.
 template <int R>
 __device__ __forceinline__ uint32_t isolation_mask(uint64_t key, const Trace& T) {
@@ -104,7 +117,7 @@ __device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, c
     static_for<R>([&](auto RI) {
       constexpr int r = decltype(RI)::value;
       if (G.role(r) != ROLE_L || !G.alive()) return;
-      const uint64_t vb = rng_k_call(G.key, r, ST_VALUE, uint64_t(G.tick));
+      const uint64_t vb = P.cv ? cv_base(P, 0, r, G.tick, G.g) : rng_k_call(G.key, r, ST_VALUE, uint64_t(G.tick));
       const int l = G.last[r];
       if (l == 0) G.align_ring(P, T);   // first entry of an empty group: choose the ring phase
       const int room = I32MAX - l;
@@ -114,7 +127,7 @@ __device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, c
       }
       const int e0 = n_ok > int(P.K) ? n_ok - int(P.K) : 0;   // only the last K stay in the ring
       for (int e = e0; e < n_ok; ++e) {
-        const int64_t v = entry_value(vb, uint32_t(e));
+        const int64_t v = entry_value(vb, uint32_t(e), cv_stride(P));
         G.ring_term(P, r, l + 1 + e) = G.term[r];
         G.ring_value(P, r, l + 1 + e) = v;
         if (P.crc_on) G.ring_crc(P, r, l + 1 + e) = crc_entry(P.crc_tab, G.term[r], v);
@@ -131,7 +144,7 @@ __device__ __forceinline__ void run_tick(Group<R, SEM>& G, const DevPlanes& P, c
 
   // 2. rounds in ascending replica id, against the roles as they are now.
   const TickSrc base{P.log_term, P.log_value, P.log_crc, P.crc_tab, P.crc_on, uint32_t(R), G.g, P.KP, P.kmask, G.rot, G.rota, G.rotb, G.sb, G.sb2, 0, 1,
-                     G.cache_leader, G.cache_from, G.cache_term, G.cache_vbase};
+                     G.cache_leader, G.cache_from, G.cache_term, G.cache_vbase, cv_stride(P)};
   auto make_src = [base](int c) {
     TickSrc s = base;
     s.leader = c;

@@ -8,11 +8,12 @@ import ctypes as C
 
 import numpy as np
 
-RAFT_ABI_VERSION = 5
+RAFT_ABI_VERSION = 6
 RAFT_MAX_REPLICAS = 8
 
 FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
 SEM_REF, SEM_RAFT = 0, 1
+CLIENT_TRACE, CLIENT_STAGED = 0, 1   # raft_config.client_source (include/raftstep.h)
 ROLE_NAMES = {FOLLOWER: "follower", CANDIDATE: "candidate", LEADER: "leader"}  # main.go:51-57
 
 F_NONE, F_PANIC_GETLOG, F_DEADLOCK_VRES, F_DEADLOCK_LEADER_VREQ, F_RING_EVICTED, F_OVERFLOW = range(6)
@@ -35,7 +36,7 @@ DIAG = {
     "lean_lxs_whole_row": 21, "lean_hwx": 22, "lean_passed": 23, "lean_forced": 24, "lean_switch": 5,
     "lean_sxs": 25, "lean_sxs_stale_in_row": 26, "list_sxs_materialised": 61, "list_sxs_entered": 62,
     "list_stale_moved": 63, "lean_sxs_vx": 27, "list_return_vx": 28, "list_lxs_vx": 29,
-    "lean_sh": 30, "list_sh_copied": 31,
+    "lean_sh": 30, "list_sh_copied": 31, "list_sh_entries": 1, "lean_sh_closed": 2,
     "list_lanes": 42, "list_deferred": 33, "list_isolation": 34, "list_switch": 37, "list_quiet": 48,
     "list_isolated_leader": 49, "list_ssync": 50, "list_election": 51, "list_first_round": 52,
     "list_return": 53, "list_return_trunc": 54, "list_stale": 55, "list_hwx": 56, "list_three_seg": 57,
@@ -60,7 +61,8 @@ class Config(C.Structure):
         ("payload_crc", C.c_uint32), ("corrupt_per_65536", C.c_uint32),
         ("isolate_leader", C.c_uint32),
         ("ticks_per_launch", C.c_uint32), ("debug_flags", C.c_uint32),
-        ("reserved", C.c_uint32 * 3),
+        ("client_source", C.c_uint32),
+        ("reserved", C.c_uint32 * 2),
     ]
 
 
@@ -86,6 +88,7 @@ def default_config(**kw):
     c.isolate_leader = 0
     c.ticks_per_launch = 1    # one tick per launch
     c.debug_flags = 0
+    c.client_source = CLIENT_TRACE   # values from the trace RNG (main.go:92's rand.Int())
     for k, v in kw.items():
         if not hasattr(c, k):
             raise TypeError(f"unknown config field {k!r}")
@@ -198,6 +201,7 @@ SIGNATURES = {
     "raft_store_state": (C.c_int, [P, P]),
     "raft_store_state_range": (C.c_int, [P, C.c_uint64, C.c_uint64, P]),
     "raft_tick": (C.c_int, [P, C.c_int64, C.c_uint32, P]),
+    "raft_stage_values": (C.c_int, [P, C.c_int64, C.c_uint32, P]),
     "raft_sync": (C.c_int, [P]),
     "raft_tick_records": (C.c_int, [P, C.c_uint32, P]),
     "raft_comm_info": (C.c_int, [P, P, P, P]),
@@ -217,8 +221,8 @@ SIGNATURES = {
     "raft_diag_read": (C.c_int, [P, P, C.c_uint32]),
     "raft_debug_force_pass": (C.c_int, [P, C.c_int64]),
     "raft_debug_diag_mode": (C.c_int, [P, C.c_uint32]),
-    "raft_stream_probe": (C.c_int, [C.c_int, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(C.c_double),
-                                    C.POINTER(C.c_double)]),
+    "raft_stream_probe": (C.c_int, [C.c_int, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
+                                    C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "raft_debug_group_words": (C.c_int, [P, C.c_uint64, P, C.c_uint32]),
 }
 
@@ -227,6 +231,7 @@ SIGNATURES = {
 # loaded through RAFTSTEP_LIB (A/B runs) may lack them
 OPTIONAL = ("raft_debug_diag_mode", "raft_stream_probe", "raft_engine_features")
 FEATURE_SHARED_ENTRIES, FEATURE_VIRTUAL_SUFFIXES = 1, 2   # raft_engine_features (include/raftstep.h)
+PROBE_PLAIN_RING, PROBE_NT_RECORD, PROBE_NO_HEARTBEAT = 1, 2, 4   # raft_stream_probe flags
 
 
 def bind(lib):

@@ -38,22 +38,15 @@ def _check(rc):
         raise RaftError(rc, load_library().raft_last_error().decode(errors="replace"))
 
 
-def stream_probe(device=0, replicas=5, elems=1 << 24, reps=10, heartbeat=True):
+def stream_probe(device=0, replicas=5, elems=1 << 24, reps=10, heartbeat=True, flags=0):
     """The steady lean kernel's byte mix on fresh buffers (raft_stream_probe):
     (us per pass, bytes per pass). heartbeat=False: without the heartbeat
-    store (a group in shared form; RAFTSTEP_PROBE_MODE bit 2)."""
+    store (a group in shared form; abi.PROBE_NO_HEARTBEAT). `flags`: further
+    abi.PROBE_* bits (store policies, A/B)."""
     lib = load_library()
     us, by = C.c_double(), C.c_double()
-    old = os.environ.get("RAFTSTEP_PROBE_MODE")
-    if not heartbeat:
-        os.environ["RAFTSTEP_PROBE_MODE"] = str(int(old or 0) | 4)
-    try:
-        _check(lib.raft_stream_probe(int(device), int(replicas), int(elems), int(reps), C.byref(us), C.byref(by)))
-    finally:
-        if old is None:
-            os.environ.pop("RAFTSTEP_PROBE_MODE", None)
-        else:
-            os.environ["RAFTSTEP_PROBE_MODE"] = old
+    f = int(flags) | (0 if heartbeat else abi.PROBE_NO_HEARTBEAT)
+    _check(lib.raft_stream_probe(int(device), int(replicas), int(elems), int(reps), f, C.byref(us), C.byref(by)))
     return us.value, by.value
 
 
@@ -175,6 +168,16 @@ class Engine:
             return np.array(s.v, dtype=np.int64)
         _check(self.lib.raft_tick(self.h, first_tick, nticks, None))
         return None
+
+    def stage_values(self, first_tick, values):
+        """RAFT_CLIENT_STAGED: copy the client values of ticks first_tick ..
+        first_tick + len(values) - 1 into HBM; values[t][e][g] int64
+        (raft_stage_values: [nticks][E][G])."""
+        v = np.ascontiguousarray(values, dtype=np.int64)
+        if v.ndim != 3 or v.shape[1:] != (self.cfg.entries_per_tick, self.cfg.groups):
+            raise ValueError(f"staged values: shape {v.shape}, expected (nticks, {self.cfg.entries_per_tick}, "
+                             f"{self.cfg.groups})")
+        _check(self.lib.raft_stage_values(self.h, int(first_tick), v.shape[0], _ptr(v)))
 
     def tick_records(self, nticks):
         """Per-tick stats [nticks][8] of the last tick(stats=True) call (device-reduced,

@@ -229,5 +229,10 @@ def test_stream_probe_reports_its_bytes():
     assert by7 == 1024 * 124 and us7 > 0
     us1, by1 = stream_probe(0, 1, 1 << 20, 3, heartbeat=False)   # (the shared-form mix: 36 + 12 B)
     assert by1 == (1 << 20) * 48 and 0 < us1 < 1e5
+    # the mode is an explicit argument, not the process environment
+    us2, by2 = stream_probe(0, 1, 1 << 20, 3, flags=abi.PROBE_NO_HEARTBEAT | abi.PROBE_NT_RECORD)
+    assert by2 == by1 and 0 < us2 < 1e5
     with pytest.raises(RaftError):
         stream_probe(0, 9, 1 << 20, 1)
+    with pytest.raises(RaftError):
+        stream_probe(0, 5, 1 << 20, 1, flags=8)
