@@ -383,8 +383,8 @@ enum raft_diag_counter {
   RAFT_DIAG_LIST_LXS_VX = 29,         /* LXS entered with a virtual suffix */
   RAFT_DIAG_LEAN_SH = 30,             /* steady ticks whose entries went to the shared ring (SH) */
   RAFT_DIAG_LIST_SH_COPIED = 31,      /* groups in shared form whose entries the list kernel copied back */
-  RAFT_DIAG_LIST_SH_ENTRIES = 1,      /* ... the shared entries it copied (0 for groups closed ahead of a window) */
-  RAFT_DIAG_LEAN_SH_CLOSED = 2,       /* groups whose shared form closed ahead of an isolation window start */
+  RAFT_DIAG_LIST_SH_ENTRIES = 1,      /* ... the shared entries it copied */
+  RAFT_DIAG_LIST_LAG_CATCHUP = 6,     /* REF + CRC: a follower that rejected a corrupted copy caught up (list kernel) */
   RAFT_DIAG_LEAN_SWITCH = 5,          /* ring segment switches */
   /* full fast-path body (list kernel / one-pass kernel): 32 + bit */
   RAFT_DIAG_LIST_LANES = 42,          /* groups looked at */

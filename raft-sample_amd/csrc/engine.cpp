@@ -648,7 +648,6 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
     e->P.grotb = Strided<uint16_t, 16>{&e->P.gseg->rotb};
     e->P.gsb2 = Strided<int32_t, 16>{&e->P.gseg->sb2};
     e->P.gshf = Strided<int32_t, 16>{&e->P.gseg->shf};
-    e->P.gshn = Strided<uint16_t, 16>{&e->P.gseg->shn};
   }
   // sharded group lists (raft_device.hpp): NSHARD shards of scap entries
   const uint64_t scap = ((Gp / 256 + NSHARD - 1) / NSHARD) * 256;
@@ -668,18 +667,13 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   // shared entries (raft_device.hpp ROT_SH): without EXT isolation churn (under
   // it groups leave the steady form too often for the copy-back to pay), with
   // slots below the rotation's flag bit; RAFTSTEP_SH=0 turns them off
-  // (round 6: under isolation churn too, closed ahead of every window start,
-  // DevPlanes::sh_look; RAFTSTEP_SH=3 keeps them open under churn — the round-5
-  // form, whose copy-backs at window starts made C4 4x slower: A/B only)
-  e->P.sh = K <= ROT_SHX / 2 ? 1u : 0u;
+  // (round 6: measured again under churn with every group closing its shared
+  // form ahead of its next isolation window, so that no copy-back was needed:
+  // C4 2.51 -> 2.18-2.23e10 — a wave's lanes then mix shared and R-copy
+  // ring rows, and both kinds of row store go out with holes)
+  e->P.sh = (c.isolate_per_65536 == 0 && K < ROT_SH) ? 1u : 0u;
   if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 0) e->P.sh = 0;
-  e->P.sh_look = 0;
-  if (e->P.sh && c.isolate_per_65536 && c.client_period && c.entries_per_tick) {
-    // client ticks enough for K entries (E per client tick), in ticks, + one period of margin
-    const uint64_t ct = (c.ring_depth + c.entries_per_tick - 1) / c.entries_per_tick;
-    e->P.sh_look = uint32_t(std::min<uint64_t>((ct + 1) * c.client_period, 1u << 20));
-    if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 3) e->P.sh_look = 0;
-  }
+  if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 2 && K < ROT_SH) e->P.sh = 1;   // (also under churn)
   if (e->P.sh) {
     A(reinterpret_cast<void**>(&e->P.sh_term), K * Gp * 4);
     A(reinterpret_cast<void**>(&e->P.sh_value), K * Gp * 8);

@@ -322,6 +322,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   int jb_n = 0, jb_from = 0, jb_term = 0, jb_sb = 0, jb_sb2 = 0;
   uint32_t jb_col = 0, jb_rot = 0, jb_rotb = 0;   // destination column; ring words (rot | rota << 16, rotb)
   uint64_t jb_q0 = 0, jb_kv = 0;
+  int jb_scol = -1;     // >= 0: the entries are read from this column instead (staged values), jb_sd slots back
+  int jb_sd = 0;
   uint32_t df = 0;      // diagnostics: lane class bits (P.dbg)
   uint32_t vxf = 0;     // diagnostics: 1 = a return with a virtual suffix (no copy), 2 = LXS entered with one
   bool stored = false;  // the group's rows may have been written (returned)
@@ -641,12 +643,27 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     }
     const bool gom = go && !lx;   // the main steady-state path
     if (gom && !bail) bail = int64_t(Ll) + n > I32MAX || n >= int(P.K);
+    // REF with payload CRC (round 6): one follower whose last AppendEntries
+    // was rejected (a corrupted copy, EXT) lags — its log ends at its
+    // MatchIndex m < Ll (REF keeps MatchIndex on a failure, main.go:375-378).
+    // Its AppendEntries this tick is case (ii) of main.go:353-360: entries
+    // m+1 .. Ll+n with prevLogIndex m and prevLogTerm GetLog(m).Term (one ring
+    // read); accepted, the leader's entries m+1..Ll are copied into its
+    // column by the wave (GetLogsFrom, main.go:357) and the group is in step
+    // again. Taken while m > 0, the batch fits the ring (Ll+n-m < K) and this
+    // tick has entries; anything else takes the general path as before.
+    int lg = -1;
     if (gom) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == sr) continue;   // the returning stale leader: checked with its AppendEntries below
         if (p == xi) {   // MSYNC stays exact for an isolated follower / candidate (not a fresh row: unchanged, explicit)
           if (!stale) bail |= m[p] != last[p] || m[p] > Ll || ((fresh >> p) & 1u);
+          continue;
+        }
+        if (!RAFT && CRC && p != c && lg < 0 && n > 0 && m[p] > 0 && m[p] < Ll && m[p] == last[p] &&
+            Ll + n - m[p] < int(P.K)) {
+          lg = p;
           continue;
         }
         bail |= (p != c) && m[p] != Ll && !((fresh >> p) & 1u);
@@ -697,12 +714,19 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
                                          cv_stride(P), n, cm);
       }
     }
+    int lg_pt = 0;   // the lagging follower's prevLogTerm: the leader's entry at its MatchIndex
+    if (!RAFT && CRC && gom && !bail && lg >= 0) {
+      const uint32_t so = ring_slot(sel(m, lg), GW.rot(), GW.rota(), GW.rotb(), GW.sb(), GW.sb2(), P.kmask);
+      lg_pt = ring_ld(P.log_term + ring_tile(g, P.KP, R), ring_in_tile(g, R, so, uint32_t(c)));
+    }
     uint32_t okm = 0, cch = 0, mch = 0, ltch = 0;
     if (gom && !bail) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
         if (p == c || p == xi || p == sr) continue;   // xi: dropped (sender sees false, receiver unchanged)
         const int l = last[p];
+        const bool lgp = !RAFT && CRC && p == lg;
+        const int np = lgp ? Ll + n - l : n;          // len(Logs) of p's AppendEntries
         bool ok;
         if constexpr (RAFT) {
           // same term (checked), log exactly as long as the leader's before this tick
@@ -710,17 +734,18 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           if ((crcbad >> p) & 1u) bail = true;                    // rejected payload: backoff path
           ok = true;
         } else {
+          const int pi = lgp ? l : prev_idx, pt = lgp ? lg_pt : prev_term;
           ok = Lt >= term[p];                                     // main.go:129-133
           if (ok && l > 0) {                                      // main.go:135
-            if (int64_t(l) + n < prev_idx) ok = false;            // 137-140
-            else if (prev_idx < 1 || prev_idx > l || prev_idx <= l - int(P.K) || prev_idx != l) bail = true;
-            else ok = lt[p] == prev_term;                         // 142-145 (GetLog(l) == last entry)
+            if (int64_t(l) + np < pi) ok = false;                 // 137-140
+            else if (pi < 1 || pi > l || pi <= l - int(P.K) || pi != l) bail = true;
+            else ok = lt[p] == pt;                                // 142-145 (GetLog(l) == last entry)
           }
-          if (ok && int64_t(l) + n > I32MAX) bail = true;
+          if (ok && int64_t(l) + np > I32MAX) bail = true;
           if (ok && ((crcbad >> p) & 1u)) ok = false;             // EXT: payload rejected
         }
         if (ok) {
-          const int nl = l + n;                                   // 148-149
+          const int nl = l + np;                                  // 148-149
           last[p] = nl;
           if (n && lt[p] != Lt) ltch |= 1u << p;
           if (Lc > commit[p]) {                                   // 151-152
@@ -731,6 +756,19 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           }
           if (nl != m[p]) { m[p] = nl; mch |= 1u << p; }          // 156 -> 375-377
           okm |= 1u << p;
+          if (lgp) {   // its catch-up: the leader's entries l+1..Ll, copied from the leader's column below
+            jb_n = Ll - l;
+            jb_from = l + 1;
+            jb_col = uint32_t(p);
+            jb_term = Lt;
+            jb_scol = c;
+            jb_sd = 0;
+            jb_rot = GW.rot() | (uint32_t(GW.rota()) << 16);
+            jb_rotb = GW.rotb();
+            jb_sb = GW.sb();
+            jb_sb2 = GW.sb2();
+            if (P.dbg) atomicAdd(&P.dbg[6], 1ull);   // diagnostics: a lagging follower caught up
+          }
         }
       }
     }
@@ -780,8 +818,10 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       // (VX: sr's entries above L0 = xlo are virtual, of its own term)
       bail |= (L0 + 1 <= Ll ? tc1 : Lt) == ((L0 + 1 <= ls && !(meta & M_VX)) ? ts1 : sel(term, sr));
       // (the catch-up regenerates the primary's entries L0+1..Ll: they must
-      // all be from the current run of consecutive calls, T.contig_q)
-      if (!(meta & M_VX)) bail |= T.entries_before(T.tick) - uint64_t(Ll - L0) < T.contig_q;
+      // all be from the current run of consecutive calls, T.contig_q; with
+      // staged client values nothing is regenerable and the catch-up reads
+      // them from the primary's column instead — GetLogsFrom, main.go:357)
+      if (!(meta & M_VX) && !P.cv) bail |= T.entries_before(T.tick) - uint64_t(Ll - L0) < T.contig_q;
       if (!bail) {
         df |= (1u << 21) | (ls > L0 ? 1u << 22 : 0u);   // class: stale leader's return (its log truncated at L0)
         // the primary's entries after L0 (at most K): copied below by the whole wave
@@ -796,6 +836,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         jb_term = Lt;
         jb_q0 = T.entries_before(T.tick) - uint64_t(jb_n);
         jb_kv = sm64(key ^ ((uint64_t(ST_VALUE) << 32) | uint32_t(c)));
+        jb_scol = P.cv ? c : -1;   // (staged values: read from the primary's column, same slots)
         jb_rot = rot | (rota << 16);
         jb_rotb = rotb;
         jb_sb = sbo;
@@ -1055,11 +1096,13 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
             const uint32_t rota = GW.rota();
             // (a stale leader's entries above Ll are moved by regenerating them:
             // only when they are all from the current run of calls, T.contig_q;
-            // else no switch — placement only, the entries stay where they are)
+            // with staged values by reading them from their old slots, all in
+            // the current segment (sb <= Ll+1); else no switch — placement
+            // only, the entries stay where they are)
+            const bool mv_ok = P.cv ? sbo <= Ll + 1
+                                    : T.entries_before(T.tick + 1) - uint64_t(xtop - Ll) >= T.contig_q;
             const bool ok = ring_switch_ok(d, uint32_t(rot), rota, sbo, GW.sb2(), lo, P.K, P.kmask) &&
-                            xtop - Ll <= int(P.K) &&
-                            !(stale && xtop > Ll && !(meta & M_VX) &&
-                              T.entries_before(T.tick + 1) - uint64_t(xtop - Ll) < T.contig_q);
+                            xtop - Ll <= int(P.K) && !(stale && xtop > Ll && !(meta & M_VX) && !mv_ok);
             df |= hi > Ll ? 64u : 0u;
             df |= ok ? 0u : 128u;
             if (hi <= Ll && ok) {
@@ -1074,6 +1117,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
                 jb_term = x_term;
                 jb_q0 = T.entries_before(T.tick + 1) - uint64_t(jb_n);
                 jb_kv = sm64(key ^ ((uint64_t(ST_VALUE) << 32) | uint32_t(xi)));
+                jb_scol = P.cv ? xi : -1;   // (staged values: read from its old slot, d back)
+                jb_sd = int(d);
                 jb_rot = uint32_t((rot + int(d)) & int(P.kmask));
                 jb_rotb = 0;
                 jb_sb = -2147483647 - 1;
@@ -1144,8 +1189,9 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   // (a switch needs sr < 0).
   constexpr int CPS = 4;   // entries per lane and pass
   WPROF(wp1 = __builtin_amdgcn_s_memtime(); uint64_t wg = 0, wo = 0, wsc = 0;)
+  constexpr bool JOBS = RAFT || CRC;   // (entry jobs: RAFT returns / moves, REF + CRC lagging followers)
   int jn = 0, jpre = 0, jtot = 0;   // this lane's job size, exclusive wave prefix, wave total
-  if constexpr (RAFT) {
+  if constexpr (JOBS) {
     jn = jb_n;
     jpre = jn;
 #pragma unroll
@@ -1156,14 +1202,22 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     jtot = __shfl(jpre, 63);
     jpre -= jn;
   }
-  const int passes = RAFT ? (jtot + 64 * CPS - 1) / (64 * CPS) : 0;   // (wave-uniform)
+  const int passes = JOBS ? (jtot + 64 * CPS - 1) / (64 * CPS) : 0;   // (wave-uniform)
+  // jobs that read entries (staged values; a lagging follower's catch-up)
+  // may read what this wave wrote in its previous step (pipelined list
+  // kernel) from other lanes: those stores complete before the job's loads
+  // (which bypass L1)
+  if (JOBS && passes > 0 && __ballot(jb_scol >= 0)) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
   for (int pass_i = 0; pass_i < (passes > 0 ? passes : 1); ++pass_i) {
     int32_t ct[CPS];
     int64_t cv[CPS];
     uint32_t cdst[CPS];      // destination element offset inside the ring (64-bit tile base below)
     uint64_t ctb[CPS];
     bool con[CPS];
-    if constexpr (RAFT) {
+    if constexpr (JOBS) {
       const int lane = threadIdx.x & 63;
 #pragma unroll
       for (int k = 0; k < CPS; ++k) {
@@ -1175,7 +1229,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
 #pragma unroll
         for (int step = 32; step > 0; step >>= 1)
           if (__shfl(jpre, o + step) <= e) o += step;
-        const int j = e - __shfl(jpre, o);
+        const int j0 = e - __shfl(jpre, o);
         // (every shuffle unconditional: a shuffle reading a lane that is off
         // in a divergent branch returns 0)
         const int from = __shfl(jb_from, o), term = __shfl(jb_term, o);
@@ -1187,19 +1241,32 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
                             uint32_t(__shfl(int(uint32_t(jb_q0)), o));
         const uint64_t kv = (uint64_t(uint32_t(__shfl(int(uint32_t(jb_kv >> 32)), o))) << 32) |
                             uint32_t(__shfl(int(uint32_t(jb_kv)), o));
+        const int scol = __shfl(jb_scol, o), sd = __shfl(jb_sd, o), jnn = __shfl(jn, o);
+        // a move read from its old slots goes from the top down: entry i's new
+        // slot is entry i+d's old one, so every entry is read (this pass, or
+        // an earlier one) before a lower one overwrites its old slot
+        const int j = (scol >= 0 && sd != 0) ? jnn - 1 - j0 : j0;
         if (con[k]) {
-          // global client entry q: tick (q / E) * period, entry q mod E of that tick
-          const uint64_t q = q0 + uint64_t(j);
-          const uint64_t qt = T.entries == 1u ? q : q / T.entries;
-          const uint32_t qe = T.entries == 1u ? 0u : uint32_t(q - qt * T.entries);
           ct[k] = term;
-          cv[k] = int64_t(sm64(sm64(kv ^ (qt * T.period)) ^ uint64_t(qe)) >> 1);
           ctb[k] = ring_tile(gg, P.KP, R);
-          cdst[k] = ring_in_tile(gg, R, ring_slot(from + j, rr & 0xFFFFu, rr >> 16, rb, sb_, sb2_, P.kmask), col);
+          const uint32_t ds = ring_slot(from + j, rr & 0xFFFFu, rr >> 16, rb, sb_, sb2_, P.kmask);
+          cdst[k] = ring_in_tile(gg, R, ds, col);
+          if (scol >= 0) {   // the entry read from column scol, sd slots back (a return or a lagging
+                             // follower: the leader's column, same slot; a move: its own column, its old slot)
+            const uint32_t so = ring_in_tile(gg, R, (ds - uint32_t(sd)) & P.kmask, uint32_t(scol));
+            ct[k] = ring_ld(P.log_term + ctb[k], so);
+            cv[k] = ring_ld(P.log_value + ctb[k], so);
+          } else {
+            // global client entry q: tick (q / E) * period, entry q mod E of that tick
+            const uint64_t q = q0 + uint64_t(j);
+            const uint64_t qt = T.entries == 1u ? q : q / T.entries;
+            const uint32_t qe = T.entries == 1u ? 0u : uint32_t(q - qt * T.entries);
+            cv[k] = int64_t(sm64(sm64(kv ^ (qt * T.period)) ^ uint64_t(qe)) >> 1);
+          }
         }
       }
     }
-    WPROF(uint64_t wq0 = __builtin_amdgcn_s_memtime(); if constexpr (RAFT) { int z = 0; for (int k = 0; k < CPS; ++k) z += ct[k]; if (__ballot(z == 0x7FFFFFFF)) wg += 1; } uint64_t wq1 = __builtin_amdgcn_s_memtime(); wg += wq1 - wq0;)
+    WPROF(uint64_t wq0 = __builtin_amdgcn_s_memtime(); if constexpr (JOBS) { int z = 0; for (int k = 0; k < CPS; ++k) z += ct[k]; if (__ballot(z == 0x7FFFFFFF)) wg += 1; } uint64_t wq1 = __builtin_amdgcn_s_memtime(); wg += wq1 - wq0;)
     if (LIST && pass_i == 0 && n && wr != 0) {   // this tick's entries: scattered groups, each lane its own R-contiguous segment
       const uint64_t tb = ring_tile(g, P.KP, R);
       int32_t* const rt = P.log_term + tb;
@@ -1229,7 +1296,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       }
     }
     WPROF(uint64_t wq2 = __builtin_amdgcn_s_memtime(); wo += wq2 - wq1;)
-    if constexpr (RAFT) {
+    if constexpr (JOBS) {
 #pragma unroll
       for (int k = 0; k < CPS; ++k) {
         if (!con[k]) continue;
@@ -1473,6 +1540,7 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     // no real record equals, so that any record the tick writes (LXS / SXS
     // entry, whatever its value) is written back
     LxRec lx0{-2147483647 - 1, -2147483647 - 1};
+    int shf0 = 0;   // SH: the group's first shared index (ROT_SH)
     if (valid) {
       // gmeta, grot, gsb and gss from the list entry (the lean kernel's reads,
       // LIST_WORDS: coalesced by slot), the other words from their planes
@@ -1486,22 +1554,42 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       ra0 = cw.rota; rb0 = cw.rotb; sc0 = cw.sb2;
       if (T.iso_p) gi0 = cw.iso;
       if (uses_glx(m0)) lx0 = P.glx[g];
-      // a group the lean kernel left in shared form (ROT_SH): its shared
-      // entries back into the R columns first (the bit is cleared in the
-      // staged rotation and written back with it)
-      // (closed, ROT_SHX, ahead of a window start: nothing left to copy)
-      if (r0 & ROT_SH) {
-        const int nc = sh_copy_back<R>(P, g, ss0.last, cw.shf, sh_end(r0, cw.shf, cw.shn), r0, ra0, rb0, sb0, sc0);
-        if (P.dbg) {
-          atomicAdd(&P.dbg[31], 1ull);
-          if (nc) atomicAdd(&P.dbg[1], (unsigned long long)nc);
-        }
+      shf0 = cw.shf;
+    }
+    // a group the lean kernel left in shared form (ROT_SH): its shared entries
+    // back into the R columns first (the bit is cleared in the staged rotation
+    // and written back with it). Wave-cooperative (round 6): the wave's lanes
+    // take such groups one at a time and copy each one's live entries
+    // together, one entry per lane and pass — up to K entries x R columns per
+    // group, which one lane copying its own group took K dependent passes for
+    // (C5 with corrupted copies, K = 512: every rejection copies a group back).
+    // The block barrier below orders these stores before the tick's own.
+    for (uint64_t shm = __ballot(valid && (r0 & ROT_SH)); shm; shm &= shm - 1) {
+      const int src = int(__builtin_ctzll(shm));
+      const uint32_t gs = uint32_t(__shfl(int(g), src));
+      const int L = __shfl(ss0.last, src), lo = max(__shfl(shf0, src), L - int(P.K) + 1);
+      const uint32_t rs = uint32_t(__shfl(int(r0), src)), ras = uint32_t(__shfl(int(ra0), src)),
+                     rbs = uint32_t(__shfl(int(rb0), src));
+      const int sbs = __shfl(sb0, src), scs = __shfl(sc0, src);
+      const uint64_t tb = ring_tile(gs, P.KP, R), shb = sh_tile(gs, P.KP);
+      for (int idx = lo + int(lane); idx <= L; idx += 64) {
+        const uint32_t slot = ring_slot(idx, rs, ras, rbs, sbs, scs, P.kmask);
+        const uint32_t so = sh_in_tile(gs, slot), o = ring_in_tile(gs, R, slot, 0u);
+        const int32_t tt = at(P.sh_term + shb, so);
+        const int64_t vv = at(P.sh_value + shb, so);
+        fill_seg<R>(P.log_term + tb + o, tt);
+        fill_seg<R>(P.log_value + tb + o, vv);
+        if constexpr (CRC) fill_seg<R>(P.log_crc + tb + o, at(P.sh_crc + shb, so));
+      }
+      if (P.dbg && lane == 0) {
+        atomicAdd(&P.dbg[31], 1ull);
+        if (L >= lo) atomicAdd(&P.dbg[1], (unsigned long long)(L - lo + 1));
       }
     }
     // (a group in shared form was taken by the lean kernel at the tick before
     // this one: its heartbeat time is implied, and written back from here)
     const int32_t hbs = (r0 & ROT_SH) ? T.at_tick(T.tick - 1).now : hb0;
-    smeta[t] = m0; sgrot[t] = uint16_t(r0 & ~ROT_SHM); sgiso[t] = gi0; shb[t] = hbs; sgss[t] = ss0; sglx[t] = lx0;
+    smeta[t] = m0; sgrot[t] = uint16_t(r0 & ~ROT_SH); sgiso[t] = gi0; shb[t] = hbs; sgss[t] = ss0; sglx[t] = lx0;
     sgrota[t] = ra0; sgrotb[t] = rb0; sgsb[t] = sb0; sgsb2[t] = sc0;
     __syncthreads();
     {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
@@ -1642,7 +1730,6 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   if (T.iso_p) im = iso_windows<R>(key, T, &act, &starting);
   bool held = false;
   bool shw = false;             // SH: this tick's entries go to the shared ring (ROT_SH)
-  bool shc = false;             // SH: the group's shared form closes this tick (ROT_SHX)
   uint32_t p_mr = 0;            // a passed group's words as read here, for its list entry
   int32_t p_sb = 0;
   SsRec p_ss{0, 0, 0, 0};
@@ -1835,17 +1922,6 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
           }
         }
         shw = P.sh && take && n > 0 && w_slot < 0 && !sw_d && !(RAFT && (meta & M_HWX));   // (in phase only)
-        // SH under isolation churn (round 6, DevPlanes::sh_look): no shared
-        // entry is written within sh_look ticks of a window start, so at that
-        // start, when the group leaves the lean kernel, its shared entries are
-        // out of every log's window and nothing is copied back. A group in
-        // shared form closes it here (ROT_SHX: [shf, L] stay shared, this
-        // tick's entries and later ones go to the R replica rings)
-        const bool shx = (uint32_t(rot) & ROT_SHX) != 0u;
-        if (shw && (shx || (P.sh_look && window_starts_within(key, T, P.sh_look)))) {
-          shw = false;
-          shc = shm && !shx;
-        }
         nl = L + n;
         if (RAFT ? nl > s.cl : (2 * (R - 1) > R && nl > s.cl)) cl2 = nl;
         cf2 = s.cl > s.cf ? s.cl : s.cf;
@@ -1872,13 +1948,6 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
           at(P.grot, g) = uint16_t(uint32_t(rot) | ROT_SH);
           at(P.gshf, g) = L + 1;
         }
-        if (shc) {   // closed: the live shared entries are [max(shf, L+1-K), L] (a rare dependent read of shf)
-          const int shf1 = max(int(at(P.gshf, g)), L + 1 - int(P.K));
-          at(P.gshf, g) = shf1;
-          at(P.gshn, g) = uint16_t(L + 1 - shf1);
-          at(P.grot, g) = uint16_t(uint32_t(rot) | ROT_SHX);
-          df |= 4u;   // diagnostics: SH closed ahead of a window start
-        }
         if (hwx_clear) at(P.gmeta, g) = uint16_t(meta & ~M_HWX);
         if (sw_d) {   // the new segment starts at this tick's first entry
           if (sw_rota >= 0) at(P.grotb, g) = uint16_t(sw_rota);   // (else the older segments are dead)
@@ -1896,7 +1965,6 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
         w_slot = -1;
         x_slot = -1;
         shw = false;
-        shc = false;
       }
     }
   }

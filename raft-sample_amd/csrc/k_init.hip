@@ -128,7 +128,6 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
       // SH (ROT_SH): entries from shf on are read from the shared ring (the
       // digest of the materialised state, without materialising it)
       const int shf = (P.sh && (rot & ROT_SH)) ? at(P.gshf, g) : 2147483647;
-      const int she = (P.sh && (rot & ROT_SH)) ? sh_end(rot, shf, at(P.gshn, g)) : 2147483647;   // (closed: ROT_SHX)
       const uint64_t shb = sh_tile(g, P.KP);
 #pragma unroll 1
       for (int idx = hwm > int(P.K) ? hwm - int(P.K) + 1 : 1; idx <= l; ++idx) {
@@ -136,7 +135,7 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
         int32_t lt;
         int64_t lv;
         uint32_t lc = 0;
-        if (idx >= shf && idx < she) {
+        if (idx >= shf) {
           const uint32_t so = sh_in_tile(g, slot);
           lt = at(P.sh_term + shb, so);
           lv = at(P.sh_value + shb, so);

@@ -129,8 +129,7 @@ struct __attribute__((aligned(16))) GSeg {
   uint16_t rota, rotb;   // rotation of the previous / older segment
   int32_t sb2;           // first index of the previous segment (0: none older)
   uint8_t iso;           // EXT leader-isolation victims (nibble per epoch parity: 8 | replica)
-  uint8_t pad;
-  uint16_t shn;          // SH closed (ROT_SHX): the shared entries are [shf, shf + shn) (<= K of them)
+  uint8_t pad[3];
   int32_t shf;           // SH (ROT_SH): the first index whose entries live in the shared ring
 };
 // A plane of T with a byte stride S (a field of an array of records): the
@@ -177,7 +176,6 @@ struct DevPlanes {
   int64_t* sh_value;
   uint32_t* sh_crc;
   Strided<int32_t, 16> gshf;    // GSeg::shf
-  Strided<uint16_t, 16> gshn;   // GSeg::shn
   const uint32_t* crc_tab;  // 8 x 256 slice-by-8 CRC32C tables
   uint32_t crc_on;     // payload_crc
   uint32_t corrupt_p;  // EXT corruption probability / 65536
@@ -203,15 +201,9 @@ struct DevPlanes {
   // (RAFTSTEP_VX=0 turns it off); the fast paths then give a group entering
   // LXS a virtual suffix
   uint32_t vx;
-  // SH (ROT_SH) enabled: steady groups' entries go to the shared ring
-  // (KP < 2^14; RAFTSTEP_SH=0 turns it off)
+  // SH (ROT_SH) enabled: steady groups' entries go to the shared ring (no
+  // EXT isolation configured, KP < 2^15; RAFTSTEP_SH=0 turns it off)
   uint32_t sh;
-  // SH under EXT isolation churn (round 6): a group stops writing the shared
-  // ring (ROT_SHX) once an isolation window starts within the next sh_look
-  // ticks, enough client ticks for K entries: its shared entries are then out
-  // of every log's window (dead) when the window starts and takes the group
-  // off the lean kernel, so nothing is copied back (0: no isolation)
-  uint32_t sh_look;
   // SH: a group in shared form is taken by the lean (or fused) kernel every
   // tick, so its heartbeat time (hb, every follower's timer reset) is implied:
   // now of the last tick run. Its hb store is skipped; whoever copies the
@@ -349,15 +341,6 @@ __device__ __forceinline__ uint32_t ring_in_tile(uint32_t g, uint32_t R, uint32_
 // they load a group; the engine's flush before host reads, digests and
 // handler batches). Nothing is regenerated: a flush at any time is exact.
 constexpr uint32_t ROT_SH = 0x8000u;
-// SH closed (round 6, with ROT_SH; see DevPlanes::sh_look): the group's
-// entries [shf, shf + shn) stay in the shared ring, later ones are written to
-// the R replica rings again (bit 14 of grot: KP <= 2^13, so no slot moves)
-constexpr uint32_t ROT_SHX = 0x4000u;
-constexpr uint32_t ROT_SHM = ROT_SH | ROT_SHX;
-// one past the last shared index of a group in shared form (open: none)
-__device__ __forceinline__ int sh_end(uint32_t rot, int shf, uint32_t shn) {
-  return (rot & ROT_SHX) ? shf + int(shn) : 2147483647;
-}
 __device__ __forceinline__ uint64_t sh_tile(uint32_t g, uint32_t KP) { return uint64_t(g >> 6) * (KP * 64u); }
 __device__ __forceinline__ uint32_t sh_in_tile(uint32_t g, uint32_t slot) { return slot * 64u + (g & 63u); }
 
@@ -639,15 +622,15 @@ __device__ __forceinline__ void vx_materialize(const DevPlanes& P, uint32_t g, u
   at(P.gmeta, g) = uint16_t(meta & ~M_VX);
 }
 
-// SH (see ROT_SH): the live shared entries [max(shf, L-K+1), min(she-1, L)]
-// of group g (every log of length L: SSYNC, normal class; she = sh_end) into
-// all R replica columns. The caller clears ROT_SHM in grot (or in its staged
-// copy). Returns the number of entries copied.
+// SH (see ROT_SH): the live shared entries [max(shf, L-K+1), L] of group g
+// (every log of length L: SSYNC, normal class) into all R replica columns.
+// The caller clears ROT_SH in grot (or in its staged copy). Returns the
+// number of entries copied.
 template <int R>
-__device__ __forceinline__ int sh_copy_back(const DevPlanes& P, uint32_t g, int L, int shf, int she, uint32_t rot,
+__device__ __forceinline__ int sh_copy_back(const DevPlanes& P, uint32_t g, int L, int shf, uint32_t rot,
                                             uint32_t rota, uint32_t rotb, int sb, int sb2) {
   const uint64_t tb = ring_tile(g, P.KP, R), sb_t = sh_tile(g, P.KP);
-  const int lo = max(shf, L - int(P.K) + 1), hi = min(she - 1, L);
+  const int lo = max(shf, L - int(P.K) + 1), hi = L;
   for (int idx = lo; idx <= hi; ++idx) {
     const uint32_t slot = ring_slot(idx, rot, rota, rotb, sb, sb2, P.kmask);
     const uint32_t so = sh_in_tile(g, slot), o = ring_in_tile(g, R, slot, 0u);
@@ -671,10 +654,9 @@ __device__ __forceinline__ void sh_materialize(const DevPlanes& P, uint32_t g, i
   const uint32_t rot = at(P.grot, g);
   if (!(rot & ROT_SH)) return;
   const GSeg cw = P.gseg[g];
-  sh_copy_back<R>(P, g, P.gss[g].last, cw.shf, sh_end(rot, cw.shf, cw.shn), rot, cw.rota, cw.rotb, at(P.gsb, g),
-                  cw.sb2);
+  sh_copy_back<R>(P, g, P.gss[g].last, cw.shf, rot, cw.rota, cw.rotb, at(P.gsb, g), cw.sb2);
   at(P.hb, g) = hb;   // (implied while shared: now of the last tick it was taken)
-  at(P.grot, g) = uint16_t(rot & ~ROT_SHM);
+  at(P.grot, g) = uint16_t(rot & ~ROT_SH);
 }
 
 // Group context: the R replicas of one group, in registers. SEM selects the

@@ -38,19 +38,6 @@ __device__ __forceinline__ uint32_t iso_windows(uint64_t key, const Trace& T, ui
   }
   return mask;
 }
-// Does an isolation window (either mode) start in (T.tick, T.tick + H]?
-// (SH under churn, DevPlanes::sh_look: the epochs of that range, one hash each)
-__device__ __forceinline__ bool window_starts_within(uint64_t key, const Trace& T, uint32_t H) {
-  const uint64_t inner = sm64(key ^ (uint64_t(ST_ISOLATE) << 32));
-  const int64_t t1 = T.tick + int64_t(H);
-  bool any = false;
-  for (int64_t e = (T.tick + 1) >> 5; e <= (t1 >> 5); ++e) {
-    const uint64_t h = sm64(inner ^ uint64_t(e));
-    const int64_t start = e * 32 + int64_t((h >> 24) & 31);
-    any |= (h & 0xFFFF) < T.iso_p && start > T.tick && start <= t1;
-  }
-  return any;
-}
 // Hashed-victim mode: the replicas cut off this tick.
 template <int R>
 __device__ __forceinline__ uint32_t isolation_mask(uint64_t key, const Trace& T) {

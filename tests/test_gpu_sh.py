@@ -149,42 +149,34 @@ def test_corrupted_copies_leave_the_shared_form(monkeypatch):
         t += k
     cls = e.diag_read()
     assert cls["list_sh_copied"] > 0 and cls["lean_sh"] > 0, cls
+    # (round 6) the rejecting follower catches up on the fast path the next
+    # tick: the leader's entries copied from its column by the list kernel
+    assert cls["list_lag_catchup"] > 0, cls
     _digests(e, o, f"after tick {t - 1}")
     H.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")
 
 
-@pytest.mark.parametrize("sh,K", [("1", 16), ("1", 128), ("3", 128)],
-                         ids=["closed_ahead_K16", "closed_ahead_K128", "open_round5_form"])
-def test_under_isolation_churn(monkeypatch, sh, K):
-    """Shared entries under C4's leader-isolation churn (round 6, the default):
-    a group stops writing the shared ring once a window starts within
-    DevPlanes::sh_look ticks (ROT_SHX), so when the window takes it off the
-    lean kernel its shared entries are out of every log's window and the list
-    kernel copies nothing back (list_sh_entries == 0). RAFTSTEP_SH=3 keeps the
-    round-5 form (open until the window, every live entry copied back).
-    Statistics of every call, then digests and the whole state, equal the
-    oracle's; virtual suffixes and ring segment switches run alongside."""
+def test_forced_on_under_isolation_churn(monkeypatch):
+    """RAFTSTEP_SH=2 (the A/B knob: shared entries under C4's leader-isolation
+    churn too, with virtual suffixes and ring segment switches): every group
+    leaves and re-enters the shared form through the list kernel's copy-back
+    (the wave-cooperative one, round 6); statistics of every call, then
+    digests and the whole state, equal the oracle's."""
     import bench
-    monkeypatch.setenv("RAFTSTEP_SH", sh)
+    monkeypatch.setenv("RAFTSTEP_SH", "2")
     wl = bench.WORKLOADS["C4"]
-    kw = bench.engine_kwargs(wl, 7, 1 << 13, 0, K, 1, 0)
+    kw = bench.engine_kwargs(wl, 7, 1 << 13, 0, wl["ring_depth"], 1, 0)
+    kw["isolate_per_65536"] = 4 * wl["iso"][0]
     e, o = Engine(**kw), oracle.Oracle(**kw)
     assert e.features()["shared_entries"]
     e.diag_enable()
     e.init_new_nodes(0)
     o.init_new_nodes(0)
     t = 0
-    for k in (48, 20, 20, 20, 13, 30) + ((60, 60, 60) if K > 16 else ()):
+    for k in (48, 20, 20, 20, 13, 30):
         assert list(e.tick(t, k)) == list(o.tick(t, k, threads=16)), f"stats of ticks [{t}, {t + k})"
         t += k
-        if k == 13:
-            _digests(e, o, f"after tick {t - 1} (shared form, closed or open)")
     cls = e.diag_read()
-    print("class counters:", cls)
-    assert cls["lean_sh"] > 0 and cls["list_sh_copied"] > 0, cls
-    if sh == "1":
-        assert cls["lean_sh_closed"] > 0 and cls["list_sh_entries"] == 0, cls
-    else:
-        assert cls["lean_sh_closed"] == 0 and cls["list_sh_entries"] > 0, cls
+    assert cls["list_sh_copied"] > 100 and cls["lean_sh"] > 0 and cls["list_sh_entries"] > 0, cls
     _digests(e, o, f"after tick {t - 1}")
     H.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")

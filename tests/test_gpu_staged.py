@@ -96,7 +96,7 @@ def test_staged_churn_matches_oracle_and_covers_the_classes():
     """C4's configuration (R=7, K=128, leader isolation, RAFT) on 2^16 groups
     with staged values, against ONE oracle over every group: elections, first
     rounds, stale leaders (their own appends stored, not virtual), returns
-    (catch-up copied from the primary's ring by the general kernel), LXS /
+    (catch-up read from the primary's ring column by the list kernel), LXS /
     SXS / HWX, segment switches. Virtual suffixes are off in this mode."""
     wl = bench.WORKLOADS["C4S"]
     G = 1 << 16
@@ -115,7 +115,9 @@ def test_staged_churn_matches_oracle_and_covers_the_classes():
     cls = e.diag_read()
     print("class counters:", cls)
     need = ["lean_ssync", "lean_lxs", "lean_switch", "lean_hwx", "lean_sxs", "list_quiet", "list_isolated_leader",
-            "list_election", "list_first_round", "list_stale", "list_window_start", "list_sxs_entered"]
+            "list_election", "list_first_round", "list_stale", "list_window_start", "list_sxs_entered",
+            "list_return", "list_return_trunc",   # (returns: catch-up read from the primary's column)
+            "list_stale_moved", "lean_sxs_stale_in_row"]   # (moves: read from the stale leader's old slots)
     low = {k: cls[k] for k in need if cls[k] < 1000}
     assert not low, f"classes taken fewer than 1000 times: {low}\nall: {cls}"
     assert cls["list_return_vx"] == 0 and cls["lean_sxs_vx"] == 0 and cls["list_lxs_vx"] == 0
@@ -137,7 +139,9 @@ def test_staged_c5_with_corruption_matches_oracle():
     o = oracle.Oracle(**kw)
     e.init_steady(0, 0)
     o.init_steady(0, 0)
+    e.diag_enable()
     _, total = _run_both(e, o, [3, 10, 10], 1, seed, 64, G, full_at=(2,))
+    assert e.diag_read()["list_lag_catchup"] > 100
     # rejections happened (AppendEntries false); a fault needs 3 rejections of one follower in a row
     assert total[4] > 0 and total[6] <= 2
 

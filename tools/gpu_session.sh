@@ -15,6 +15,7 @@
 #   sqc5      one SQ counter pass of C5 (LDS instructions and waits, busy cycles)
 #   smoke     __graft_entry__.smoke()
 #   bench:ARGS  bench.py with extra arguments (ARGS: comma-separated)
+#   prof:W / pmc:W  kernel trace / PMC passes of bench.py --workload W (e.g. C2S, C4S)
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -62,6 +63,10 @@ for s in "$@"; do
              -d "$OUT/sq_c4r" -o p --output-format csv -- python3 -u bench.py --workload C4R $Q > "$OUT/sq2.log" 2>&1 ;;
     pmcc4) $P --pmc FETCH_SIZE -d "$OUT/pmc_c4_fetch" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc5.log" 2>&1 \
            && $P --pmc WRITE_SIZE -d "$OUT/pmc_c4_write" -o p --output-format csv -- python3 -u bench.py --workload C4 $Q > "$OUT/pmc6.log" 2>&1 ;;
+    prof:*) w="${s#prof:}"; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_${w,,}" -o run --output-format csv \
+              -- python3 -u bench.py --workload $w $Q > "$OUT/prof_${w,,}.log" 2>&1 ;;
+    pmc:*) w="${s#pmc:}"; $P --pmc FETCH_SIZE -d "$OUT/pmc_${w,,}_fetch" -o p --output-format csv -- python3 -u bench.py --workload $w $Q > "$OUT/pmc_${w,,}_f.log" 2>&1 \
+           && $P --pmc WRITE_SIZE -d "$OUT/pmc_${w,,}_write" -o p --output-format csv -- python3 -u bench.py --workload $w $Q > "$OUT/pmc_${w,,}_w.log" 2>&1 ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
   rc=$?

@@ -22,6 +22,21 @@ $S --fetch $O/pmc_c4_fetch --write $O/pmc_c4_write --kernel tick_list_kernel --w
    --skip 53 --take 20 --out profiles/pmc_C4_list.json > /dev/null
 $S --fetch $O/pmc_c5_fetch --write $O/pmc_c5_write --kernel tick_lean_kernel --workload "$W5" \
    --algorithmic-bytes $(($(LB C5)*1048576/2)) --skip 5 --take 40 --launches-per-tick 2 --out profiles/pmc_C5_lean.json > /dev/null
-for f in C2_lean C2X_lean C4_lean C4_list C5_lean; do
+# staged client values (round 6): the same kernels plus 8 E B per group-step
+for w in C2S C4S; do
+  [ -d "$O/pmc_${w,,}_fetch" ] || continue
+  WW=$(python3 -c "import json;print(json.load(open('$B'))['extra_workloads']['$w']['workload'])")
+  if [ $w = C2S ]; then
+    $S --fetch $O/pmc_c2s_fetch --write $O/pmc_c2s_write --kernel tick_lean_kernel --workload "$WW" \
+       --algorithmic-bytes $(($(LB C2S)*1048576/2)) --skip 5 --take 40 --launches-per-tick 2 --out profiles/pmc_C2S_lean.json > /dev/null
+  else
+    $S --fetch $O/pmc_c4s_fetch --write $O/pmc_c4s_write --kernel tick_lean_kernel --workload "$WW" \
+       --algorithmic-bytes $(($(LB C4S)*4194304)) --skip 53 --take 20 --out profiles/pmc_C4S_lean.json > /dev/null
+    $S --fetch $O/pmc_c4s_fetch --write $O/pmc_c4s_write --kernel tick_list_kernel --workload "$WW" \
+       --skip 53 --take 20 --out profiles/pmc_C4S_list.json > /dev/null
+  fi
+done
+for f in C2_lean C2X_lean C4_lean C4_list C5_lean C2S_lean C4S_lean C4S_list; do
+  [ -f profiles/pmc_$f.json ] || continue
   python3 -c "import json; d=json.load(open('profiles/pmc_$f.json')); print('$f', round(d.get('hbm_bytes_per_tick', d['hbm_bytes_per_launch'])/1e6,1), 'MB/tick', d.get('traffic_over_algorithmic'))"
 done
