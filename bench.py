@@ -508,7 +508,10 @@ def measure(ctx, wl_key, wl, G, R, E, K, steps, warmup, repeats, tpl=1, leader=0
     fused = tpl > 1 and not churn and not crc and two_pass
     mean_tpl = steps / -(-steps // tpl) if fused else 1
     iso = "iso" in wl and wl["iso"][0] > 0
-    B = lean_bytes(R, E, crc, segmented=iso, fuse=mean_tpl, glx=iso and wl.get("semantics", 0) == 1,
+    # (2K physical ring slots, whose segment boundary the lean kernel reads: under
+    # isolation churn and, round 6, with corrupted copies — DevPlanes::sh_keep)
+    B = lean_bytes(R, E, crc, segmented=iso or bool(crc and wl.get("corrupt")), fuse=mean_tpl,
+                   glx=iso and wl.get("semantics", 0) == 1,
                    shared=shared, staged=staged) if two_pass else \
         algorithmic_bytes(R, E, crc) + (8 * E if staged else 0)
     kname = ("tick_fused_kernel" if fused else "tick_lean_kernel") if two_pass else "tick_fast_kernel"

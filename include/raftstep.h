@@ -385,6 +385,7 @@ enum raft_diag_counter {
   RAFT_DIAG_LIST_SH_COPIED = 31,      /* groups in shared form whose entries the list kernel copied back */
   RAFT_DIAG_LIST_SH_ENTRIES = 1,      /* ... the shared entries it copied */
   RAFT_DIAG_LIST_LAG_CATCHUP = 6,     /* REF + CRC: a follower that rejected a corrupted copy caught up (list kernel) */
+  RAFT_DIAG_LIST_SH_KEPT = 7,         /* REF + CRC: listed groups that kept their shared form (no copy-back) */
   RAFT_DIAG_LEAN_SWITCH = 5,          /* ring segment switches */
   /* full fast-path body (list kernel / one-pass kernel): 32 + bit */
   RAFT_DIAG_LIST_LANES = 42,          /* groups looked at */

@@ -614,7 +614,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   // physical ring slots: 2K where groups can drift out of the global ring
   // phase (EXT isolation churn), so that their rotation can be switched in
   // place (raft_device.hpp ring_slot)
-  const uint64_t phys = c.isolate_per_65536 > 0 ? 2 : 1;
+  // (and where shared entries stay through rejected copies, DevPlanes::sh_keep)
+  const uint64_t phys = (c.isolate_per_65536 > 0 || (c.payload_crc && c.corrupt_per_65536)) ? 2 : 1;
   const uint64_t K = c.ring_depth * phys;
   e->KP = K;
   const bool raft = c.semantics == RAFT_SEM_RAFT;
@@ -674,6 +675,9 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   e->P.sh = (c.isolate_per_65536 == 0 && K < ROT_SH) ? 1u : 0u;
   if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 0) e->P.sh = 0;
   if (const char* sh = getenv("RAFTSTEP_SH"); sh && atoi(sh) == 2 && K < ROT_SH) e->P.sh = 1;   // (also under churn)
+  // REF with corrupted copies: the shared form survives a rejection (DevPlanes::sh_keep; KP = 2K above)
+  e->P.sh_keep = (e->P.sh && !raft && c.payload_crc && c.corrupt_per_65536 && K >= 2ull * c.ring_depth) ? 1u : 0u;
+  if (const char* sk = getenv("RAFTSTEP_SH_KEEP"); sk && atoi(sk) == 0) e->P.sh_keep = 0;
   if (e->P.sh) {
     A(reinterpret_cast<void**>(&e->P.sh_term), K * Gp * 4);
     A(reinterpret_cast<void**>(&e->P.sh_value), K * Gp * 8);

@@ -301,7 +301,7 @@ __device__ __forceinline__ bool quiet_leaderless(const DevPlanes& P, const Trace
 template <int R, bool CRC, int SEM, bool LIST, class Rows, class Words>
 __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, unsigned long long* stats, uint32_t* work,
                                            int32_t* work_tick, uint32_t* work_count, int force_slow, const uint32_t g,
-                                           const uint32_t* tab, const Rows& RW, const Words& GW) {
+                                           const uint32_t* tab, const Rows& RW, const Words& GW, const int shf = -1) {
   constexpr bool RAFT = SEM == SEM_RAFT;
   WPROF(uint64_t wp0 = __builtin_amdgcn_s_memtime(); uint64_t wp1 = wp0, wp2 = wp0, wp3 = wp0;)
   int sv[7] = {0, 0, 0, 0, 0, 0, 0};   // committed, ae_ok, ae_fail, leader_groups, term bumps, votes, won
@@ -716,8 +716,11 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     }
     int lg_pt = 0;   // the lagging follower's prevLogTerm: the leader's entry at its MatchIndex
     if (!RAFT && CRC && gom && !bail && lg >= 0) {
-      const uint32_t so = ring_slot(sel(m, lg), GW.rot(), GW.rota(), GW.rotb(), GW.sb(), GW.sb2(), P.kmask);
-      lg_pt = ring_ld(P.log_term + ring_tile(g, P.KP, R), ring_in_tile(g, R, so, uint32_t(c)));
+      const int ml = sel(m, lg);
+      const uint32_t so = ring_slot(ml, GW.rot(), GW.rota(), GW.rotb(), GW.sb(), GW.sb2(), P.kmask);
+      // (a group kept in shared form, shf >= 0: entries from shf on are in the shared ring)
+      lg_pt = (shf >= 0 && ml >= shf) ? ring_ld(P.sh_term + sh_tile(g, P.KP), sh_in_tile(g, so))
+                                      : ring_ld(P.log_term + ring_tile(g, P.KP, R), ring_in_tile(g, R, so, uint32_t(c)));
     }
     uint32_t okm = 0, cch = 0, mch = 0, ltch = 0;
     if (gom && !bail) {
@@ -757,7 +760,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           if (nl != m[p]) { m[p] = nl; mch |= 1u << p; }          // 156 -> 375-377
           okm |= 1u << p;
           if (lgp) {   // its catch-up: the leader's entries l+1..Ll, copied from the leader's column below
-            jb_n = Ll - l;
+            // (kept in shared form: only those below shf; the rest are the shared ones it now holds too)
+            jb_n = max(0, (shf >= 0 ? min(Ll, shf - 1) : Ll) - l);
             jb_from = l + 1;
             jb_col = uint32_t(p);
             jb_term = Lt;
@@ -1267,7 +1271,20 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       }
     }
     WPROF(uint64_t wq0 = __builtin_amdgcn_s_memtime(); if constexpr (JOBS) { int z = 0; for (int k = 0; k < CPS; ++k) z += ct[k]; if (__ballot(z == 0x7FFFFFFF)) wg += 1; } uint64_t wq1 = __builtin_amdgcn_s_memtime(); wg += wq1 - wq0;)
-    if (LIST && pass_i == 0 && n && wr != 0) {   // this tick's entries: scattered groups, each lane its own R-contiguous segment
+    if (LIST && !RAFT && CRC && pass_i == 0 && n && wr != 0 && shf >= 0) {
+      // a group kept in shared form (DevPlanes::sh_keep): this tick's entries
+      // are the leader's, held by every replica that accepted them (and, once
+      // it catches up, by a follower that rejected its copy): one shared copy
+      const uint64_t shb = sh_tile(g, P.KP);
+      const uint32_t cs = crc_term_state(tab, w_term);
+      for (int e = 0; e < n; ++e) {
+        const int64_t v = cv_value(w_vb, uint32_t(e), cv_stride(P));
+        const uint32_t so = sh_in_tile(g, uint32_t((w_ph + e) & int(P.kmask)));
+        P.sh_term[shb + so] = w_term;
+        P.sh_value[shb + so] = v;
+        P.sh_crc[shb + so] = crc_value_final(tab, cs, v);
+      }
+    } else if (LIST && pass_i == 0 && n && wr != 0) {   // this tick's entries: scattered groups, each lane its own R-contiguous segment
       const uint64_t tb = ring_tile(g, P.KP, R);
       int32_t* const rt = P.log_term + tb;
       int64_t* const rv = P.log_value + tb;
@@ -1564,7 +1581,10 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     // group, which one lane copying its own group took K dependent passes for
     // (C5 with corrupted copies, K = 512: every rejection copies a group back).
     // The block barrier below orders these stores before the tick's own.
-    for (uint64_t shm = __ballot(valid && (r0 & ROT_SH)); shm; shm &= shm - 1) {
+    // (REF with corrupted copies, DevPlanes::sh_keep: the group keeps its
+    // shared form through the tick — fast_group's `shf` — and nothing is copied)
+    const bool keep = SEM != SEM_RAFT && CRC && P.sh_keep;
+    for (uint64_t shm = __ballot(valid && (r0 & ROT_SH) && !keep); shm; shm &= shm - 1) {
       const int src = int(__builtin_ctzll(shm));
       const uint32_t gs = uint32_t(__shfl(int(g), src));
       const int L = __shfl(ss0.last, src), lo = max(__shfl(shf0, src), L - int(P.K) + 1);
@@ -1589,7 +1609,10 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     // (a group in shared form was taken by the lean kernel at the tick before
     // this one: its heartbeat time is implied, and written back from here)
     const int32_t hbs = (r0 & ROT_SH) ? T.at_tick(T.tick - 1).now : hb0;
-    smeta[t] = m0; sgrot[t] = uint16_t(r0 & ~ROT_SH); sgiso[t] = gi0; shb[t] = hbs; sgss[t] = ss0; sglx[t] = lx0;
+    smeta[t] = m0; sgrot[t] = uint16_t(keep ? r0 : (r0 & ~ROT_SH)); sgiso[t] = gi0; shb[t] = hbs; sgss[t] = ss0;
+    sglx[t] = lx0;
+    const int shk = (keep && (r0 & ROT_SH)) ? shf0 : -1;   // (kept in shared form from this index on)
+    if (P.dbg && shk >= 0) atomicAdd(&P.dbg[7], 1ull);
     sgrota[t] = ra0; sgrotb[t] = rb0; sgsb[t] = sb0; sgsb2[t] = sc0;
     __syncthreads();
     {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
@@ -1613,12 +1636,12 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     if (P.diag & 32u) { __syncthreads(); continue; }
     bool wrote = (P.diag & 64u) ? valid
                                 : fast_group<R, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab,
-                                                                    rw, gw);
+                                                                    rw, gw, shk);
     WPROF(const uint64_t wi2 = __builtin_amdgcn_s_memtime(); wk2 += wi2 - wi1;)
     if (steps > 1) {   // the following tick too, on the staged state (pipelined tick)
       __threadfence_block();   // this step's ring stores, seen by the next step's gathers
       wrote |= fast_group<R, CRC, SEM, true>(P, T.at_tick(T.tick + 1), nx.stats, nx.work, nx.work_tick,
-                                                 nx.work_count, 0, g, tab, rw, gw);
+                                                 nx.work_count, 0, g, tab, rw, gw, shk);
     }
     WPROF(const uint64_t wi3 = __builtin_amdgcn_s_memtime(); wk3 += wi3 - wi2;)
     {   // dirty rows -> the 16-B pieces of the record they touch

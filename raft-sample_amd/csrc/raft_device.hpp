@@ -204,6 +204,13 @@ struct DevPlanes {
   // SH (ROT_SH) enabled: steady groups' entries go to the shared ring (no
   // EXT isolation configured, KP < 2^15; RAFTSTEP_SH=0 turns it off)
   uint32_t sh;
+  // SH kept through rejections (round 6; REF with payload CRC and EXT
+  // corruption, KP = 2K): a follower that rejects a corrupted copy keeps a
+  // log that is a prefix of the leader's, and the shared ring's 2K slots still
+  // hold its whole window while it lags by less than K, so the list kernel
+  // runs the rejection and the catch-up on the shared form without copying
+  // it back (k_fast.hip fast_group, `shf`)
+  uint32_t sh_keep;
   // SH: a group in shared form is taken by the lean (or fused) kernel every
   // tick, so its heartbeat time (hb, every follower's timer reset) is implied:
   // now of the last tick run. Its hb store is skipped; whoever copies the
@@ -647,14 +654,33 @@ __device__ __forceinline__ int sh_copy_back(const DevPlanes& P, uint32_t g, int 
   return hi >= lo ? hi - lo + 1 : 0;
 }
 // ... reading every word from memory, writing the implied heartbeat time hb
-// and clearing the bit (general kernels, one-pass kernel, the engine's flush)
+// and clearing the bit (general kernels, one-pass kernel, the engine's flush).
+// A group kept in shared form through a rejection (DevPlanes::sh_keep) may
+// have explicit rows with one follower lagging: each column gets the shared
+// entries of its own window [max(shf, last_r-K+1), last_r].
 template <int R>
 __device__ __forceinline__ void sh_materialize(const DevPlanes& P, uint32_t g, int32_t hb) {
   if (!P.sh) return;
   const uint32_t rot = at(P.grot, g);
   if (!(rot & ROT_SH)) return;
   const GSeg cw = P.gseg[g];
-  sh_copy_back<R>(P, g, P.gss[g].last, cw.shf, rot, cw.rota, cw.rotb, at(P.gsb, g), cw.sb2);
+  const int sb = at(P.gsb, g);
+  if (at(P.gmeta, g) & M_SSYNC) {
+    sh_copy_back<R>(P, g, P.gss[g].last, cw.shf, rot, cw.rota, cw.rotb, sb, cw.sb2);
+  } else {
+    const uint64_t tb = ring_tile(g, P.KP, R), sb_t = sh_tile(g, P.KP);
+#pragma unroll 1
+    for (int r = 0; r < R; ++r) {
+      const int L = at(P.last, rix<R>(g, r));
+      for (int idx = max(cw.shf, L - int(P.K) + 1); idx <= L; ++idx) {
+        const uint32_t slot = ring_slot(idx, rot, cw.rota, cw.rotb, sb, cw.sb2, P.kmask);
+        const uint32_t so = sh_in_tile(g, slot), o = ring_in_tile(g, R, slot, uint32_t(r));
+        at(P.log_term + tb, o) = at(P.sh_term + sb_t, so);
+        at(P.log_value + tb, o) = at(P.sh_value + sb_t, so);
+        if (P.crc_on) at(P.log_crc + tb, o) = at(P.sh_crc + sb_t, so);
+      }
+    }
+  }
   at(P.hb, g) = hb;   // (implied while shared: now of the last tick it was taken)
   at(P.grot, g) = uint16_t(rot & ~ROT_SH);
 }

@@ -36,7 +36,7 @@ DIAG = {
     "lean_lxs_whole_row": 21, "lean_hwx": 22, "lean_passed": 23, "lean_forced": 24, "lean_switch": 5,
     "lean_sxs": 25, "lean_sxs_stale_in_row": 26, "list_sxs_materialised": 61, "list_sxs_entered": 62,
     "list_stale_moved": 63, "lean_sxs_vx": 27, "list_return_vx": 28, "list_lxs_vx": 29,
-    "lean_sh": 30, "list_sh_copied": 31, "list_sh_entries": 1, "list_lag_catchup": 6,
+    "lean_sh": 30, "list_sh_copied": 31, "list_sh_entries": 1, "list_lag_catchup": 6, "list_sh_kept": 7,
     "list_lanes": 42, "list_deferred": 33, "list_isolation": 34, "list_switch": 37, "list_quiet": 48,
     "list_isolated_leader": 49, "list_ssync": 50, "list_election": 51, "list_first_round": 52,
     "list_return": 53, "list_return_trunc": 54, "list_stale": 55, "list_hwx": 56, "list_three_seg": 57,

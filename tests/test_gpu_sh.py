@@ -134,10 +134,17 @@ def test_copy_back_before_handler_batches_and_views(monkeypatch):
     H.assert_same_state(e.store_state(), o.store_state(), "after tick 30")
 
 
-def test_corrupted_copies_leave_the_shared_form(monkeypatch):
+@pytest.mark.parametrize("keep", ["1", "0"], ids=["kept", "copied_back"])
+def test_corrupted_copies(monkeypatch, keep):
     """C5's shape with EXT corruption: a tick whose copy to a follower is
-    corrupted goes to the list kernel (rejection), which copies the group's
-    shared entries back first."""
+    corrupted goes to the list kernel (rejection: the follower's append
+    skipped, AppendEntries false), and the next tick the follower catches up
+    there. Round 6 (DevPlanes::sh_keep, the default): the group keeps its
+    shared form through both — the rejecting follower's log is a prefix of the
+    leader's and the 2K-slot shared ring still holds its window — so nothing
+    is copied back; RAFTSTEP_SH_KEEP=0: the list kernel copies the group's
+    shared entries back first (round 5's form)."""
+    monkeypatch.setenv("RAFTSTEP_SH_KEEP", keep)
     e, o = _pair(monkeypatch, replicas=5, payload_crc=1, entries_per_tick=8, ring_depth=32,
                  corrupt_per_65536=300)
     e.init_steady(0, 0)
@@ -148,10 +155,14 @@ def test_corrupted_copies_leave_the_shared_form(monkeypatch):
         assert list(e.tick(t, k)) == list(o.tick(t, k)), f"stats of ticks [{t}, {t + k})"
         t += k
     cls = e.diag_read()
-    assert cls["list_sh_copied"] > 0 and cls["lean_sh"] > 0, cls
-    # (round 6) the rejecting follower catches up on the fast path the next
-    # tick: the leader's entries copied from its column by the list kernel
-    assert cls["list_lag_catchup"] > 0, cls
+    print("class counters:", cls)
+    assert cls["lean_sh"] > 0 and cls["list_lag_catchup"] > 0, cls
+    if keep == "1":
+        assert cls["list_sh_kept"] > 0 and cls["list_sh_copied"] == 0, cls
+    else:
+        assert cls["list_sh_copied"] > 0 and cls["list_sh_kept"] == 0, cls
+    # a digest mid-run (kept groups read from the shared ring, lagging ones too)
+    _digests(e, o, f"after tick {t - 1}, before the host view")
     _digests(e, o, f"after tick {t - 1}")
     H.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")
 
