@@ -254,6 +254,7 @@ struct raft_engine {
   // RAFT_CLIENT_STAGED: the caller's client values in HBM, [cv_n][E][G]
   // int64 for ticks [cv_t0, cv_t0 + cv_n) (raft_stage_values; DevPlanes::cv)
   int64_t* cvbuf = nullptr;
+  uint8_t* giso_plane = nullptr;   // DevPlanes::giso (round 6: a dense plane)
   uint64_t cv_cap = 0;          // elements allocated
   int64_t cv_t0 = 0;
   uint32_t cv_n = 0;
@@ -638,13 +639,14 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   A(reinterpret_cast<void**>(&e->P.hb), Gp * 4);
   A(reinterpret_cast<void**>(&e->P.xmatch), R * R * Gp * 4);
   A(reinterpret_cast<void**>(&e->P.gmeta), Gp * 2);
-  A(reinterpret_cast<void**>(&e->P.gseg), Gp * sizeof(GSeg));   // (giso / grota / grotb / gsb2: views, below)
+  A(reinterpret_cast<void**>(&e->P.gseg), Gp * sizeof(GSeg));   // (grota / grotb / gsb2 / gshf: views, below)
+  A(reinterpret_cast<void**>(&e->giso_plane), Gp);               // (DevPlanes::giso)
   A(reinterpret_cast<void**>(&e->P.gss), Gp * sizeof(SsRec));
   A(reinterpret_cast<void**>(&e->P.glx), Gp * sizeof(LxRec));
   A(reinterpret_cast<void**>(&e->P.grot), Gp * 2);
   A(reinterpret_cast<void**>(&e->P.gsb), Gp * 4);
   if (rc == RAFT_OK) {
-    e->P.giso = Strided<uint8_t, 16>{&e->P.gseg->iso};
+    e->P.giso = Strided<uint8_t, 1>{e->giso_plane};
     e->P.grota = Strided<uint16_t, 16>{&e->P.gseg->rota};
     e->P.grotb = Strided<uint16_t, 16>{&e->P.gseg->rotb};
     e->P.gsb2 = Strided<int32_t, 16>{&e->P.gseg->sb2};
@@ -757,6 +759,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   z = z == hipSuccess ? hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(e->P.gmeta), uint16_t(NO_PRIMARY), Gp,
                                            e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gseg, 0, Gp * sizeof(GSeg), e->stream) : z;
+  z = z == hipSuccess ? hipMemsetAsync(e->giso_plane, 0, Gp, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.glst, 0, Gp, e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.gss, 0, Gp * sizeof(SsRec), e->stream) : z;
   z = z == hipSuccess ? hipMemsetAsync(e->P.glx, 0, Gp * sizeof(LxRec), e->stream) : z;
@@ -886,6 +889,7 @@ int store_range(raft_engine* e, uint64_t g0, uint64_t n, raft_state_view* v) {
   if (!rc) rc = d2h(e, meta, e->P.gmeta + g0, n);
   std::vector<GSeg> cold;   // the packed cold words (GSeg), split below
   if (!rc && (v->iso_victim || v->log_term || v->log_value || v->log_crc)) rc = d2h(e, cold, e->P.gseg + g0, n);
+  if (!rc && v->iso_victim) rc = d2h(e, giso, e->giso_plane + g0, n);
 
   if (!rc && raft) rc = rows2d(xn, e->P.xnext);
   const bool logs = v->log_term || v->log_value || v->log_crc;
@@ -907,12 +911,10 @@ int store_range(raft_engine* e, uint64_t g0, uint64_t n, raft_state_view* v) {
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(e->stream));
   if (!cold.empty()) {   // (the packed cold words, copied above, split after the copy completed)
-    giso.resize(n);
     rota.resize(n);
     rotb.resize(n);
     sb2.resize(n);
     for (uint64_t g = 0; g < n; ++g) {
-      giso[g] = cold[g].iso;
       rota[g] = cold[g].rota;
       rotb[g] = cold[g].rotb;
       sb2[g] = cold[g].sb2;
@@ -1134,12 +1136,9 @@ int raft_load_state(raft_engine* e, const raft_state_view* v) {
   if (!rc) rc = h2d(e, e->P.hb, hb);
   if (!rc) rc = h2d(e, e->P.xmatch, xm);
   if (!rc) rc = h2d(e, e->P.gmeta, meta);
-  std::vector<GSeg> cold(Gp);   // loaded rings: rotation 0, one segment; the isolation victims
-  for (uint64_t g = 0; g < Gp; ++g) {
-    cold[g] = GSeg{};
-    cold[g].iso = giso[g];
-  }
+  const std::vector<GSeg> cold(Gp, GSeg{});   // loaded rings: rotation 0, one segment
   if (!rc) rc = h2d(e, e->P.gseg, cold);
+  if (!rc) rc = h2d(e, e->giso_plane, giso);   // the isolation victims
   const std::vector<uint16_t> rot(Gp, 0);
   const std::vector<int32_t> sb0(Gp, 0);
   if (!rc) rc = h2d(e, e->P.grot, rot);
@@ -2070,7 +2069,7 @@ int raft_debug_group_words(raft_engine* e, uint64_t group, int32_t* out, uint32_
   HIPCHK(hipMemcpyAsync(&rot, e->P.grot + group, 2, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipMemcpyAsync(&sb, e->P.gsb + group, 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
-  iso = cw.iso;
+  HIPCHK(hipMemcpy(&iso, e->giso_plane + group, 1, hipMemcpyDeviceToHost));
   rota = cw.rota;
   rotb = cw.rotb;
   sb2 = cw.sb2;

@@ -1,4 +1,5 @@
 // k_fast.hip — the steady-state tick kernel (the metric path).
+#include <cstdlib>
 #include "tick_common.hpp"
 
 namespace raftstep {
@@ -190,7 +191,7 @@ struct WordAcc {
   uint16_t* meta_;
   uint16_t* rot_;
   Cold<uint16_t> rota_;
-  Cold<uint8_t> iso_;
+  std::conditional_t<LDS, uint8_t*, Strided<uint8_t, 1>> iso_;
   int32_t* hb_;
   int32_t* sb_;
   SsRec* ss_;
@@ -1569,7 +1570,7 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       hb0 = at(P.hb, g);
       const GSeg cw = P.gseg[g];   // the cold words, one 16-B load (GSeg)
       ra0 = cw.rota; rb0 = cw.rotb; sc0 = cw.sb2;
-      if (T.iso_p) gi0 = cw.iso;
+      if (T.iso_p) gi0 = at(P.giso, g);
       if (uses_glx(m0)) lx0 = P.glx[g];
       shf0 = cw.shf;
     }
@@ -2353,8 +2354,13 @@ static void launch_list_t(const DevPlanes& P, const Trace& T, unsigned long long
   // blocks measured the same list kernel time on C4 and a 15% slower lean
   // kernel beside it, round 2)
   constexpr uint64_t GPB = 256 / 64 * LIST_LANES;
-  const unsigned blocks =
-      unsigned(std::min<uint64_t>((P.G + GPB - 1) / GPB, resident_blocks(tick_list_kernel<R, CRC, SEM, 256>, 256)));
+  static const unsigned cap = [] {
+    const char* v = std::getenv("RAFTSTEP_LIST_BLOCKS");   // experiment knob: cap the resident grid
+    return v ? unsigned(std::strtoul(v, nullptr, 10)) : 0u;
+  }();
+  uint64_t lim = resident_blocks(tick_list_kernel<R, CRC, SEM, 256>, 256);
+  if (cap) lim = std::min<uint64_t>(lim, cap);
+  const unsigned blocks = unsigned(std::min<uint64_t>((P.G + GPB - 1) / GPB, lim));
   hipExtLaunchKernelGGL(tick_list_kernel<R, CRC, SEM, 256>, dim3(blocks), dim3(256), 0, s, c, d, 0, P, T, stats, work,
                         work_tick, work_count, list, count, next_count, steps, nx);
 }

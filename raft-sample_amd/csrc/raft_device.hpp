@@ -128,7 +128,7 @@ constexpr int STAT_TICK = STAT_SLOTS * NSTAT + STAT_PKS * 8;   // words per tick
 struct __attribute__((aligned(16))) GSeg {
   uint16_t rota, rotb;   // rotation of the previous / older segment
   int32_t sb2;           // first index of the previous segment (0: none older)
-  uint8_t iso;           // EXT leader-isolation victims (nibble per epoch parity: 8 | replica)
+  uint8_t iso_unused;    // (round 5's leader-isolation victims; now the dense DevPlanes::giso plane)
   uint8_t pad[3];
   int32_t shf;           // SH (ROT_SH): the first index whose entries live in the shared ring
 };
@@ -157,7 +157,12 @@ struct DevPlanes {
   int32_t* hwm;        // RAFT mode: [Gp][R] highest LastApplied ever (== last in REF)
   uint16_t* gmeta;     // primary leader id:4 | fault:4 | DEFER | MSYNC | STEADY
   GSeg* gseg;          // [Gp] the packed cold words (GSeg); giso / grota / grotb / gsb2 are views of its fields
-  Strided<uint8_t, 16> giso;    // EXT leader-isolation victims, nibble per epoch parity: 8 | replica (0 = none)
+  // EXT leader-isolation victims, nibble per epoch parity: 8 | replica (0 =
+  // none). Round 6: a dense [Gp] byte plane (it was GSeg::iso): the lean
+  // kernel reads it for every lane with a window active, and a strided
+  // 1-of-16-B read cost each such lane a whole sector (C4's lean kernel
+  // fetched 1.27x its algorithmic bytes)
+  Strided<uint8_t, 1> giso;
   SsRec* gss;          // [Gp] the compressed state of an SSYNC group
   LxRec* glx;          // [Gp] LXS: the cut-off leader's extra entries and the earliest follower deadline
   uint16_t* grot;      // ring rotation of the current segment: entry idx >= gsb sits at slot (idx-1+grot) mod KP
