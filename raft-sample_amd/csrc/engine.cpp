@@ -680,6 +680,8 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   // REF with corrupted copies: the shared form survives a rejection (DevPlanes::sh_keep; KP = 2K above)
   e->P.sh_keep = (e->P.sh && !raft && c.payload_crc && c.corrupt_per_65536 && K >= 2ull * c.ring_depth) ? 1u : 0u;
   if (const char* sk = getenv("RAFTSTEP_SH_KEEP"); sk && atoi(sk) == 0) e->P.sh_keep = 0;
+  e->P.list_sort = 1;
+  if (const char* ls = getenv("RAFTSTEP_LIST_SORT"); ls && atoi(ls) == 0) e->P.list_sort = 0;
   if (e->P.sh) {
     A(reinterpret_cast<void**>(&e->P.sh_term), K * Gp * 4);
     A(reinterpret_cast<void**>(&e->P.sh_value), K * Gp * 8);

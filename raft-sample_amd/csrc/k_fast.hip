@@ -1529,6 +1529,8 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
   __shared__ uint16_t sgrota[LB], sgrotb[LB];
   __shared__ int32_t sgsb[LB], sgsb2[LB];
   __shared__ uint32_t sdm[LB];   // dirty rows, then dirty 16-B pieces, of each lane's record
+  __shared__ uint32_t skey[LB];  // (form key, slot), sorted (P.list_sort)
+  __shared__ int32_t sshk[LB];   // fast_group's `shf` of each slot
   constexpr uint32_t GPB = uint32_t(LB) / 64u * LIST_LANES;   // groups per block and round
   shard_zero(next_count);
   const uint32_t n = shard_prefix(count, pre);
@@ -1615,6 +1617,29 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     const int shk = (keep && (r0 & ROT_SH)) ? shf0 : -1;   // (kept in shared form from this index on)
     if (P.dbg && shk >= 0) atomicAdd(&P.dbg[7], 1ull);
     sgrota[t] = ra0; sgrotb[t] = rb0; sgsb[t] = sb0; sgsb2[t] = sc0;
+    sshk[t] = shk;
+    // the tick runs on slot p of the block's staged groups: with P.list_sort
+    // the slots ordered by the groups' form bits (gmeta above the leader and
+    // fault fields, and whether an isolation record is live), a bitonic sort
+    // of (key, slot) in LDS, so that a wave's lanes take fewer distinct paths
+    // through fast_group; staging and write-back stay by slot (coalesced)
+    uint32_t p = t;
+    if (P.list_sort) {
+      skey[t] = (valid ? ((uint32_t(m0) >> 7) << 1 | (gi0 ? 1u : 0u)) : 0x3FFu) << 8 | t;
+      __syncthreads();
+#pragma unroll 1
+      for (uint32_t k = 2; k <= uint32_t(LB); k <<= 1)
+#pragma unroll 1
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+          const uint32_t x = t ^ j;
+          if (x > t) {
+            const uint32_t a = skey[t], b = skey[x];
+            if ((a > b) == ((t & k) == 0)) { skey[t] = b; skey[x] = a; }
+          }
+          __syncthreads();
+        }
+      p = skey[t] & 0xFFu;
+    }
     __syncthreads();
     {   // coalesced record staging, 16 B per lane and load, RQ loads in flight per lane
       const int4* grec = reinterpret_cast<const int4*>(P.rec);
@@ -1630,23 +1655,27 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
     __syncthreads();
     WPROF(const uint64_t wi1 = __builtin_amdgcn_s_memtime(); wk1 += wi1 - wi0;)
     sdm[t] = 0u;
-    const RowAcc<R, true> rw{&srec[t * RW], 0u, &sdm[t]};
-    const WordAcc<true> gw{&smeta[t], &sgrot[t], &sgrota[t], &sgiso[t], &shb[t], &sgsb[t], &sgss[t], &sgrotb[t],
-                           &sgsb2[t], &sglx[t], g};
+    __syncthreads();
+    const uint32_t gp = sg[p];
+    const bool vp = gp < P.G;
+    const int shp = sshk[p];
+    const RowAcc<R, true> rw{&srec[p * RW], 0u, &sdm[p]};
+    const WordAcc<true> gw{&smeta[p], &sgrot[p], &sgrota[p], &sgiso[p], &shb[p], &sgsb[p], &sgss[p], &sgrotb[p],
+                           &sgsb2[p], &sglx[p], gp};
     // (P.diag, timing only, results wrong: 32 = staging alone, 64 = staging and write-back, no tick)
     if (P.diag & 32u) { __syncthreads(); continue; }
-    bool wrote = (P.diag & 64u) ? valid
-                                : fast_group<R, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, g, tab,
-                                                                    rw, gw, shk);
+    bool wrote = (P.diag & 64u) ? vp
+                                : fast_group<R, CRC, SEM, true>(P, T, stats, work, work_tick, work_count, 0, gp, tab,
+                                                                    rw, gw, shp);
     WPROF(const uint64_t wi2 = __builtin_amdgcn_s_memtime(); wk2 += wi2 - wi1;)
     if (steps > 1) {   // the following tick too, on the staged state (pipelined tick)
       __threadfence_block();   // this step's ring stores, seen by the next step's gathers
       wrote |= fast_group<R, CRC, SEM, true>(P, T.at_tick(T.tick + 1), nx.stats, nx.work, nx.work_tick,
-                                                 nx.work_count, 0, g, tab, rw, gw, shk);
+                                                 nx.work_count, 0, gp, tab, rw, gw, shp);
     }
     WPROF(const uint64_t wi3 = __builtin_amdgcn_s_memtime(); wk3 += wi3 - wi2;)
     {   // dirty rows -> the 16-B pieces of the record they touch
-      const uint32_t rows = (valid && wrote) ? sdm[t] : 0u;
+      const uint32_t rows = (vp && wrote) ? sdm[p] : 0u;
       uint32_t pm = 0;
 #pragma unroll
       for (int k = 0; k < NPL; ++k)
@@ -1654,7 +1683,7 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
           const uint32_t q0 = uint32_t(k * R) / 4u, q1 = uint32_t(k * R + R - 1) / 4u;
           pm |= ((2u << q1) - 1u) & ~((1u << q0) - 1u);
         }
-      sdm[t] = pm;
+      sdm[p] = pm;
     }
     __syncthreads();
     {   // coalesced write-back of the records that may have changed

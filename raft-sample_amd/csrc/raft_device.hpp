@@ -216,6 +216,10 @@ struct DevPlanes {
   // runs the rejection and the catch-up on the shared form without copying
   // it back (k_fast.hip fast_group, `shf`)
   uint32_t sh_keep;
+  // list kernel: each block orders its staged groups by their form bits
+  // before the tick (round 6), so that a wave's lanes run fewer distinct paths
+  // of fast_group (RAFTSTEP_LIST_SORT=0 turns it off)
+  uint32_t list_sort;
   // SH: a group in shared form is taken by the lean (or fused) kernel every
   // tick, so its heartbeat time (hb, every follower's timer reset) is implied:
   // now of the last tick run. Its hb store is skipped; whoever copies the
