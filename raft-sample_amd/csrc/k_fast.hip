@@ -1572,7 +1572,15 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       hb0 = at(P.hb, g);
       const GSeg cw = P.gseg[g];   // the cold words, one 16-B load (GSeg)
       ra0 = cw.rota; rb0 = cw.rotb; sc0 = cw.sb2;
-      if (T.iso_p) gi0 = at(P.giso, g);
+      // giso only where fast_group reads it: leader-isolation mode, a window
+      // of the group active at this tick or (two steps) the next one
+      if (T.iso_p && T.iso_leader) {
+        const uint64_t key = group_key(T.seed, P.gbase + g);
+        uint32_t a0 = 0, a1 = 0, s0 = 0;
+        iso_windows<R>(key, T, &a0, &s0);
+        if (steps > 1) iso_windows<R>(key, T.at_tick(T.tick + 1), &a1, &s0);
+        if (a0 | a1) gi0 = at(P.giso, g);
+      }
       if (uses_glx(m0)) lx0 = P.glx[g];
       shf0 = cw.shf;
     }
