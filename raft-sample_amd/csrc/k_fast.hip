@@ -653,7 +653,12 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     // column by the wave (GetLogsFrom, main.go:357) and the group is in step
     // again. Taken while m > 0, the batch fits the ring (Ll+n-m < K) and this
     // tick has entries; anything else takes the general path as before.
+    // Several followers may lag at once (round 6: two rejections in one tick
+    // were C5V's deferrals, ~130 groups a tick): any number whose catch-up
+    // copies nothing — a group kept in shared form (shf >= 0) whose follower
+    // holds every entry below shf — and at most one whose catch-up is copied (lg).
     int lg = -1;
+    uint32_t lgm = 0;   // the lagging followers
     if (gom) {
 #pragma unroll
       for (int p = 0; p < R; ++p) {
@@ -662,10 +667,14 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           if (!stale) bail |= m[p] != last[p] || m[p] > Ll || ((fresh >> p) & 1u);
           continue;
         }
-        if (!RAFT && CRC && p != c && lg < 0 && n > 0 && m[p] > 0 && m[p] < Ll && m[p] == last[p] &&
+        if (!RAFT && CRC && p != c && n > 0 && m[p] > 0 && m[p] < Ll && m[p] == last[p] &&
             Ll + n - m[p] < int(P.K)) {
-          lg = p;
-          continue;
+          const bool nocopy = shf >= 0 && m[p] + 1 >= shf;
+          if (nocopy || lg < 0) {
+            lgm |= 1u << p;
+            if (!nocopy) lg = p;
+            continue;
+          }
         }
         bail |= (p != c) && m[p] != Ll && !((fresh >> p) & 1u);
         // RAFT: a follower with extra entries or another term takes the general path
@@ -715,13 +724,17 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
                                          cv_stride(P), n, cm);
       }
     }
-    int lg_pt = 0;   // the lagging follower's prevLogTerm: the leader's entry at its MatchIndex
-    if (!RAFT && CRC && gom && !bail && lg >= 0) {
-      const int ml = sel(m, lg);
-      const uint32_t so = ring_slot(ml, GW.rot(), GW.rota(), GW.rotb(), GW.sb(), GW.sb2(), P.kmask);
-      // (a group kept in shared form, shf >= 0: entries from shf on are in the shared ring)
-      lg_pt = (shf >= 0 && ml >= shf) ? ring_ld(P.sh_term + sh_tile(g, P.KP), sh_in_tile(g, so))
-                                      : ring_ld(P.log_term + ring_tile(g, P.KP, R), ring_in_tile(g, R, so, uint32_t(c)));
+    int lg_pt[R];   // each lagging follower's prevLogTerm: the leader's entry at its MatchIndex (one ring read each)
+#pragma unroll
+    for (int p = 0; p < R; ++p) {
+      lg_pt[p] = 0;
+      if (!RAFT && CRC && gom && !bail && ((lgm >> p) & 1u)) {
+        const int ml = m[p];
+        const uint32_t so = ring_slot(ml, GW.rot(), GW.rota(), GW.rotb(), GW.sb(), GW.sb2(), P.kmask);
+        // (a group kept in shared form, shf >= 0: entries from shf on are in the shared ring)
+        lg_pt[p] = (shf >= 0 && ml >= shf) ? ring_ld(P.sh_term + sh_tile(g, P.KP), sh_in_tile(g, so))
+                                           : ring_ld(P.log_term + ring_tile(g, P.KP, R), ring_in_tile(g, R, so, uint32_t(c)));
+      }
     }
     uint32_t okm = 0, cch = 0, mch = 0, ltch = 0;
     if (gom && !bail) {
@@ -729,7 +742,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       for (int p = 0; p < R; ++p) {
         if (p == c || p == xi || p == sr) continue;   // xi: dropped (sender sees false, receiver unchanged)
         const int l = last[p];
-        const bool lgp = !RAFT && CRC && p == lg;
+        const bool lgp = !RAFT && CRC && ((lgm >> p) & 1u);
         const int np = lgp ? Ll + n - l : n;          // len(Logs) of p's AppendEntries
         bool ok;
         if constexpr (RAFT) {
@@ -738,7 +751,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           if ((crcbad >> p) & 1u) bail = true;                    // rejected payload: backoff path
           ok = true;
         } else {
-          const int pi = lgp ? l : prev_idx, pt = lgp ? lg_pt : prev_term;
+          const int pi = lgp ? l : prev_idx, pt = lgp ? lg_pt[p] : prev_term;
           ok = Lt >= term[p];                                     // main.go:129-133
           if (ok && l > 0) {                                      // main.go:135
             if (int64_t(l) + np < pi) ok = false;                 // 137-140
@@ -760,7 +773,8 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
           }
           if (nl != m[p]) { m[p] = nl; mch |= 1u << p; }          // 156 -> 375-377
           okm |= 1u << p;
-          if (lgp) {   // its catch-up: the leader's entries l+1..Ll, copied from the leader's column below
+          if (lgp && p != lg && P.dbg) atomicAdd(&P.dbg[6], 1ull);   // (a catch-up that copies nothing)
+          if (lgp && p == lg) {   // its catch-up: the leader's entries l+1..Ll, copied from the leader's column below
             // (kept in shared form: only those below shf; the rest are the shared ones it now holds too)
             jb_n = max(0, (shf >= 0 ? min(Ll, shf - 1) : Ll) - l);
             jb_from = l + 1;

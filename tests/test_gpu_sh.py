@@ -167,6 +167,30 @@ def test_corrupted_copies(monkeypatch, keep):
     H.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")
 
 
+def test_several_lagging_followers(monkeypatch):
+    """Round 6: with corruption at 3000/65536 per follower and tick, two or
+    more followers of a group reject in the same tick (or one rejects again
+    while it lags) ~1% of group-ticks; in the kept shared form their
+    catch-ups copy nothing, so fast_group takes them all (case (ii) of
+    main.go:353-360 per follower, one prevLogTerm ring read each) instead of
+    deferring the group to the general kernel. Stats of every call, digests
+    and the whole state against the oracle."""
+    e, o = _pair(monkeypatch, replicas=5, payload_crc=1, entries_per_tick=8, ring_depth=32,
+                 corrupt_per_65536=3000)
+    e.init_steady(0, 0)
+    o.init_steady(0, 0)
+    e.diag_enable()
+    t = 1
+    for k in (8, 8, 16):
+        assert list(e.tick(t, k)) == list(o.tick(t, k)), f"stats of ticks [{t}, {t + k})"
+        t += k
+        _digests(e, o, f"after tick {t - 1}")
+    cls = e.diag_read()
+    print("class counters:", cls)
+    assert cls["list_sh_kept"] > 0 and cls["list_lag_catchup"] > 20 * max(1, cls["list_deferred"]), cls
+    H.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")
+
+
 def test_forced_on_under_isolation_churn(monkeypatch):
     """RAFTSTEP_SH=2 (the A/B knob: shared entries under C4's leader-isolation
     churn too, with virtual suffixes and ring segment switches): every group

@@ -30,5 +30,15 @@ e.tick(t, 5)
 t += 5
 e.diag_enable(True)
 e.tick(t, a.ticks)
-c = e.diag_read()
-print(json.dumps({k: v / a.ticks for k, v in sorted(c.items(), key=lambda kv: -kv[1]) if v}, indent=1))
+import ctypes as C  # noqa: E402
+from raftstep import abi  # noqa: E402
+buf = (C.c_uint64 * abi.DIAG_COUNTERS)()
+e.lib.raft_diag_read(e.h, buf, abi.DIAG_COUNTERS)
+names = {i: k for k, i in abi.DIAG.items()}
+# (a DIAG=1 build also counts deferral reasons: list slots 43-47)
+reasons = {43: "defer_reason_not_steady", 44: "defer_reason_iso", 45: "defer_reason_follower_out_of_step",
+           46: "defer_reason_rows_out_of_step", 47: "defer_reason_later"}
+c = {names.get(i, reasons.get(i, f"slot{i}")): int(buf[i]) for i in range(abi.DIAG_COUNTERS)}
+c["general_worklist_note"] = "general_launches counts windows"
+print(json.dumps({k: (v / a.ticks if isinstance(v, int) else v) for k, v in sorted(c.items(), key=lambda kv: str(kv[1])) if v},
+                 indent=1))
