@@ -36,7 +36,15 @@ for w in C2S C4S; do
        --skip 53 --take 20 --out profiles/pmc_C4S_list.json > /dev/null
   fi
 done
-for f in C2_lean C2X_lean C4_lean C4_list C5_lean C2S_lean C4S_lean C4S_list; do
+# C5 with corrupted copies (rejections timed): one lean launch per tick (no split: the list runs)
+if [ -d "$O/pmc_c5v_fetch" ]; then
+  WW=$(python3 -c "import json;print(json.load(open('$B'))['extra_workloads']['C5V']['workload'])")
+  $S --fetch $O/pmc_c5v_fetch --write $O/pmc_c5v_write --kernel tick_lean_kernel --workload "$WW" \
+     --algorithmic-bytes $(($(LB C5V)*1048576)) --skip 5 --take 20 --out profiles/pmc_C5V_lean.json > /dev/null
+  $S --fetch $O/pmc_c5v_fetch --write $O/pmc_c5v_write --kernel tick_list_kernel --workload "$WW" \
+     --skip 5 --take 20 --out profiles/pmc_C5V_list.json > /dev/null
+fi
+for f in C2_lean C2X_lean C4_lean C4_list C5_lean C2S_lean C4S_lean C4S_list C5V_lean C5V_list; do
   [ -f profiles/pmc_$f.json ] || continue
   python3 -c "import json; d=json.load(open('profiles/pmc_$f.json')); print('$f', round(d.get('hbm_bytes_per_tick', d['hbm_bytes_per_launch'])/1e6,1), 'MB/tick', d.get('traffic_over_algorithmic'))"
 done
