@@ -70,6 +70,11 @@ ENV_KNOBS = {
                    "isolation churn too (A/B only: 4x slower on C4; tests/test_gpu_sh.py)",
     "RAFTSTEP_VX": "exact: 0 = no virtual log suffixes (C4's stale leaders' entries stored and copied back at "
                    "their return; tests/test_gpu_fullsize.py, test_gpu_pipeline.py)",
+    "RAFTSTEP_SH_KEEP": "exact: 0 = REF groups with corrupted copies leave the shared form (copied back) instead of "
+                        "keeping it through the rejection (tests/test_gpu_sh.py)",
+    "RAFTSTEP_LIST_SORT": "exact: 0 = the list kernel ticks its staged groups in list order, not form order "
+                          "(whole GPU suite with it on; an A/B knob)",
+    "RAFTSTEP_LIST_BLOCKS": "exact: caps the list kernel's resident grid (A/B knob, round 6: the default grid was best)",
     "RAFTSTEP_DEBUG_WORK": "exact: prints worklist sizes, synchronises (in-line form)",
     "RAFTSTEP_DEBUG_PIPE": "exact: prints the pipeline choice",
     "RAFTSTEP_DEBUG_FAST": "exact: prints class counters after every call (synchronising)",
