@@ -680,6 +680,11 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   // REF with corrupted copies: the shared form survives a rejection (DevPlanes::sh_keep; KP = 2K above)
   e->P.sh_keep = (e->P.sh && !raft && c.payload_crc && c.corrupt_per_65536 && K >= 2ull * c.ring_depth) ? 1u : 0u;
   if (const char* sk = getenv("RAFTSTEP_SH_KEEP"); sk && atoi(sk) == 0) e->P.sh_keep = 0;
+  // the shared ring's slot chunk (sh_in_tile): 16 consecutive slots of a group
+  // contiguous where the list kernel writes whole batches of kept groups
+  // (REF with corrupted copies, E >= 16: C5V); one row per slot otherwise
+  e->P.sh_cs = (e->P.sh_keep && c.entries_per_tick >= 16 && (K & 15u) == 0) ? 4u : 0u;
+  if (const char* cs = getenv("RAFTSTEP_SH_CHUNK"); cs && atoi(cs) == 0) e->P.sh_cs = 0;
   e->P.list_sort = 1;
   if (const char* ls = getenv("RAFTSTEP_LIST_SORT"); ls && atoi(ls) == 0) e->P.list_sort = 0;
   if (e->P.sh) {

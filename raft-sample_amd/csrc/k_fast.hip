@@ -732,7 +732,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
         const int ml = m[p];
         const uint32_t so = ring_slot(ml, GW.rot(), GW.rota(), GW.rotb(), GW.sb(), GW.sb2(), P.kmask);
         // (a group kept in shared form, shf >= 0: entries from shf on are in the shared ring)
-        lg_pt[p] = (shf >= 0 && ml >= shf) ? ring_ld(P.sh_term + sh_tile(g, P.KP), sh_in_tile(g, so))
+        lg_pt[p] = (shf >= 0 && ml >= shf) ? ring_ld(P.sh_term + sh_tile(g, P.KP), sh_in_tile(g, so, P.sh_cs))
                                            : ring_ld(P.log_term + ring_tile(g, P.KP, R), ring_in_tile(g, R, so, uint32_t(c)));
       }
     }
@@ -1286,7 +1286,64 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       }
     }
     WPROF(uint64_t wq0 = __builtin_amdgcn_s_memtime(); if constexpr (JOBS) { int z = 0; for (int k = 0; k < CPS; ++k) z += ct[k]; if (__ballot(z == 0x7FFFFFFF)) wg += 1; } uint64_t wq1 = __builtin_amdgcn_s_memtime(); wg += wq1 - wq0;)
-    if (LIST && !RAFT && CRC && pass_i == 0 && n && wr != 0 && shf >= 0) {
+    // Batches of at least LIST_COOP entries (C5: 64) are written by the whole
+    // wave, one group at a time, one entry per lane: the lane-per-group loop
+    // had each store instruction touch 64 groups' ring tiles (256-512 KB
+    // apart) — 64 address translations per instruction; C5V's list kernel
+    // spent 615K of a step's 650K cycles in those stores (tools/list_prof.py,
+    // profiles/r06/t/). One group's batch spans a few KB of one tile.
+    constexpr int LIST_COOP = 8;
+    const bool coop_w = LIST && pass_i == 0 && n >= LIST_COOP;   // (wave-uniform)
+    const bool kept = !RAFT && CRC && wr != 0 && shf >= 0;
+    if (coop_w) {
+      const int lane = int(threadIdx.x & 63);
+      for (uint64_t bm = __ballot(wr != 0); bm; bm &= bm - 1) {
+        const int src = int(__builtin_ctzll(bm));
+        const uint32_t gs = uint32_t(__shfl(int(g), src));
+        const int ts = __shfl(w_term, src), phs = __shfl(w_ph, src);
+        const uint32_t ws = uint32_t(__shfl(int(wr), src));
+        const bool ks = __shfl(int(kept), src) != 0;
+        const uint64_t vbs = (uint64_t(uint32_t(__shfl(int(uint32_t(w_vb >> 32)), src))) << 32) |
+                             uint32_t(__shfl(int(uint32_t(w_vb)), src));
+        uint32_t cs = 0;
+        if constexpr (CRC) cs = crc_term_state(tab, ts);
+        if (ks) {   // a group kept in shared form: one shared copy (see below)
+          const uint64_t shb = sh_tile(gs, P.KP);
+          for (int e = lane; e < n; e += 64) {
+            const int64_t v = cv_value(vbs, uint32_t(e), cv_stride(P));
+            const uint32_t so = sh_in_tile(gs, uint32_t((phs + e) & int(P.kmask)), P.sh_cs);
+            P.sh_term[shb + so] = ts;
+            P.sh_value[shb + so] = v;
+            if constexpr (CRC) P.sh_crc[shb + so] = crc_value_final(tab, cs, v);
+          }
+        } else {    // its own R-contiguous segment per entry
+          const uint64_t tb = ring_tile(gs, P.KP, R);
+          int32_t* const rt = P.log_term + tb;
+          int64_t* const rv = P.log_value + tb;
+          uint32_t* const rc = CRC ? P.log_crc + tb : nullptr;
+          for (int e = lane; e < n; e += 64) {
+            const int64_t v = cv_value(vbs, uint32_t(e), cv_stride(P));
+            uint32_t stamp = 0;
+            if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
+            const uint32_t o = ring_in_tile(gs, R, uint32_t((phs + e) & int(P.kmask)), 0u);
+            if (ws == (1u << R) - 1u) {
+              fill_segx<LIST, R>(rt + o, ts);
+              fill_segx<LIST, R>(rv + o, v);
+              if constexpr (CRC) fill_segx<LIST, R>(rc + o, stamp);
+            } else {
+#pragma unroll
+              for (int p = 0; p < R; ++p) {
+                if (!((ws >> p) & 1u)) continue;
+                ring_stx<LIST>(rt, o + p, ts);
+                ring_stx<LIST>(rv, o + p, v);
+                if constexpr (CRC) ring_stx<LIST>(rc, o + p, stamp);
+              }
+            }
+          }
+        }
+      }
+      if (wr != 0) df |= 512u;
+    } else if (LIST && pass_i == 0 && n && kept) {
       // a group kept in shared form (DevPlanes::sh_keep): this tick's entries
       // are the leader's, held by every replica that accepted them (and, once
       // it catches up, by a follower that rejected its copy): one shared copy
@@ -1294,7 +1351,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
       const uint32_t cs = crc_term_state(tab, w_term);
       for (int e = 0; e < n; ++e) {
         const int64_t v = cv_value(w_vb, uint32_t(e), cv_stride(P));
-        const uint32_t so = sh_in_tile(g, uint32_t((w_ph + e) & int(P.kmask)));
+        const uint32_t so = sh_in_tile(g, uint32_t((w_ph + e) & int(P.kmask)), P.sh_cs);
         P.sh_term[shb + so] = w_term;
         P.sh_value[shb + so] = v;
         P.sh_crc[shb + so] = crc_value_final(tab, cs, v);
@@ -1619,7 +1676,7 @@ __global__ __launch_bounds__(LB) void tick_list_kernel(DevPlanes P, Trace T, uns
       const uint64_t tb = ring_tile(gs, P.KP, R), shb = sh_tile(gs, P.KP);
       for (int idx = lo + int(lane); idx <= L; idx += 64) {
         const uint32_t slot = ring_slot(idx, rs, ras, rbs, sbs, scs, P.kmask);
-        const uint32_t so = sh_in_tile(gs, slot), o = ring_in_tile(gs, R, slot, 0u);
+        const uint32_t so = sh_in_tile(gs, slot, P.sh_cs), o = ring_in_tile(gs, R, slot, 0u);
         const int32_t tt = at(P.sh_term + shb, so);
         const int64_t vv = at(P.sh_value + shb, so);
         fill_seg<R>(P.log_term + tb + o, tt);
@@ -2086,7 +2143,41 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       k_x[k] = anyx && ((uint32_t(__shfl(xrow ? int(1u << x_r) : 0, src)) >> rr) & 1u) != 0u;
     }
     const uint64_t cvs = cv_stride(P);
-    for (int e = 0; e < n; ++e) {
+    // Shared ring in slot chunks (P.sh_cs > 0, C5V): a chunk of 16 slots x 64
+    // groups is contiguous, group-major inside, so the wave writes it
+    // transposed — element k*64 + lane of the chunk is group (k*64+lane) >> 4's
+    // slot (k*64+lane) & 15 — with that group's term, value stream and CRC
+    // state by shuffle: whole lines, as the row form does for cs = 0. (The
+    // row loop below would write 4 B of a different line per lane and entry.)
+    const bool shx = anysh && P.sh_cs != 0u;   // (wave-uniform)
+    if (shx) {
+      const uint32_t csz = 1u << P.sh_cs;
+      const uint32_t vb_lo = uint32_t(w_vb), vb_hi = uint32_t(w_vb >> 32);
+      for (uint32_t cb = uint32_t(ph) & ~(csz - 1u); cb < uint32_t(ph + n); cb += csz) {
+        for (uint32_t k = 0; k < csz; ++k) {
+          const uint32_t idx = k * 64u + uint32_t(lane);
+          const int gl = int(idx >> P.sh_cs);
+          const uint32_t sl = cb + (idx & (csz - 1u));
+          const int e = int(sl) - ph;
+          const bool on = __shfl(int(wsh), gl) != 0 && e >= 0 && e < n;
+          const int ts = __shfl(w_term, gl);
+          const uint64_t vbg = (uint64_t(uint32_t(__shfl(int(vb_hi), gl))) << 32) | uint32_t(__shfl(int(vb_lo), gl));
+          uint32_t csg = 0;
+          if constexpr (CRC) csg = uint32_t(__shfl(int(cs), gl));
+          const int64_t c0 = int64_t((uint64_t(uint32_t(__shfl(int(uint32_t(uint64_t(cv0) >> 32)), gl))) << 32) |
+                                     uint32_t(__shfl(int(uint32_t(uint64_t(cv0))), gl)));
+          if (on) {
+            const int64_t v = (cvs && e == 0) ? c0 : cv_value(vbg, uint32_t(e), cvs);
+            const uint32_t so = sh_in_tile(uint32_t(gl), sl & P.kmask, P.sh_cs);
+            ring_st(P.sh_term + shb, so, ts);
+            ring_st(P.sh_value + shb, so, v);
+            if constexpr (CRC) ring_st(P.sh_crc + shb, so, crc_value_final(tab, csg, v));
+          }
+        }
+      }
+    }
+    const bool rowloop = anyrow || __ballot(wd || wx) != 0ull || (anysh && !shx);   // (wave-uniform)
+    for (int e = 0; rowloop && e < n; ++e) {
       // (staged values: every leader of the group appends the same request,
       // entry 0 already loaded with the group's words)
       const int64_t v = (cvs && e == 0) ? cv0 : cv_value(w_vb, uint32_t(e), cvs);
@@ -2097,8 +2188,8 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
       int64_t xv = 0;
       if (RAFT && !CRC && x_slot >= 0) xv = cvs ? v : cv_value(x_vb, uint32_t(e), 0u);
       const int xlo = int(uint32_t(uint64_t(xv))), xhi = int(uint32_t(uint64_t(xv) >> 32));
-      if (wsh) {   // SH: one copy, 64 consecutive groups' entries per wave row
-        const uint32_t so = uint32_t((ph + e) & int(P.kmask)) * 64u + uint32_t(lane);
+      if (wsh && !shx) {   // SH: one copy, 64 consecutive groups' entries per wave row
+        const uint32_t so = sh_in_tile(uint32_t(lane), uint32_t((ph + e) & int(P.kmask)), P.sh_cs);
         ring_st(P.sh_term + shb, so, w_term);
         ring_st(P.sh_value + shb, so, v);
         if constexpr (CRC) ring_st(P.sh_crc + shb, so, stamp);
@@ -2289,7 +2380,7 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
         if constexpr (CRC) stamp = crc_value_final(tab, cs, v);
         if (P.sh) {   // (wave-uniform)
           if (take) {
-            const uint32_t so = uint32_t((ph + e) & int(P.kmask)) * 64u + uint32_t(lane);
+            const uint32_t so = sh_in_tile(uint32_t(lane), uint32_t((ph + e) & int(P.kmask)), P.sh_cs);
             ring_st(P.sh_term + shb, so, term);
             ring_st(P.sh_value + shb, so, v);
             if constexpr (CRC) ring_st(P.sh_crc + shb, so, stamp);

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void digest_kernel(DevPlanes P, int raft, uint
         int64_t lv;
         uint32_t lc = 0;
         if (idx >= shf) {
-          const uint32_t so = sh_in_tile(g, slot);
+          const uint32_t so = sh_in_tile(g, slot, P.sh_cs);
           lt = at(P.sh_term + shb, so);
           lv = at(P.sh_value + shb, so);
           if (P.crc_on) lc = at(P.sh_crc + shb, so);

@@ -216,6 +216,7 @@ struct DevPlanes {
   // runs the rejection and the catch-up on the shared form without copying
   // it back (k_fast.hip fast_group, `shf`)
   uint32_t sh_keep;
+  uint32_t sh_cs;      // log2 of the shared ring's slot chunk (sh_in_tile)
   // list kernel: each block orders its staged groups by their form bits
   // before the tick (round 6), so that a wave's lanes run fewer distinct paths
   // of fast_group (RAFTSTEP_LIST_SORT=0 turns it off)
@@ -358,7 +359,16 @@ __device__ __forceinline__ uint32_t ring_in_tile(uint32_t g, uint32_t R, uint32_
 // handler batches). Nothing is regenerated: a flush at any time is exact.
 constexpr uint32_t ROT_SH = 0x8000u;
 __device__ __forceinline__ uint64_t sh_tile(uint32_t g, uint32_t KP) { return uint64_t(g >> 6) * (KP * 64u); }
-__device__ __forceinline__ uint32_t sh_in_tile(uint32_t g, uint32_t slot) { return slot * 64u + (g & 63u); }
+// Inside a tile (64 groups x KP slots) the slots go in chunks of 2^cs
+// (DevPlanes::sh_cs): chunk-major, then group, then the slot in the chunk.
+// cs = 0 (the default): one row of 64 groups per slot, which a wave of 64
+// consecutive groups writes whole. cs = 4 (round 6: REF with corrupted copies
+// and batches of >= 16 entries, C5V): one group's 16 consecutive slots are
+// contiguous, so the list kernel's write of a rejected / catching-up group's
+// batch touches a few lines per plane instead of one line per entry.
+__device__ __forceinline__ uint32_t sh_in_tile(uint32_t g, uint32_t slot, uint32_t cs) {
+  return ((slot >> cs) << (6u + cs)) + ((g & 63u) << cs) + (slot & ((1u << cs) - 1u));
+}
 
 // Addressing: every access is a wave-uniform base (SGPRs: the plane, or a
 // ring tile) plus a 32-bit per-lane byte offset, so the compiler emits
@@ -649,7 +659,7 @@ __device__ __forceinline__ int sh_copy_back(const DevPlanes& P, uint32_t g, int 
   const int lo = max(shf, L - int(P.K) + 1), hi = L;
   for (int idx = lo; idx <= hi; ++idx) {
     const uint32_t slot = ring_slot(idx, rot, rota, rotb, sb, sb2, P.kmask);
-    const uint32_t so = sh_in_tile(g, slot), o = ring_in_tile(g, R, slot, 0u);
+    const uint32_t so = sh_in_tile(g, slot, P.sh_cs), o = ring_in_tile(g, R, slot, 0u);
     const int32_t t = at(P.sh_term + sb_t, so);
     const int64_t v = at(P.sh_value + sb_t, so);
     const uint32_t c = P.crc_on ? at(P.sh_crc + sb_t, so) : 0u;
@@ -683,7 +693,7 @@ __device__ __forceinline__ void sh_materialize(const DevPlanes& P, uint32_t g, i
       const int L = at(P.last, rix<R>(g, r));
       for (int idx = max(cw.shf, L - int(P.K) + 1); idx <= L; ++idx) {
         const uint32_t slot = ring_slot(idx, rot, cw.rota, cw.rotb, sb, cw.sb2, P.kmask);
-        const uint32_t so = sh_in_tile(g, slot), o = ring_in_tile(g, R, slot, uint32_t(r));
+        const uint32_t so = sh_in_tile(g, slot, P.sh_cs), o = ring_in_tile(g, R, slot, uint32_t(r));
         at(P.log_term + tb, o) = at(P.sh_term + sb_t, so);
         at(P.log_value + tb, o) = at(P.sh_value + sb_t, so);
         if (P.crc_on) at(P.log_crc + tb, o) = at(P.sh_crc + sb_t, so);

@@ -167,15 +167,18 @@ def test_corrupted_copies(monkeypatch, keep):
     H.assert_same_state(e.store_state(), o.store_state(), f"after tick {t - 1}")
 
 
-def test_several_lagging_followers(monkeypatch):
+@pytest.mark.parametrize("E,K", [(8, 32), (16, 64)])
+def test_several_lagging_followers(monkeypatch, E, K):
     """Round 6: with corruption at 3000/65536 per follower and tick, two or
     more followers of a group reject in the same tick (or one rejects again
     while it lags) ~1% of group-ticks; in the kept shared form their
     catch-ups copy nothing, so fast_group takes them all (case (ii) of
     main.go:353-360 per follower, one prevLogTerm ring read each) instead of
-    deferring the group to the general kernel. Stats of every call, digests
-    and the whole state against the oracle."""
-    e, o = _pair(monkeypatch, replicas=5, payload_crc=1, entries_per_tick=8, ring_depth=32,
+    deferring the group to the general kernel. E = 16: the shared ring in
+    16-slot chunks (DevPlanes::sh_cs, the list kernel's wave-cooperative batch
+    writes). Stats of every call, digests and the whole state against the
+    oracle."""
+    e, o = _pair(monkeypatch, replicas=5, payload_crc=1, entries_per_tick=E, ring_depth=K,
                  corrupt_per_65536=3000)
     e.init_steady(0, 0)
     o.init_steady(0, 0)

@@ -21,19 +21,30 @@ ap.add_argument("--ticks", type=int, default=20)
 a = ap.parse_args()
 wl = bench.WORKLOADS[a.workload]
 R = wl.get("replicas", 5)
-e = Engine(**bench.engine_kwargs(wl, R, wl["groups"], 0, wl["ring_depth"], wl["entries"], wl["crc"]))
-e.init_new_nodes(0)
-e.tick(0, wl["settle"])
-t = wl["settle"]
-e.tick(t, 5)
-t += 5
+G = wl["groups"]
+e = Engine(**bench.engine_kwargs(wl, R, G, 0, wl["ring_depth"], wl["entries"], wl["crc"]))
+
+
+def run(t, k, **kw):   # (staged workloads: this call's values first)
+    if wl.get("staged"):
+        e.stage_values(t, bench.staged_values(wl["seed"], 0, G, t, k, wl["entries"]))
+    e.tick(t, k, **kw)
+    return t + k
+
+
+if wl.get("init") == "new":
+    e.init_new_nodes(0)
+    t = run(0, wl["settle"])
+else:
+    e.init_steady(0, 0)
+    t = 1
+t = run(t, 5)
 e.profile(3)
-e.tick(t, a.ticks, stats=False)
-t += a.ticks
+t = run(t, a.ticks, stats=False)
 lms, ln = e.profile_read()
 e.profile(0)
 e.diag_enable(True)
-e.tick(t, a.ticks, stats=False)
+t = run(t, a.ticks, stats=False)
 buf = (C.c_uint64 * 72)()
 e.lib.raft_diag_read(e.h, buf, 72)
 d = list(buf)
