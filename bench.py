@@ -74,6 +74,8 @@ ENV_KNOBS = {
                         "keeping it through the rejection (tests/test_gpu_sh.py)",
     "RAFTSTEP_SH_CHUNK": "exact: 0 = the shared ring one row per slot instead of 16-slot chunks where the list "
                          "kernel writes kept groups' batches (REF + corruption, E >= 16; tests/test_gpu_sh.py)",
+    "RAFTSTEP_SHARD_SB": "exact: log2 of the consecutive 256-group blocks sharing a list / worklist shard chunk "
+                         "(default: up to 64; 0 = the round-5 block-interleaved shards; A/B knob)",
     "RAFTSTEP_LIST_SORT": "exact: 0 = the list kernel ticks its staged groups in list order, not form order "
                           "(whole GPU suite with it on; an A/B knob)",
     "RAFTSTEP_LIST_BLOCKS": "exact: caps the list kernel's resident grid (A/B knob, round 6: the default grid was best)",

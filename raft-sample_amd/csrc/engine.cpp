@@ -653,7 +653,15 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
     e->P.gshf = Strided<int32_t, 16>{&e->P.gseg->shf};
   }
   // sharded group lists (raft_device.hpp): NSHARD shards of scap entries
-  const uint64_t scap = ((Gp / 256 + NSHARD - 1) / NSHARD) * 256;
+  // shard chunks (raft_device.hpp shard_home): 2^sb consecutive blocks per
+  // chunk, at most 64 blocks and at least NSHARD chunks over the engine's
+  // blocks; a shard holds its chunks' groups (RAFTSTEP_SHARD_SB: A/B knob)
+  const uint64_t nblk = (Gp + 255) / 256;
+  uint32_t ssb = 0;
+  while (ssb < 6 && (nblk >> (ssb + 1)) >= uint64_t(NSHARD)) ++ssb;
+  if (const char* sv = getenv("RAFTSTEP_SHARD_SB")) ssb = uint32_t(std::min(6, std::max(0, atoi(sv))));
+  const uint64_t nchunk = (nblk + (1ull << ssb) - 1) >> ssb;
+  const uint64_t scap = ((nchunk + NSHARD - 1) / NSHARD) << (ssb + 8);
   for (int q = 0; q < NWORK; ++q) {
     A(reinterpret_cast<void**>(&e->work[q]), NSHARD * scap * 4);
     A(reinterpret_cast<void**>(&e->work_tick[q]), NSHARD * scap * 4);
@@ -716,6 +724,7 @@ int raft_engine_create(const raft_config* cfg, raft_engine** out) {
   }
   e->P.Gp = Gp;
   e->P.scap = uint32_t(scap);
+  e->P.shard_sb = ssb;
   e->P.G = c.groups;
   e->P.gbase = c.group_base;
   e->P.K = c.ring_depth;

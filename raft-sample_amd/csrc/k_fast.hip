@@ -1492,7 +1492,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
   // lane on its group's shard
   if constexpr (LIST) {
     if (bail) {
-      const uint32_t k = shard_home(g);
+      const uint32_t k = shard_home(g, P.shard_sb);
       const uint32_t off = k * P.scap + atomicAdd(&work_count[k * SHARD_STRIDE], 1u);
       work[off] = g;
       work_tick[off] = int32_t(T.tick);
@@ -1501,7 +1501,7 @@ __device__ __forceinline__ bool fast_group(const DevPlanes& P, const Trace& T, u
     __shared__ uint32_t wn[4], wbase;
     const uint64_t bm = __ballot(bail);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t k = blockIdx.x & uint32_t(NSHARD - 1);   // == shard_home(g)
+    const uint32_t k = shard_of_block(blockIdx.x, P.shard_sb);   // == shard_home(g)
     if (lane == 0) wn[wave] = uint32_t(__popcll(bm));
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2254,7 +2254,7 @@ __global__ __launch_bounds__(256) void tick_lean_kernel(DevPlanes P, Trace T, un
   __shared__ uint32_t wn[4], wbase;
   const uint64_t bm = __ballot(pass);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t k = gblk & uint32_t(NSHARD - 1);   // == shard_home(g)
+  const uint32_t k = shard_of_block(gblk, P.shard_sb);   // == shard_home(g)
   if (lane == 0) wn[wave] = uint32_t(__popcll(bm));
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -2428,7 +2428,7 @@ __global__ __launch_bounds__(256) void tick_fused_kernel(DevPlanes P, Trace T, i
   // id only: no list kernel runs in a list-skipping call, and the end-of-call
   // check turns any such entry into RAFT_EINTERNAL before one could)
   if (pass) {
-    const uint32_t k = blockIdx.x & uint32_t(NSHARD - 1);
+    const uint32_t k = shard_of_block(blockIdx.x, P.shard_sb);
     list[k * P.scap + atomicAdd(&count[k * SHARD_STRIDE], 1u)] = g;
   }
 }

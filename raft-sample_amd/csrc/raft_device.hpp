@@ -195,6 +195,7 @@ struct DevPlanes {
   uint32_t dbg_pass;   // test knob (raft_debug_force_pass): the lean kernel passes this group to the list (~0u: none)
   int32_t* rec;        // [Gp][NPL][R] group records holding every per-replica row above (see rix)
   uint32_t scap;       // capacity of one shard of a sharded group list (see below)
+  uint32_t shard_sb;   // log2 of the consecutive 256-group blocks per shard chunk (shard_home)
   uint8_t* glst;       // [Gp] two-step list marks: 1 = passed by the last lean kernel to a list kernel that
                        // also runs this tick for it (the lean kernel leaves the group alone and clears the mark)
   // the lean kernel's record / heartbeat stores are non-temporal when the
@@ -260,7 +261,12 @@ constexpr int NLISTS = 3;
 constexpr int WC_TAKEN = (NWORK + NLISTS) * SHARD_WORDS;
 constexpr int WC_DONE = WC_TAKEN + 8;
 constexpr int WCOUNT_WORDS = WC_TAKEN + SHARD_STRIDE;
-__device__ __forceinline__ uint32_t shard_home(uint32_t g) { return (g >> 8) & uint32_t(NSHARD - 1); }
+// (round 6: 2^sb consecutive blocks share a shard — DevPlanes::shard_sb — so
+// that a shard's entries, appended roughly in dispatch order, are groups of
+// a few neighbouring blocks: the list kernel's wave then works on groups
+// whose records, ring tiles and per-group words are near each other)
+__device__ __forceinline__ uint32_t shard_of_block(uint32_t b, uint32_t sb) { return (b >> sb) & uint32_t(NSHARD - 1); }
+__device__ __forceinline__ uint32_t shard_home(uint32_t g, uint32_t sb) { return shard_of_block(g >> 8, sb); }
 // pre[0..NSHARD] (LDS) = exclusive prefix of the shard counts; returns the total.
 // Block-wide: every thread calls it.
 __device__ __forceinline__ uint32_t shard_prefix(const uint32_t* cnt, uint32_t* pre) {
