@@ -311,6 +311,8 @@ Trace make_trace(const raft_engine* e, int64_t tick) {
   // staged client values: no entry is ever regenerated (entry jobs read the
   // rings instead: the general kernel), whatever the run
   if (e->cfg.client_source == RAFT_CLIENT_STAGED) T.contig_q = ~uint64_t(0);
+  T.n_tick = T.client_entries_slow(tick);
+  T.eb_tick = T.entries_before_slow(tick);
   return T;
 }
 

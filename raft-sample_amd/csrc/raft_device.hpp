@@ -431,19 +431,30 @@ struct Trace {          // per-launch trace parameters (virtual clock + RNG)
   // entries appended from there on are regenerable from the trace RNG
   // (k_fast.hip entry jobs), older ones are not
   uint64_t contig_q;
+  // this tick's client entries and the client entries before it, computed by
+  // the host (make_trace) or at_tick: the 64-bit divisions by `period` they
+  // need were scalar code at the start of every wave (round 6)
+  uint32_t n_tick;
+  uint64_t eb_tick;
+  __host__ __device__ __forceinline__ uint64_t entries_before_slow(int64_t t) const {
+    return period && t > 0 ? uint64_t((t + int64_t(period) - 1) / int64_t(period)) * entries : 0u;
+  }
+  __host__ __device__ __forceinline__ uint32_t client_entries_slow(int64_t t) const {
+    return (period && (t % int64_t(period)) == 0) ? entries : 0u;
+  }
   __device__ __forceinline__ Trace at_tick(int64_t t) const {
     Trace x = *this;
     x.tick = t;
     x.now = int32_t(t * secs);
+    x.n_tick = client_entries_slow(t);
+    x.eb_tick = entries_before_slow(t);
     return x;
   }
-  __device__ __forceinline__ uint32_t client_entries() const {
-    return (period && (tick % int64_t(period)) == 0) ? entries : 0u;
-  }
+  __device__ __forceinline__ uint32_t client_entries() const { return n_tick; }
   // Client entries of all ticks before t (ticks >= 0): the ring phase that
   // keeps every steady group's appends in the same slots (ring_phase()).
   __device__ __forceinline__ uint64_t entries_before(int64_t t) const {
-    return period && t > 0 ? uint64_t((t + int64_t(period) - 1) / int64_t(period)) * entries : 0u;
+    return t == tick ? eb_tick : entries_before_slow(t);
   }
 };
 

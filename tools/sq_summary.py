@@ -13,7 +13,7 @@ for d in sys.argv[1:]:
     for r in csv.DictReader(open(f[0])):
         agg[r["Kernel_Name"].split("(")[0][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, v in agg.items():
-        if "tick" not in k:
+        if "tick" not in k and "probe" not in k:
             continue
         avg = {c: sum(x) / len(x) for c, x in v.items()}
         w = max(avg.get("SQ_WAVES", 1), 1)
